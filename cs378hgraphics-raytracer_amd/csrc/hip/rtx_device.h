@@ -1,0 +1,225 @@
+// rtx_device.h — gfx950 device code for the ray-trace hot path.
+//
+// Per-lane FP64 arithmetic reproduces the reference operation for operation
+// (see rt_math.h for the glm 0.9.8 order); the control structure is the
+// GPU's own:
+//   * iterative two-level BVH traversal with an explicit per-lane stack in
+//     LDS (stack[depth*64 + lane]: conflict-free ds_read/ds_write_b32),
+//   * closest-hit = lexicographic min of (t, DFS rank) — the winner the
+//     reference's "first strict '<' in candidate order" produces
+//     (scene.cpp:157-180, trimesh.cpp:79-95) — with conservative t-pruning,
+//   * shadow rays walk the reference's sorted all-hits list one hit at a
+//     time: next = min (t, object rank, sub-index) > previous key, which is
+//     the order libstdc++ std::sort (insertion sort for <= 16 hits, stable)
+//     gives the list built in candidate order (light.cpp:21-53),
+//   * recursion (RayTracer.cpp:108-174) becomes a per-lane stack of pending
+//     rays carrying their path weight.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include "../common/rt_math.h"
+#include "rtx.h"
+
+namespace rtxd {
+
+using rtm::dvec2;
+using rtm::dvec3;
+using rtm::mk3;
+
+#define RTX_RAY_EPS 0.00000001           // scene/ray.h:136
+#define RTX_EPS32 (0.00000001 / 32)      // util.h:7,9 ZCHK / BTTC
+#define RTX_EPS_BACKUP 0.0000000001      // light.cpp:13
+#define RTX_INF 1.0e308
+#define RTX_MAX_LIGHTS 64
+
+struct DevScene {
+  const RtxNode* snodes;
+  const RtxObject* objs;
+  const RtxMaterial* mats;
+  const RtxMesh* meshes;
+  const RtxNode* mnodes;
+  const RtxFace* faces;
+  const RtxFaceIds* fids;
+  const double* vnormals;
+  const RtxVertexMaterial* vmats;
+  const RtxLight* lights;
+  const RtxTexture* texs;
+  const uint8_t* texels;
+  const double* picks;   // area-light sample positions [light][ss_res][3]
+  int32_t n_snodes, n_objs, n_lights, ss_res;
+  double margin;         // world-space pruning slack
+  double lmargin;        // mesh-local pruning slack
+  double cos45;          // glm::cos(PI / 4) computed on the host (light.cpp:145)
+  double ambient[3];
+  double air_index;      // intensityValue of air's index (material.cpp:17-21)
+};
+
+struct Counters {
+  int64_t camera, secondary, shadow, nodes, objects, tris, shades;
+};
+
+__host__ __device__ __forceinline__ dvec3 ld3(const double* p) { return mk3(p[0], p[1], p[2]); }
+
+// ------------------------------------------------------------------ slab
+// BoundingBox::intersect (bbox.cc:33-70), exact: same divisions, same
+// vd == 0 skip, same per-axis early outs.  Also returns tMin/tMax.
+__device__ __forceinline__ bool slab(const double* bmin, const double* bmax, const dvec3& o, const dvec3& d,
+                                     double& tMinOut, double& tMaxOut) {
+  double tMin = -1.0e308, tMax = 1.0e308;
+#pragma unroll
+  for (int a = 0; a < 3; ++a) {
+    const double vd = rtm::get(d, a);
+    if (vd == 0.0) continue;
+    const double oa = rtm::get(o, a);
+    double t1 = (bmin[a] - oa) / vd;
+    double t2 = (bmax[a] - oa) / vd;
+    if (t1 > t2) {
+      double tt = t1;
+      t1 = t2;
+      t2 = tt;
+    }
+    if (t1 > tMin) tMin = t1;
+    if (t2 < tMax) tMax = t2;
+    if (tMin > tMax) return false;
+    if (tMax < RTX_RAY_EPS) return false;
+  }
+  tMinOut = tMin;
+  tMaxOut = tMax;
+  return true;
+}
+
+// ------------------------------------------------------------------ textures
+// TextureMap::getMappedValue / getPixelAt (material.cpp:84-138)
+__device__ __forceinline__ dvec3 tex_pixel(const DevScene& S, const RtxTexture& t, int x, int y) {
+  if (0 <= x && x < t.width && 0 <= y && y < t.height) {
+    const uint8_t* p = S.texels + t.offset + (size_t(x) + size_t(y) * t.width) * 3;
+    return mk3(double(p[0]), double(p[1]), double(p[2]));
+  }
+  return mk3(0.0, 0.0, 0.0);
+}
+
+__device__ dvec3 tex_lookup(const DevScene& S, int tex, const dvec2& uv) {
+  const RtxTexture t = S.texs[tex];
+  double x = uv.x, y = uv.y;
+  if (0.0 <= x && x <= 1.0 && 0.0 <= y && y <= 1.0) {
+    x *= t.width - 1;
+    y *= t.height - 1;
+    int ix = (int)x, iy = (int)y;
+    x -= ix;
+    y -= iy;
+    dvec3 prows[2];
+#pragma unroll
+    for (int i = 0; i < 2; i++) {
+      dvec3 pl = tex_pixel(S, t, i + ix, 0 + iy);
+      dvec3 pr = tex_pixel(S, t, i + ix, 1 + iy);
+      prows[i] = y * (pr - pl) + pl;
+    }
+    return (x * (prows[1] - prows[0]) + prows[0]) / 255.0;
+  }
+  return mk3(0.0, 1.0, 0.0);
+}
+
+// MaterialParameter::value / intensityValue (material.cpp:140-158)
+__device__ __forceinline__ dvec3 pval(const DevScene& S, const RtxParam& p, const dvec2& uv) {
+  if (p.tex >= 0) return tex_lookup(S, p.tex, uv);
+  return ld3(p.v);
+}
+__device__ __forceinline__ double intensity(const dvec3& v) { return (0.299 * v.x) + (0.587 * v.y) + (0.114 * v.z); }
+
+// A material evaluated at one hit (all parameters looked up once).
+struct EvalMat {
+  dvec3 ke, ka, ks, kd, kr, kt;
+  double sh, index;
+  int flags;
+};
+
+__device__ EvalMat eval_material(const DevScene& S, const RtxMaterial& m, const dvec2& uv) {
+  EvalMat e;
+  e.ke = pval(S, m.p[RTX_P_KE], uv);
+  e.ka = pval(S, m.p[RTX_P_KA], uv);
+  e.ks = pval(S, m.p[RTX_P_KS], uv);
+  e.kd = pval(S, m.p[RTX_P_KD], uv);
+  e.kr = pval(S, m.p[RTX_P_KR], uv);
+  e.kt = pval(S, m.p[RTX_P_KT], uv);
+  const RtxParam& shp = m.p[RTX_P_SHININESS];
+  e.sh = shp.tex >= 0 ? 128.0 * intensity(pval(S, shp, uv)) : intensity(ld3(shp.v));  // material.h:204-209
+  e.index = intensity(pval(S, m.p[RTX_P_INDEX], uv));
+  e.flags = m.flags;
+  return e;
+}
+
+// Interpolated per-vertex material (trimesh.cpp:157-163): Material() +=
+// b_k * M_k.  Decision U2: flags all false.
+__device__ EvalMat eval_vertex_material(const DevScene& S, const RtxMesh& me, const RtxFaceIds& fi,
+                                        const dvec3& bary) {
+  EvalMat e;
+  dvec3 z = mk3(0.0, 0.0, 0.0);
+  e.ke = z; e.ka = z; e.ks = z; e.kd = z; e.kr = z; e.kt = z;
+  dvec3 shv = z, idx = mk3(1.0, 1.0, 1.0);
+  const double bw[3] = {bary.x, bary.y, bary.z};
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    const RtxVertexMaterial& vm = S.vmats[me.vert_off + fi.vi[k]];
+    e.ke += ld3(vm.ke) * bw[k];
+    e.ka += ld3(vm.ka) * bw[k];
+    e.ks += ld3(vm.ks) * bw[k];
+    e.kd += ld3(vm.kd) * bw[k];
+    e.kr += ld3(vm.kr) * bw[k];
+    e.kt += ld3(vm.kt) * bw[k];
+    shv += ld3(vm.shininess) * bw[k];
+    idx += ld3(vm.index) * bw[k];
+  }
+  e.sh = intensity(shv);
+  e.index = intensity(idx);
+  e.flags = 0;
+  return e;
+}
+
+// ------------------------------------------------------------------ resolve helpers
+// Box::computeNormal (Box.cpp:99-108)
+__device__ dvec3 box_normal(const DevScene& S, const RtxMaterial& m, int bestIndex, const dvec2& uv) {
+  dvec3 b = pval(S, m.p[RTX_P_BUMP], uv);
+  if (rtm::length(b) > 0.0001) return rtm::normalize(b - mk3(0.5, 0.5, 0.5));
+  if (bestIndex < 3) return mk3(-double(bestIndex == 0), -double(bestIndex == 1), -double(bestIndex == 2));
+  return mk3(double(bestIndex == 3), double(bestIndex == 4), double(bestIndex == 5));
+}
+
+// ------------------------------------------------------------------ primitives, closest hit
+// TrimeshFace::intersectLocal (trimesh.cpp:119-156) up to the barycentric
+// denominators; the barycentrics are computed for the winner only.
+__device__ __forceinline__ bool tri_hit(const RtxFace& F, const dvec3& p, const dvec3& d, double& tOut) {
+  const dvec3 n = ld3(F.n);
+  double t = rtm::dot(n, d);
+  if (t < RTX_EPS32 && t > -RTX_EPS32) return false;
+  const dvec3 v0 = ld3(F.v0), v1 = ld3(F.v1), v2 = ld3(F.v2);
+  t = rtm::dot(v0 - p, n) / t;
+  if (t < RTX_EPS32) return false;
+  const dvec3 P = rtm::ray_at(p, d, t);
+  if (rtm::dot(rtm::cross(v1 - v0, P - v0), n) < RTX_EPS32) return false;
+  if (rtm::dot(rtm::cross(v2 - v1, P - v1), n) < RTX_EPS32) return false;
+  if (rtm::dot(rtm::cross(v0 - v2, P - v2), n) < RTX_EPS32) return false;
+  const double faceArea = rtm::dot(rtm::cross(v1 - v0, v2 - v0), n);
+  if (faceArea < RTX_EPS32 && faceArea > -RTX_EPS32) return false;
+  tOut = t;
+  return true;
+}
+
+__device__ __forceinline__ dvec3 tri_bary(const RtxFace& F, const dvec3& p, const dvec3& d, double t) {
+  const dvec3 n = ld3(F.n);
+  const dvec3 v0 = ld3(F.v0), v1 = ld3(F.v1), v2 = ld3(F.v2);
+  const dvec3 P = rtm::ray_at(p, d, t);
+  const double faceArea = rtm::dot(rtm::cross(v1 - v0, v2 - v0), n);
+  const double baryU = rtm::dot(rtm::cross(v1 - P, v2 - P), n);
+  const double baryV = rtm::dot(rtm::cross(v2 - P, v0 - P), n);
+  dvec3 b = mk3(baryU / faceArea, baryV / faceArea, 0);
+  b.z = 1 - b.x - b.y;
+  return b;
+}
+
+// Lexicographic key order used by both queries.
+__device__ __forceinline__ bool key_less(double ta, int ra, int sa, double tb, int rb, int sb) {
+  return ta < tb || (ta == tb && (ra < rb || (ra == rb && sa < sb)));
+}
+
+}  // namespace rtxd

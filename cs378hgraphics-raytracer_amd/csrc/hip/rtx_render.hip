@@ -1,0 +1,1608 @@
+// rtx_render.hip — gfx950 render kernels + the C ABI of include/rtx.h.
+//
+// Design:
+//   * ONE traversal loop per wave, shared by every query a lane can have —
+//     closest hit of a camera / reflection / refraction ray, or the next hit
+//     of a shadow ray's ordered walk — so lanes that are at different points
+//     of their sample still traverse together.  The loop is flattened over
+//     the three levels (scene node / object / mesh node): each iteration
+//     processes one unit, the per-lane stack lives in LDS.
+//   * Around it, a per-lane state machine restates trace/traceRay/shade/
+//     srsAttenuation (RayTracer.cpp:35-174, material.cpp:34-69,
+//     light.cpp:16-53): camera ray -> pending-ray stack -> shade light by
+//     light -> shadow walk hit by hit.
+//   * Lanes refill with new samples as soon as they finish (ballot + popc
+//     + mbcnt over a wave-local queue fed 256 samples per atomic), so the
+//     wave stays full; sample colours go to an HBM sample buffer and a
+//     second kernel sums each pixel's samples in the reference's si-major
+//     order (RayTracer.cpp:288-298).
+//   * Adaptive AA (RayTracer.cpp:316-365) runs one pixel per wave with the
+//     region recursion kept wave-uniform.
+#include <hip/hip_runtime.h>
+
+#include <climits>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "rtx_device.h"
+
+using namespace rtxd;
+using rtm::dvec2;
+using rtm::dvec3;
+using rtm::mk3;
+
+#define WG 256
+#define WAVES_PER_WG (WG / 64)
+#define MAX_DEPTH 16               // -r limit of this build
+#define MAX_PENDING (MAX_DEPTH + 2)
+#define MAX_DOF 64
+#define QCHUNK 256                 // samples per queue atomic
+
+#define Q_NONE 0
+#define Q_CLOSEST 1
+#define Q_NEXT 2
+
+// ============================================================ frame parameters
+struct FrameParams {
+  RtxRenderParams P;
+  RtxCamera cam;
+  double offv[MAX_DOF * 3];  // DoF eye offsets (RayTracer.cpp:64-69), host cos/sin
+  int spp;                   // samples per pixel (1 or s^2)
+  int s;                     // s (AA grid)
+  int ppw;                   // pixels per work item
+  int bw, bh;                // pixel block shape of one item
+  int tw, th;                // tile size (whole image if no tiling)
+  int tiles_x, tiles_y;
+  int n_owned;               // owned tiles
+  int items_per_tile;
+  int bx_per_tile;           // blocks per tile row
+  int64_t n_items;           // work items (pixel blocks)
+  int64_t n_samples;         // n_items * ppw * spp  (sample ids)
+};
+
+// Work item -> pixel; out_index is the output slot (packed tile order or
+// (i + j*w) reference order).
+__device__ __forceinline__ bool item_pixel(const FrameParams& F, int64_t item, int pix_in_item, int& i, int& j,
+                                           int64_t& out_index) {
+  const int k = static_cast<int>(item / F.items_per_tile);
+  const int b = static_cast<int>(item % F.items_per_tile);
+  const int tile_id = F.P.tile > 0 ? F.P.shard + k * F.P.nshards : 0;
+  const int tx = tile_id % F.tiles_x, ty = tile_id / F.tiles_x;
+  const int bx = b % F.bx_per_tile, by = b / F.bx_per_tile;
+  const int lx = bx * F.bw + pix_in_item % F.bw;
+  const int ly = by * F.bh + pix_in_item / F.bw;
+  if (lx >= F.tw || ly >= F.th) return false;
+  i = tx * F.tw + lx;
+  j = ty * F.th + ly;
+  if (i >= F.P.width || j >= F.P.height) return false;
+  if (F.P.packed && F.P.tile > 0)
+    out_index = static_cast<int64_t>(k) * F.tw * F.th + static_cast<int64_t>(ly) * F.tw + lx;
+  else
+    out_index = static_cast<int64_t>(i) + static_cast<int64_t>(j) * F.P.width;
+  return true;
+}
+
+__device__ __forceinline__ double radinv2(int n) {  // hammersley x (util.cpp:3-11)
+  double mul = 0.5, result = 0.0;
+  while (n > 0) {
+    result += (n % 2) ? mul : 0;
+    n /= 2;
+    mul /= 2.0;
+  }
+  return result;
+}
+
+// ============================================================ traversal
+// Unified query over the two-level BVH.
+//   Q_CLOSEST: Scene::intersect (scene.cpp:157-180): min over objects of
+//     (t_world, object rank) where each object's t is its own closest hit
+//     (Geometry::intersect + intersectLocal; a trimesh reduces its faces by
+//     (t_local, face rank) first, trimesh.cpp:79-95).
+//   Q_NEXT: the smallest (t_world, object rank, sub) list entry strictly
+//     after (tp, rp, sq) with t_world <= tlimit (Scene::intersectList +
+//     std::sort, light.cpp:25-26).
+// Nodes are skipped only when the exact slab test (bbox.cc:33-70) rejects
+// them or when their entry/exit distance proves that nothing inside can
+// change the answer (margins in DESIGN.md).
+template <bool STATS>
+__device__ __forceinline__ bool traverse(const DevScene& S, const int qmode, const dvec3& P, const dvec3& D,
+                                         const double tp, const int rp, const int sq, const double tlimit,
+                                         double& bt, int& bobj, int& bsub, int* __restrict__ stk, const int lane,
+                                         Counters& C) {
+  const bool closest = qmode == Q_CLOSEST;
+  bt = tlimit;
+  bobj = INT_MAX;
+  bsub = INT_MAX;
+  bool have = false;
+  if (S.n_snodes == 0) return false;
+  const double tlo = closest ? -RTX_INF : tp - S.margin;
+  int sp = 0, node = 0, mode = 0;  // mode: 0 scene node, 1 object, 2 mesh node
+  int oc = 0, oe = 0;
+  // mesh context
+  dvec3 lp = mk3(0, 0, 0), ld = mk3(0, 0, 0);
+  double len = 1.0, mbest = RTX_INF;
+  int moi = 0, mbase = 0, mnoff = 0, mfoff = 0, mface = -1;
+  bool mhave = false;
+  for (;;) {
+    if (mode == 0) {
+      const RtxNode nd = S.snodes[node];
+      if (STATS) C.nodes++;
+      double a, b;
+      bool ok = slab(nd.bmin, nd.bmax, P, D, a, b);
+      if (ok && (a > bt + S.margin || b < tlo)) ok = false;
+      if (ok) {
+        if (nd.count == 0) {
+          stk[sp * 64 + lane] = nd.right;
+          ++sp;
+          node = node + 1;
+        } else {
+          oc = nd.first;
+          oe = nd.first + nd.count;
+          mode = 1;
+        }
+        continue;
+      }
+      if (sp == 0) break;
+      --sp;
+      node = stk[sp * 64 + lane];
+      continue;
+    }
+    if (mode == 1) {
+      const int oi = oc++;
+      const RtxObject& o = S.objs[oi];
+      if (STATS) C.objects++;
+      double a, b;
+      // Geometry::intersect's world-box test (scene.cpp:15) + prune
+      if (slab(o.wmin, o.wmax, P, D, a, b) && !(a > bt + S.margin) && !(b < tlo)) {
+        const dvec3 pos = rtm::xform_point(o.inv, P);
+        dvec3 dir = rtm::xform_point(o.inv, P + D) - pos;
+        const double ln = rtm::length(dir);
+        dir = rtm::normalize(dir);
+        if (o.type == RTX_OBJ_TRIMESH) {
+          const RtxMesh me = S.meshes[o.mesh];
+          if (me.node_count > 0) {
+            lp = pos;
+            ld = dir;
+            len = ln;
+            moi = oi;
+            mbase = sp;
+            mnoff = me.node_off;
+            mfoff = me.face_off;
+            node = me.node_off;
+            mhave = false;
+            mbest = RTX_INF;
+            mface = -1;
+            mode = 2;
+            continue;
+          }
+        } else {
+          // the primitive's intersectLocalList entries, in list order.
+          // Q_CLOSEST keeps the (t, sub)-smallest entry == intersectLocal
+          // (DESIGN.md); Q_NEXT offers every entry to the key filter.
+          double lt = RTX_INF;
+          int ls = -1;
+          auto entry = [&](double t, int sb) {
+            if (closest) {
+              if (ls < 0 || t < lt || (t == lt && sb < ls)) {
+                lt = t;
+                ls = sb;
+              }
+            } else {
+              const double tw = t / ln;
+              if (key_less(tp, rp, sq, tw, oi, sb) && tw <= tlimit && (!have || key_less(tw, oi, sb, bt, bobj, bsub))) {
+                bt = tw;
+                bobj = oi;
+                bsub = sb;
+                have = true;
+              }
+            }
+          };
+          if (o.type == RTX_OBJ_SPHERE) {  // Sphere.cpp:42-72
+            const dvec3 d2 = rtm::normalize(dir);
+            const dvec3 v = -pos;
+            const double bb = rtm::dot(v, d2);
+            double disc = bb * bb - rtm::dot(v, v) + 1;
+            if (!(disc < 0.0)) {
+              disc = sqrt(disc);
+              const double t1 = bb - disc, t2 = bb + disc;
+              if (t1 > RTX_RAY_EPS) entry(t1, 0);
+              if (t2 > RTX_RAY_EPS) entry(t2, 1);
+            }
+          } else if (o.type == RTX_OBJ_BOX) {  // Box.cpp:65-97
+            for (int it = 0; it < 6; it++) {
+              const int mod0 = it % 3;
+              const double dm = rtm::get(dir, mod0);
+              if (dm == 0) continue;
+              const double t = ((it / 3) - 0.5 - rtm::get(pos, mod0)) / dm;
+              if (t < RTX_RAY_EPS) continue;
+              const int mod1 = (it + 1) % 3, mod2 = (it + 2) % 3;
+              const double x = rtm::get(pos, mod1) + t * rtm::get(dir, mod1);
+              const double y = rtm::get(pos, mod2) + t * rtm::get(dir, mod2);
+              if (x <= 0.5 && x >= -0.5 && y <= 0.5 && y >= -0.5) entry(t, it);
+            }
+          } else if (o.type == RTX_OBJ_CYLINDER) {  // Cylinder.cpp:155-263
+            const double pz = pos.z, dz = dir.z;
+            if (!(0.0 == dz)) {
+              double t1, t2;
+              if (dz > 0.0) {
+                t1 = (-pz) / dz;
+                t2 = (1.0 - pz) / dz;
+              } else {
+                t1 = (1.0 - pz) / dz;
+                t2 = (-pz) / dz;
+              }
+              if (t1 >= RTX_RAY_EPS) {
+                const dvec3 q = rtm::ray_at(pos, dir, t1);
+                if ((q.x * q.x + q.y * q.y) <= 1.0) entry(t1, 0);
+              }
+              if (t2 >= RTX_RAY_EPS) {
+                const dvec3 q = rtm::ray_at(pos, dir, t2);
+                if ((q.x * q.x + q.y * q.y) <= 1.0) entry(t2, 1);
+              }
+            }
+            const double x0 = pos.x, y0 = pos.y, x1 = dir.x, y1 = dir.y;
+            const double aa = x1 * x1 + y1 * y1;
+            const double bb = 2.0 * (x0 * x1 + y0 * y1);
+            const double cc = x0 * x0 + y0 * y0 - 1.0;
+            if (!(0.0 == aa)) {
+              double disc = bb * bb - 4.0 * aa * cc;
+              if (!(disc < 0.0)) {
+                disc = sqrt(disc);
+                const double t1 = (-bb - disc) / (2.0 * aa);
+                const double t2 = (-bb + disc) / (2.0 * aa);
+                if (t1 > RTX_RAY_EPS) {
+                  const double z = rtm::ray_at(pos, dir, t1).z;
+                  if (z >= 0.0 && z <= 1.0) entry(t1, 2);
+                }
+                if (t2 > RTX_RAY_EPS) {
+                  const double z = rtm::ray_at(pos, dir, t2).z;
+                  if (z >= 0.0 && z <= 1.0) entry(t2, 3);
+                }
+              }
+            }
+          } else if (o.type == RTX_OBJ_SQUARE) {  // Square.cpp:9-51
+            if (!(dir.z == 0.0)) {
+              const double t = -pos.z / dir.z;
+              if (!(t <= RTX_RAY_EPS)) {
+                const dvec3 Q = rtm::ray_at(pos, dir, t);
+                if (!(Q.x < -0.5 || Q.x > 0.5) && !(Q.y < -0.5 || Q.y > 0.5)) entry(t, 0);
+              }
+            }
+          }
+          if (closest && ls >= 0) {
+            const double tw = lt / ln;
+            if (!have || tw < bt || (tw == bt && oi < bobj)) {
+              bt = tw;
+              bobj = oi;
+              bsub = ls;
+              have = true;
+            }
+          }
+        }
+      }
+      if (oc == oe) {
+        if (sp == 0) break;
+        --sp;
+        node = stk[sp * 64 + lane];
+        mode = 0;
+      }
+      continue;
+    }
+    // mode == 2: mesh node (local frame of object moi)
+    {
+      const RtxNode m = S.mnodes[node];
+      if (STATS) C.nodes++;
+      double a, b;
+      bool ok = slab(m.bmin, m.bmax, lp, ld, a, b);
+      const double whi = (bt + S.margin) * len * (1.0 + 1e-12);
+      double hi = whi;
+      if (closest && mhave) hi = rtm::gmin(hi, mbest + S.lmargin);
+      const double lo = closest ? -RTX_INF : tlo * len * (1.0 - 1e-12) - S.lmargin;
+      if (ok && (a > hi || b < lo)) ok = false;
+      if (ok && m.count == 0) {
+        stk[sp * 64 + lane] = mnoff + m.right;
+        ++sp;
+        node = node + 1;
+        continue;
+      }
+      if (ok) {
+        for (int f = m.first; f < m.first + m.count; ++f) {
+          if (STATS) C.tris++;
+          double tf;
+          if (tri_hit(S.faces[mfoff + f], lp, ld, tf)) {
+            if (closest) {
+              if (!mhave || tf < mbest || (tf == mbest && f < mface)) {
+                mbest = tf;
+                mface = f;
+                mhave = true;
+              }
+            } else {
+              const double tw = tf / len;
+              if (key_less(tp, rp, sq, tw, moi, f) && tw <= tlimit &&
+                  (!have || key_less(tw, moi, f, bt, bobj, bsub))) {
+                bt = tw;
+                bobj = moi;
+                bsub = f;
+                have = true;
+              }
+            }
+          }
+        }
+      }
+      if (sp > mbase) {
+        --sp;
+        node = stk[sp * 64 + lane];
+        continue;
+      }
+      // mesh finished: Trimesh::intersectLocal's result enters Scene::intersect
+      if (closest && mhave) {
+        const double tw = mbest / len;
+        if (!have || tw < bt || (tw == bt && moi < bobj)) {
+          bt = tw;
+          bobj = moi;
+          bsub = mface;
+          have = true;
+        }
+      }
+      if (oc < oe) {
+        mode = 1;
+      } else {
+        if (sp == 0) break;
+        --sp;
+        node = stk[sp * 64 + lane];
+        mode = 0;
+      }
+    }
+  }
+  return have;
+}
+
+// Recompute the winning entry's local quantities (deterministic: same
+// operations as the traversal) and resolve the isect the reference returns:
+// world normal (scene.cpp:31-33), uv and material.
+struct Resolved {
+  dvec3 N;
+  EvalMat m;
+};
+
+__device__ Resolved resolve_hit(const DevScene& S, const dvec3& P, const dvec3& D, int oi, int sub,
+                                int* rec_face, int* rec_mleaf) {
+  Resolved r;
+  const RtxObject& o = S.objs[oi];
+  const RtxMaterial& mat = S.mats[o.material];
+  const dvec3 pos = rtm::xform_point(o.inv, P);
+  dvec3 dir = rtm::xform_point(o.inv, P + D) - pos;
+  dir = rtm::normalize(dir);
+  dvec3 nl = mk3(0.0, 0.0, 1.0);
+  dvec2 uv = rtm::mk2(0.0, 0.0);
+  if (rec_face) {
+    *rec_face = -1;
+    *rec_mleaf = -1;
+  }
+  if (o.type == RTX_OBJ_TRIMESH) {
+    const RtxMesh me = S.meshes[o.mesh];
+    const RtxFace F = S.faces[me.face_off + sub];
+    const RtxFaceIds fi = S.fids[me.face_off + sub];
+    double tl = 0.0;
+    tri_hit(F, pos, dir, tl);
+    const dvec3 bary = tri_bary(F, pos, dir, tl);
+    if (me.has_normals) {  // trimesh.cpp:166-172
+      const dvec3 n0 = ld3(S.vnormals + size_t(me.vert_off + fi.vi[0]) * 3);
+      const dvec3 n1 = ld3(S.vnormals + size_t(me.vert_off + fi.vi[1]) * 3);
+      const dvec3 n2 = ld3(S.vnormals + size_t(me.vert_off + fi.vi[2]) * 3);
+      const double mm[9] = {n0.x, n0.y, n0.z, n1.x, n1.y, n1.z, n2.x, n2.y, n2.z};
+      nl = rtm::normalize(rtm::mat3_mul(mm, bary));
+    } else {
+      nl = ld3(F.n);
+    }
+    r.m = me.has_vmats ? eval_vertex_material(S, me, fi, bary) : eval_material(S, mat, uv);
+    if (rec_face) {
+      *rec_face = fi.orig_id;
+      *rec_mleaf = fi.leaf;
+    }
+  } else {
+    if (o.type == RTX_OBJ_SPHERE) {
+      const dvec3 d2 = rtm::normalize(dir);
+      const dvec3 v = -pos;
+      const double bb = rtm::dot(v, d2);
+      const double disc = sqrt(bb * bb - rtm::dot(v, v) + 1);
+      const double t = sub == 0 ? bb - disc : bb + disc;
+      nl = rtm::normalize(rtm::ray_at(pos, d2, t));
+    } else if (o.type == RTX_OBJ_BOX) {
+      const int it = sub, mod0 = it % 3;
+      const double t = ((it / 3) - 0.5 - rtm::get(pos, mod0)) / rtm::get(dir, mod0);
+      const dvec3 ip = rtm::ray_at(pos, dir, t);
+      const int i1 = (it + 1) % 3, i2 = (it + 2) % 3;
+      const int lo = i1 < i2 ? i1 : i2, hi = i1 < i2 ? i2 : i1;
+      uv = (it < 3) ? rtm::mk2(0.5 - rtm::get(ip, lo), 0.5 + rtm::get(ip, hi))
+                    : rtm::mk2(0.5 + rtm::get(ip, lo), 0.5 + rtm::get(ip, hi));
+      nl = box_normal(S, mat, it, uv);
+    } else if (o.type == RTX_OBJ_CYLINDER) {
+      const double dz = dir.z;
+      if (sub == 0) {
+        nl = dz > 0.0 ? mk3(0.0, 0.0, -1.0) : mk3(0.0, 0.0, 1.0);
+      } else if (sub == 1) {
+        nl = dz > 0.0 ? mk3(0.0, 0.0, 1.0) : mk3(0.0, 0.0, -1.0);
+      } else {
+        const double x0 = pos.x, y0 = pos.y, x1 = dir.x, y1 = dir.y;
+        const double aa = x1 * x1 + y1 * y1;
+        const double bb = 2.0 * (x0 * x1 + y0 * y1);
+        const double cc = x0 * x0 + y0 * y0 - 1.0;
+        const double disc = sqrt(bb * bb - 4.0 * aa * cc);
+        const double t = sub == 2 ? (-bb - disc) / (2.0 * aa) : (-bb + disc) / (2.0 * aa);
+        const dvec3 Q = rtm::ray_at(pos, dir, t);
+        nl = rtm::normalize(mk3(Q.x, Q.y, 0.0));
+      }
+    } else if (o.type == RTX_OBJ_SQUARE) {
+      const double t = -pos.z / dir.z;
+      const dvec3 Q = rtm::ray_at(pos, dir, t);
+      nl = dir.z > 0.0 ? mk3(0.0, 0.0, -1.0) : mk3(0.0, 0.0, 1.0);
+      uv = rtm::mk2(Q.x + 0.5, Q.y + 0.5);
+    }
+    r.m = eval_material(S, mat, uv);
+  }
+  r.N = rtm::normalize(rtm::mat3_mul(o.normi, nl));
+  return r;
+}
+
+// ============================================================ lights
+__device__ __forceinline__ dvec3 light_dir(const RtxLight& L, const dvec3& P) {
+  if (L.type == RTX_LIGHT_DIRECTIONAL) return -ld3(L.orient);  // light.cpp:59
+  return rtm::normalize(ld3(L.pos) - P);                       // light.cpp:73
+}
+
+__device__ __forceinline__ double light_dist_atten(const RtxLight& L, const dvec3& P) {
+  if (L.type == RTX_LIGHT_DIRECTIONAL) return 1.0;  // light.cpp:56
+  const double d = rtm::distance(ld3(L.pos), P);    // light.cpp:61-64 (float terms promoted)
+  return rtm::gclamp(1.0 / (L.atten[0] + L.atten[1] * d + L.atten[2] * d * d), 0.0, 1.0);
+}
+
+// ============================================================ lane state machine
+enum { ST_IDLE = 0, ST_CAM, ST_POP, ST_HIT, ST_LIGHT, ST_SRS, ST_WALK };
+
+struct Pending {
+  dvec3 p, d, W, ktf;
+  int depth, kind;  // kind 0 camera, 1 reflection, 2 refraction
+};
+
+template <bool STATS, bool ADAPTIVE>
+__global__ void __launch_bounds__(WG) render_kernel(DevScene S, const FrameParams* __restrict__ Fp,
+                                                     unsigned long long* __restrict__ work,
+                                                     double* __restrict__ sbuf, RtxHitRecord* __restrict__ hits,
+                                                     uint8_t* __restrict__ rgb8, double* __restrict__ rgbf,
+                                                     unsigned long long* __restrict__ stats, int stack_cap,
+                                                     double* __restrict__ pbuf, int pend_cap) {
+  extern __shared__ double smem[];
+  const FrameParams& F = *Fp;
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int cslots = ADAPTIVE ? (F.spp > 64 ? F.spp : 64) : 0;
+  const int fslots = ADAPTIVE ? 16 * 8 : 0;  // adaptive region frames (8 doubles each)
+  double* colbuf = smem + static_cast<size_t>(wave) * (cslots * 3 + fslots + stack_cap * 32);
+  double* frbuf = colbuf + cslots * 3;
+  int* stk = reinterpret_cast<int*>(frbuf + fslots);
+  // per-lane pending-ray stack in HBM, field-major so a wave's accesses of
+  // one field are contiguous: entry e, field f of lane g at
+  // pbuf[(e * 13 + f) * nlanes + g]
+  const size_t nlanes = static_cast<size_t>(gridDim.x) * WG;
+  const size_t glane = static_cast<size_t>(blockIdx.x) * WG + threadIdx.x;
+  auto push = [&](int& tp, const dvec3& p, const dvec3& d, const dvec3& w, const dvec3& k, int depth, int kind) {
+    double* b = pbuf + static_cast<size_t>(tp) * 13 * nlanes + glane;
+    b[0 * nlanes] = p.x; b[1 * nlanes] = p.y; b[2 * nlanes] = p.z;
+    b[3 * nlanes] = d.x; b[4 * nlanes] = d.y; b[5 * nlanes] = d.z;
+    b[6 * nlanes] = w.x; b[7 * nlanes] = w.y; b[8 * nlanes] = w.z;
+    b[9 * nlanes] = k.x; b[10 * nlanes] = k.y; b[11 * nlanes] = k.z;
+    b[12 * nlanes] = static_cast<double>(depth * 4 + kind);
+    ++tp;
+  };
+  Counters C = {0, 0, 0, 0, 0, 0, 0};
+  const RtxRenderParams& P = F.P;
+  const double aterm = P.aterm_thresh;
+  const int ncam = P.dof ? P.dof_div + 1 : 1;
+
+  // ---- lane state (kept small: everything recomputable is recomputed)
+  int st = ST_IDLE;
+  int sample_slot = -1;  // sample-buffer / hit-record slot (regular) or k (adaptive)
+  bool rec_on = false;
+  double sx = 0, sy = 0;
+  int pass = 0, camk = 0, nrays = 0;
+  dvec3 acc = mk3(0, 0, 0);  // sum over camera rays of W * colour
+  int top = 0;
+  dvec3 rp = mk3(0, 0, 0), rd = mk3(0, 0, 0), W = mk3(0, 0, 0);
+  int rdepth = 0, rkind = 0;
+  bool first_query = false;
+  // shading of the current hit (re-resolved from (sobj, ssub) when needed)
+  double st_t = 0;
+  int sobj = 0, ssub = 0;
+  dvec3 N = mk3(0, 0, 0), i_out = mk3(0, 0, 0), dscomp = mk3(0, 0, 0);
+  dvec3 m_kd = mk3(0, 0, 0), m_ks = mk3(0, 0, 0);
+  double m_sh = 0, dattn = 0;
+  int m_flags = 0, li = 0, pick = 0;
+  dvec3 area_sum = mk3(0, 0, 0);
+  // shadow walk
+  dvec3 sdir = mk3(0, 0, 0), wpos = mk3(0, 0, 0), sattn = mk3(0, 0, 0);
+  double last_t = 0;
+  // query
+  int qmode = Q_NONE;
+  double qtp = 0;
+  int qrp = 0, qsq = 0;
+  double bt = 0;
+  int bobj = 0, bsub = 0;
+  bool bhave = false;
+
+  // ---- wave-uniform scheduler state
+  unsigned long long qnext = 0, qend = 0;
+  bool exhausted = false;
+  // adaptive
+  // region frames live in LDS (wave-uniform): frbuf[f*8 + {x1,x2,y1,y2,ax,ay,az,child}]
+  int fsp = 0, abase = 0;
+  bool atop = false;
+  int64_t apix_out = 0;
+  const int an = F.spp;
+
+  for (;;) {
+    // ------------------------------------------------ scheduling
+    if (!ADAPTIVE) {
+      unsigned long long idle = __ballot(st == ST_IDLE);
+      while (idle != 0ull) {
+        if (qnext >= qend) {
+          if (exhausted) break;
+          unsigned long long base = 0;
+          if (lane == 0) base = atomicAdd(work, static_cast<unsigned long long>(QCHUNK));
+          base = __shfl(base, 0);
+          if (base >= static_cast<unsigned long long>(F.n_samples)) {
+            exhausted = true;
+            break;
+          }
+          qnext = base;
+          qend = base + QCHUNK;
+          if (qend > static_cast<unsigned long long>(F.n_samples)) qend = F.n_samples;
+        }
+        const unsigned int rank = __builtin_amdgcn_mbcnt_hi(static_cast<unsigned int>(idle >> 32),
+                                                            __builtin_amdgcn_mbcnt_lo(static_cast<unsigned int>(idle), 0u));
+        const unsigned long long avail = qend - qnext;
+        const unsigned int nidle = __popcll(idle);
+        const unsigned int take = avail < nidle ? static_cast<unsigned int>(avail) : nidle;
+        if (st == ST_IDLE && rank < take) {
+          const int64_t sid = static_cast<int64_t>(qnext + rank);
+          const int64_t item = sid / (F.ppw * F.spp);
+          const int slot = static_cast<int>(sid % (F.ppw * F.spp));
+          const int pix = slot / F.spp, smp = slot % F.spp;
+          int i, j;
+          int64_t oidx;
+          if (item_pixel(F, item, pix, i, j, oidx)) {
+            int pi = i, pj = j;
+            double ssx = 1.0, ssy = 1.0;
+            if (P.aa_mode != RTX_AA_NONE) {  // tracePixel(i*s + si, j*s + sj)
+              pi = i * F.s + smp / F.s;
+              pj = j * F.s + smp % F.s;
+              ssx = F.s;
+              ssy = F.s;
+            }
+            // tracePixel (RayTracer.cpp:87-88)
+            sx = double(pi) / (double(P.width) * ssx);
+            sy = double(pj) / (double(P.height) * ssy);
+            sample_slot = static_cast<int>(oidx * F.spp + smp);
+            rec_on = hits != nullptr;
+            pass = 0;
+            camk = 0;
+            nrays = 0;
+            acc = mk3(0, 0, 0);
+            st = ST_CAM;
+          }
+          // out-of-image slots stay idle and are simply consumed
+        }
+        qnext += take;
+        idle = __ballot(st == ST_IDLE);
+        if (take == 0) break;
+        if (qnext < qend) break;  // every idle lane got work (or was consumed)
+      }
+    } else {
+      // adaptive: one pixel per wave; all lanes idle => chunk finished.
+      // Frames f: frbuf[f*8 + 0..3] = x1, x2, y1, y2; [4..6] = acc; [7] = child
+      if (__ballot(st != ST_IDLE) == 0ull) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        auto facc = [&](int f) { return mk3(frbuf[f * 8 + 4], frbuf[f * 8 + 5], frbuf[f * 8 + 6]); };
+        auto set_acc = [&](int f, const dvec3& a) {
+          frbuf[f * 8 + 4] = a.x;
+          frbuf[f * 8 + 5] = a.y;
+          frbuf[f * 8 + 6] = a.z;
+        };
+        auto set_frame = [&](int f, double x1, double x2, double y1, double y2) {
+          frbuf[f * 8 + 0] = x1;
+          frbuf[f * 8 + 1] = x2;
+          frbuf[f * 8 + 2] = y1;
+          frbuf[f * 8 + 3] = y2;
+          set_acc(f, mk3(0.0, 0.0, 0.0));
+          frbuf[f * 8 + 7] = -1.0;
+        };
+        // pop frame fsp-1 with value mu into its parent (adaptaa's `mu += subval`)
+        auto finish = [&](const dvec3& mu) {
+          --fsp;
+          if (fsp > 0) {
+            set_acc(fsp - 1, facc(fsp - 1) + mu);
+            frbuf[(fsp - 1) * 8 + 7] += 1.0;
+          } else {
+            acc = mu;  // pixel value
+          }
+        };
+        bool need_new_pixel = fsp == 0;
+        if (fsp > 0 && abase >= 0) {
+          const int nxt = abase + 64;
+          abase = nxt < an ? nxt : -1;  // -1: region samples complete
+        }
+        while (fsp > 0 && abase < 0) {
+          const int f = fsp - 1;
+          const int child = static_cast<int>(frbuf[f * 8 + 7]);
+          if (child < 0) {
+            // region statistics (RayTracer.cpp:337-347)
+            dvec3 mu = mk3(0.0, 0.0, 0.0), sd = mk3(0.0, 0.0, 0.0);
+            for (int k = 0; k < an; ++k) mu += mk3(colbuf[k * 3 + 0], colbuf[k * 3 + 1], colbuf[k * 3 + 2]);
+            mu *= (1.0 / (an));
+            for (int k = 0; k < an; ++k) {
+              const dvec3 s_c = mk3(colbuf[k * 3 + 0], colbuf[k * 3 + 1], colbuf[k * 3 + 2]);
+              sd += mk3(pow(fabs(s_c.x - mu.x), 2.0), pow(fabs(s_c.y - mu.y), 2.0), pow(fabs(s_c.z - mu.z), 2.0));
+            }
+            sd *= (1.0 / (an - 1));
+            if (rtm::length(sd) > P.aa_thresh && fsp < 16) {
+              set_acc(f, mk3(0.0, 0.0, 0.0));
+              frbuf[f * 8 + 7] = 0.0;
+            } else {
+              finish(mu);
+            }
+            continue;
+          }
+          if (child < 4) {
+            const double x1 = frbuf[f * 8 + 0], x2 = frbuf[f * 8 + 1], y1 = frbuf[f * 8 + 2], y2 = frbuf[f * 8 + 3];
+            const double xs[3] = {x1, (x1 + x2) / 2.0, x2};
+            const double ys[3] = {y1, (y1 + y2) / 2.0, y2};
+            const int a = child / 2, b = child % 2;
+            const double nx1 = a == 0 ? xs[0] : xs[1], nx2 = a == 0 ? xs[1] : xs[2];
+            const double ny1 = b == 0 ? ys[0] : ys[1], ny2 = b == 0 ? ys[1] : ys[2];
+            if (nx1 + 0.0001 >= nx2 || ny1 + 0.0001 >= ny2) {  // U8: the subregion contributes 0
+              set_acc(f, facc(f) + mk3(0.0, 0.0, 0.0));
+              frbuf[f * 8 + 7] += 1.0;
+              continue;
+            }
+            set_frame(fsp, nx1, nx2, ny1, ny2);
+            ++fsp;
+            abase = 0;
+            atop = false;
+          } else {
+            dvec3 mu = facc(f);
+            mu *= (1.0 / 4.0);
+            finish(mu);
+          }
+        }
+        if (fsp == 0 && !need_new_pixel) {
+          if (lane == 0) {  // setPixel (RayTracer.cpp:388-394)
+            if (rgb8) {
+              rgb8[apix_out * 3 + 0] = (uint8_t)(int)(255.0 * acc.x);
+              rgb8[apix_out * 3 + 1] = (uint8_t)(int)(255.0 * acc.y);
+              rgb8[apix_out * 3 + 2] = (uint8_t)(int)(255.0 * acc.z);
+            }
+            if (rgbf) {
+              rgbf[apix_out * 3 + 0] = acc.x;
+              rgbf[apix_out * 3 + 1] = acc.y;
+              rgbf[apix_out * 3 + 2] = acc.z;
+            }
+          }
+          need_new_pixel = true;
+        }
+        while (need_new_pixel) {
+          unsigned long long item = 0;
+          if (lane == 0) item = atomicAdd(work, 1ull);
+          item = __shfl(item, 0);
+          if (item >= static_cast<unsigned long long>(F.n_items)) {
+            exhausted = true;
+            break;
+          }
+          int i, j;
+          if (!item_pixel(F, static_cast<int64_t>(item), 0, i, j, apix_out)) continue;
+          const double x1 = double(i) / double(P.width), x2 = double(i + 1) / double(P.width);
+          const double y1 = double(j) / double(P.height), y2 = double(j + 1) / double(P.height);
+          if (x1 + 0.0001 >= x2 || y1 + 0.0001 >= y2) {  // whole pixel under eps: black (U8)
+            if (lane == 0) {
+              if (rgb8) {
+                rgb8[apix_out * 3 + 0] = 0;
+                rgb8[apix_out * 3 + 1] = 0;
+                rgb8[apix_out * 3 + 2] = 0;
+              }
+              if (rgbf) {
+                rgbf[apix_out * 3 + 0] = 0.0;
+                rgbf[apix_out * 3 + 1] = 0.0;
+                rgbf[apix_out * 3 + 2] = 0.0;
+              }
+            }
+            continue;
+          }
+          set_frame(0, x1, x2, y1, y2);
+          fsp = 1;
+          abase = 0;
+          atop = true;
+          need_new_pixel = false;
+        }
+        if (exhausted && fsp == 0) break;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        // assign samples abase + lane of region fsp-1
+        const int k = abase + lane;
+        if (k < an) {
+          const int f = fsp - 1;
+          const double x1 = frbuf[f * 8 + 0], x2 = frbuf[f * 8 + 1], y1 = frbuf[f * 8 + 2], y2 = frbuf[f * 8 + 3];
+          const double w = x2 - x1, h = y2 - y1;
+          sx = radinv2(k) * w + x1;    // hammersley x
+          sy = (0.0 / an) * h + y1;    // hammersley y is always 0 (U7)
+          sample_slot = k;
+          rec_on = hits != nullptr && atop;
+          pass = 0;
+          camk = 0;
+          nrays = 0;
+          acc = mk3(0, 0, 0);
+          st = ST_CAM;
+        }
+      }
+    }
+
+    // ------------------------------------------------ advance lanes to their next query
+    qmode = Q_NONE;
+    while (st != ST_IDLE && qmode == Q_NONE) {
+      switch (st) {
+        case ST_CAM: {
+          // next camera ray of trace(x, y) (RayTracer.cpp:35-79)
+          if (camk == ncam) {
+            dvec3 ret = acc;
+            if (P.dof) ret *= (1.0 / (P.dof_div + 1.0));
+            ret = rtm::gclamp3(ret, 0.0, 1.0);
+            if (ADAPTIVE) {
+              colbuf[sample_slot * 3 + 0] = ret.x;
+              colbuf[sample_slot * 3 + 1] = ret.y;
+              colbuf[sample_slot * 3 + 2] = ret.z;
+              if (rec_on) hits[apix_out * an + sample_slot].nrays = nrays;
+              st = ST_IDLE;
+              break;
+            }
+            double* out = sbuf + static_cast<int64_t>(sample_slot) * 3;
+            if (P.anaglyph && pass == 0) {  // tracePixel (RayTracer.cpp:92-99): park pass 0 in the buffer
+              out[0] = ret.x;
+              out[1] = ret.y;
+              out[2] = ret.z;
+              pass = 1;
+              camk = 0;
+              acc = mk3(0, 0, 0);
+              break;
+            }
+            if (P.anaglyph) {
+              out[0] = ret.x;  // red from the shifted eye, green/blue from pass 0
+            } else {
+              out[0] = ret.x;
+              out[1] = ret.y;
+              out[2] = ret.z;
+            }
+            if (rec_on) hits[sample_slot].nrays = nrays;
+            st = ST_IDLE;
+            break;
+          }
+          const RtxCamera& cam = F.cam;
+          const dvec3 eye = pass ? ld3(cam.eye) + mk3(0.25, 0.0, 0.0) : ld3(cam.eye);
+          const double x = sx - 0.5, y = sy - 0.5;
+          const dvec3 cdir = rtm::normalize(ld3(cam.look) + x * ld3(cam.u) + y * ld3(cam.v));
+          if (camk == 0) {
+            rp = eye;
+            rd = cdir;
+            first_query = rec_on && pass == 0;
+            if (first_query) {  // default record: miss (also what depth < 0 leaves)
+              RtxHitRecord* hr = ADAPTIVE ? &hits[apix_out * an + sample_slot] : &hits[sample_slot];
+              hr->object = hr->face = hr->scene_leaf = hr->mesh_leaf = -1;
+              hr->t = 1000.0;
+              hr->pad = 0;
+            }
+          } else {
+            const double fd = rtm::gmax(P.dof_fd, 1.0);
+            const dvec3 fp_n = -cdir;
+            const dvec3 fp_pt = rtm::ray_at(eye, cdir, fd);
+            double t = rtm::dot(fp_n, cdir);
+            t = rtm::dot(fp_pt - eye, fp_n) / t;
+            const dvec3 dest = rtm::ray_at(eye, cdir, t);
+            rp = eye + ld3(&F.offv[(camk - 1) * 3]);
+            rd = rtm::normalize(dest - rp);
+            first_query = false;
+          }
+          camk++;
+          if (STATS) C.camera++;
+          top = 0;
+          push(top, rp, rd, mk3(1, 1, 1), mk3(1, 1, 1), P.depth, 0);
+          st = ST_POP;
+          break;
+        }
+        case ST_POP: {
+          if (top == 0) {
+            st = ST_CAM;
+            break;
+          }
+          --top;
+          const double* b = pbuf + static_cast<size_t>(top) * 13 * nlanes + glane;
+          const int dk = static_cast<int>(b[12 * nlanes]);
+          nrays++;
+          const int pdepth = dk >= 0 ? dk / 4 : -((-dk + 3) / 4);
+          if (pdepth < 0) break;  // `depth >= 0 &&` (RayTracer.cpp:116)
+          rp = mk3(b[0 * nlanes], b[1 * nlanes], b[2 * nlanes]);
+          rd = mk3(b[3 * nlanes], b[4 * nlanes], b[5 * nlanes]);
+          W = mk3(b[6 * nlanes], b[7 * nlanes], b[8 * nlanes]);
+          area_sum = mk3(b[9 * nlanes], b[10 * nlanes], b[11 * nlanes]);  // kt factor, parked until the hit
+          rdepth = pdepth;
+          rkind = dk - pdepth * 4;
+          qmode = Q_CLOSEST;
+          qtp = -RTX_INF;
+          qrp = -1;
+          qsq = -1;
+          st = ST_HIT;
+          break;
+        }
+        case ST_HIT: {
+          // traceRay after scene->intersect (RayTracer.cpp:116-165)
+          if (first_query) {
+            first_query = false;
+            if (bhave) {
+              RtxHitRecord* hr = ADAPTIVE ? &hits[apix_out * an + sample_slot] : &hits[sample_slot];
+              const RtxObject& o = S.objs[bobj];
+              hr->object = o.orig_id;
+              hr->scene_leaf = o.leaf;
+              hr->t = bt;
+              if (o.type == RTX_OBJ_TRIMESH) {
+                const RtxMesh me = S.meshes[o.mesh];
+                const RtxFaceIds fi = S.fids[me.face_off + bsub];
+                hr->face = fi.orig_id;
+                hr->mesh_leaf = fi.leaf;
+              }
+            }
+          }
+          if (!bhave) {  // miss: no cube map => black
+            st = ST_POP;
+            break;
+          }
+          if (rkind == 1)
+            W = W * rtm::gmax3(rtm::gmin3(rtm::pow3(area_sum, bt), rtm::splat3(1.0)), rtm::splat3(0.0));
+          else if (rkind == 2)
+            W = W * rtm::pow3(area_sum, bt);
+          const Resolved R = resolve_hit(S, rp, rd, bobj, bsub, nullptr, nullptr);
+          N = R.N;
+          m_kd = R.m.kd;
+          m_ks = R.m.ks;
+          m_sh = R.m.sh;
+          m_flags = R.m.flags;
+          st_t = bt;
+          sobj = bobj;
+          ssub = bsub;
+          if (STATS) C.shades++;
+          // Material::shade (material.cpp:34-69)
+          i_out = R.m.ke + R.m.ka * mk3(S.ambient[0], S.ambient[1], S.ambient[2]);
+          li = 0;
+          st = ST_LIGHT;
+          break;
+        }
+        case ST_LIGHT: {
+          if (li == S.n_lights) {
+            // colorC = shade(...); adaptive termination; recursion
+            const dvec3 col = i_out;
+            acc += W * col;
+            const int depth = rdepth - 1;
+            st = ST_POP;
+            if (aterm > 0.0 && rtm::dot(col, col) < aterm) break;
+            if ((m_flags & RTX_MF_RECUR) && depth > 0) {
+              const Resolved R = resolve_hit(S, rp, rd, sobj, ssub, nullptr, nullptr);
+              const bool leaving = rtm::dot(N, rd) >= 0;
+              const bool in_trans = (m_flags & RTX_MF_TRANS) != 0;
+              const bool next_trans = leaving ? true : in_trans;  // air is transmissive
+              const dvec3 normal = (leaving ? -1.0 : 1.0) * N;
+              const double c = -1 * rtm::dot(normal, rd);
+              const double eta =
+                  next_trans ? (leaving ? R.m.index : S.air_index) / (leaving ? S.air_index : R.m.index) : 0;
+              const double radicand = 1 - eta * eta * (1 - c * c);
+              const bool tir = next_trans && radicand < 0;
+              // push refraction first so that reflection is traced first
+              if (next_trans && !tir && top < pend_cap) {
+                const dvec3 tp = rtm::ray_at(rp, rd, st_t + RTX_RAY_EPS);
+                const dvec3 td = eta * rd + (eta * c - sqrt(radicand)) * normal;
+                push(top, tp, td, W, leaving ? mk3(1.0, 1.0, 1.0) : R.m.kt, depth, 2);
+                if (STATS) C.secondary++;
+              }
+              if (((m_flags & RTX_MF_REFL) || tir) && top < pend_cap) {
+                const dvec3 rdir = rd + 2 * c * normal;
+                const dvec3 rs = rtm::ray_at(rp, rd, st_t - RTX_RAY_EPS);
+                push(top, rs, rdir, W * R.m.kr, leaving ? R.m.kt : mk3(1.0, 1.0, 1.0), depth, 1);
+                if (STATS) C.secondary++;
+              }
+            }
+            break;
+          }
+          const RtxLight& L = S.lights[li];
+          const dvec3 X = rtm::ray_at(rp, rd, st_t);
+          const dvec3 l_i = light_dir(L, X);
+          const dvec3 l_r = (l_i - 2 * (rtm::dot(l_i, N)) * N);
+          double dt = rtm::dot(l_i, N);
+          if (m_flags & RTX_MF_TRANS) dt = fabs(dt);
+          const dvec3 d_comp = m_kd * rtm::gmax(0.0, dt);
+          const dvec3 s_comp = m_ks * rtm::pow3(rtm::splat3(rtm::gmax(0.0, rtm::dot(l_r, rd))), m_sh);
+          dscomp = d_comp + s_comp;
+          dattn = light_dist_atten(L, X);
+          // shadowAttenuation (light.cpp:16-20) / AreaLight (light.cpp:76-87)
+          if (L.type == RTX_LIGHT_DIRECTIONAL || L.type == RTX_LIGHT_POINT) {
+            sdir = light_dir(L, X - rd * RTX_EPS_BACKUP);
+            pick = -1;
+          } else {
+            const dvec3 ori = ld3(L.orient), lpos = ld3(L.pos);
+            if (L.type == RTX_LIGHT_SPOT &&
+                !((rtm::dot(light_dir(L, X), ori) <= 0) &&
+                  (rtm::dot(rtm::normalize(X - (lpos - L.offset * ori)), ori) > S.cos45))) {
+              i_out += dattn * mk3(0.0, 0.0, 0.0) * ld3(L.color) * dscomp;
+              li++;
+              break;
+            }
+            area_sum = mk3(1.0, 1.0, 1.0);
+            pick = 0;
+          }
+          st = ST_SRS;
+          break;
+        }
+        case ST_SRS: {
+          // start one srsAttenuation (light.cpp:21-53), or finish an area light
+          const RtxLight& L = S.lights[li];
+          const dvec3 pb = rtm::ray_at(rp, rd, st_t) - rd * RTX_EPS_BACKUP;
+          if (pick >= 0) {
+            bool started = false;
+            while (pick < S.ss_res) {
+              const dvec3 lp = ld3(S.picks + (size_t(li) * S.ss_res + pick) * 3);
+              pick++;
+              if (L.type == RTX_LIGHT_SPOT &&
+                  !((rtm::dot(light_dir(L, pb), ld3(L.orient)) <= 0) &&
+                    (rtm::dot(rtm::normalize(pb - lp), ld3(L.orient)) > S.cos45)))
+                continue;
+              sdir = rtm::normalize(lp - pb);
+              started = true;
+              break;
+            }
+            if (!started) {
+              dvec3 sa = area_sum;
+              sa *= (1.0 / (S.ss_res - 1));
+              i_out += dattn * sa * ld3(L.color) * dscomp;
+              li++;
+              st = ST_LIGHT;
+              break;
+            }
+          }
+          if (STATS) C.shadow++;
+          nrays++;
+          sattn = mk3(1.0, 1.0, 1.0);
+          wpos = pb;
+          last_t = 0.0;
+          qmode = Q_NEXT;
+          qtp = -RTX_INF;
+          qrp = -1;
+          qsq = -1;
+          st = ST_WALK;
+          break;
+        }
+        case ST_WALK: {
+          const RtxLight& L = S.lights[li];
+          bool done = false;
+          dvec3 result = sattn;
+          if (!bhave) {
+            done = true;
+          } else {
+            const double t = bt - last_t;
+            last_t = bt;
+            const dvec3 pb = rtm::ray_at(rp, rd, st_t) - rd * RTX_EPS_BACKUP;
+            const Resolved R = resolve_hit(S, pb, sdir, bobj, bsub, nullptr, nullptr);
+            const bool is_inside = rtm::dot(R.N, sdir) > 0;
+            wpos = rtm::ray_at(wpos, sdir, t);
+            bool limit = false;  // sattnLimitCheck with the relative t (U14)
+            if (L.type == RTX_LIGHT_POINT) {
+              limit = rtm::dot(ld3(L.pos) - rtm::ray_at(wpos, sdir, t), sdir) <= 0;
+            } else if (L.type != RTX_LIGHT_DIRECTIONAL) {
+              const dvec3 ori = ld3(L.orient), lpos = ld3(L.pos);
+              double ti = rtm::dot(ori, sdir);
+              ti = rtm::dot(lpos - wpos, ori) / ti;
+              dvec3 imp = rtm::ray_at(wpos, sdir, ti);
+              if (L.type != RTX_LIGHT_AREA_RECT && !(rtm::dot(imp - lpos, imp - lpos) < (L.radius * L.radius)))
+                imp = mk3(0.0, 0.0, 0.0);
+              limit = rtm::dot(imp - rtm::ray_at(wpos, sdir, t), sdir) <= 0;
+            }
+            if (limit) {
+              done = true;
+            } else {
+              const bool next_trans = is_inside ? true : ((R.m.flags & RTX_MF_TRANS) != 0);
+              if (!next_trans || (aterm > 0.0 && rtm::dot(sattn, sattn) < aterm * aterm)) {
+                result = mk3(0.0, 0.0, 0.0);
+                done = true;
+              } else {
+                const dvec3 kt = is_inside ? R.m.kt : mk3(1.0, 1.0, 1.0);
+                sattn *= rtm::pow3(kt, t);
+                qmode = Q_NEXT;
+                qtp = bt;
+                qrp = bobj;
+                qsq = bsub;
+              }
+            }
+          }
+          if (done) {
+            if (pick < 0) {
+              i_out += dattn * result * ld3(L.color) * dscomp;
+              li++;
+              st = ST_LIGHT;
+            } else {
+              area_sum += result;
+              st = ST_SRS;
+            }
+          }
+          break;
+        }
+        default:
+          st = ST_IDLE;
+          break;
+      }
+    }
+
+    // ------------------------------------------------ exit / traversal
+    const unsigned long long busy = __ballot(qmode != Q_NONE);
+    if (busy == 0ull) {
+      if (__ballot(st != ST_IDLE) == 0ull && exhausted) break;
+      continue;
+    }
+    if (qmode != Q_NONE) {
+      dvec3 qP = rp, qD = rd;
+      double qlim = RTX_INF;
+      if (qmode == Q_NEXT) {
+        qP = rtm::ray_at(rp, rd, st_t) - rd * RTX_EPS_BACKUP;
+        qD = sdir;
+        const RtxLight& L = S.lights[li];
+        // any hit past a point light trips the limit check
+        if (L.type == RTX_LIGHT_POINT) qlim = rtm::distance(qP, ld3(L.pos)) * (1.0 + 1e-6) + S.margin;
+      }
+      bhave = traverse<STATS>(S, qmode, qP, qD, qtp, qrp, qsq, qlim, bt, bobj, bsub, stk, lane, C);
+    }
+  }
+  if (STATS) {
+    int64_t v[7] = {C.camera, C.secondary, C.shadow, C.nodes, C.objects, C.tris, C.shades};
+#pragma unroll
+    for (int k = 0; k < 7; ++k) {
+      int64_t x = v[k];
+      for (int off = 32; off > 0; off >>= 1) x += __shfl_down(x, off);
+      if (lane == 0) atomicAdd(&stats[k], static_cast<unsigned long long>(x));
+    }
+  }
+}
+
+// Per-pixel ordered reduction of the sample buffer (RayTracer.cpp:288-298:
+// col += tracePixel(...) in si-major order, col /= s*s; setPixel truncates).
+__global__ void __launch_bounds__(WG) reduce_kernel(const FrameParams* __restrict__ Fp, const double* __restrict__ sbuf,
+                                                     uint8_t* __restrict__ rgb8, double* __restrict__ rgbf,
+                                                     int64_t npix_slots) {
+  const FrameParams& F = *Fp;
+  const int64_t o = static_cast<int64_t>(blockIdx.x) * WG + threadIdx.x;
+  if (o >= npix_slots) return;
+  // skip slots that map outside the image (packed tiles at the border)
+  if (F.P.packed && F.P.tile > 0) {
+    const int64_t k = o / (int64_t(F.tw) * F.th);
+    const int r = static_cast<int>(o % (int64_t(F.tw) * F.th));
+    const int tile_id = F.P.shard + static_cast<int>(k) * F.P.nshards;
+    const int i = (tile_id % F.tiles_x) * F.tw + r % F.tw;
+    const int j = (tile_id / F.tiles_x) * F.th + r / F.tw;
+    if (i >= F.P.width || j >= F.P.height) return;
+  } else if (F.P.tile > 0) {  // full frame, sharded: only this shard's tiles
+    const int i = static_cast<int>(o % F.P.width), j = static_cast<int>(o / F.P.width);
+    const int tile_id = (j / F.th) * F.tiles_x + (i / F.tw);
+    if (tile_id % F.P.nshards != F.P.shard) return;
+  }
+  const double* s = sbuf + o * F.spp * 3;
+  dvec3 acc = mk3(0.0, 0.0, 0.0);
+  for (int q = 0; q < F.spp; ++q) acc += mk3(s[q * 3 + 0], s[q * 3 + 1], s[q * 3 + 2]);
+  if (F.P.aa_mode != RTX_AA_NONE) acc = acc / double(F.s * F.s);
+  if (rgb8) {
+    rgb8[o * 3 + 0] = (uint8_t)(int)(255.0 * acc.x);
+    rgb8[o * 3 + 1] = (uint8_t)(int)(255.0 * acc.y);
+    rgb8[o * 3 + 2] = (uint8_t)(int)(255.0 * acc.z);
+  }
+  if (rgbf) {
+    rgbf[o * 3 + 0] = acc.x;
+    rgbf[o * 3 + 1] = acc.y;
+    rgbf[o * 3 + 2] = acc.z;
+  }
+}
+
+// ============================================================ host side / C ABI
+namespace {
+
+thread_local std::string g_err;
+
+#define HIP_TRY(expr)                                                            \
+  do {                                                                           \
+    hipError_t e_ = (expr);                                                      \
+    if (e_ != hipSuccess) {                                                      \
+      g_err = std::string(#expr) + ": " + hipGetErrorString(e_);                 \
+      return RTX_ERR_HIP;                                                        \
+    }                                                                            \
+  } while (0)
+
+struct SceneState {
+  int device = 0;
+  DevScene S;
+  DevScene S_launch;
+  std::vector<void*> allocs;
+  RtxSceneDesc desc;           // shallow copy (pointers valid only during create)
+  RtxCamera cam;
+  std::vector<RtxLight> lights;
+  int stack_cap = 0;
+  int n_cu = 256;
+  FrameParams* d_frame = nullptr;
+  unsigned long long* d_work = nullptr;
+  unsigned long long* d_stats = nullptr;
+  double* d_picks = nullptr;
+  int picks_res = -1;
+  double* d_sbuf = nullptr;     // per-sample colours (HBM), grown on demand
+  size_t sbuf_bytes = 0;
+  double* d_pbuf = nullptr;     // per-lane pending-ray stacks (HBM)
+  size_t pbuf_bytes = 0;
+  std::vector<hipEvent_t> ev_start, ev_stop;
+};
+
+template <typename T>
+rtx_status upload(SceneState& st, const T* src, size_t n, const T** dst) {
+  if (n == 0 || !src) {
+    *dst = nullptr;
+    return RTX_OK;
+  }
+  void* p = nullptr;
+  HIP_TRY(hipMalloc(&p, n * sizeof(T)));
+  st.allocs.push_back(p);
+  HIP_TRY(hipMemcpy(p, src, n * sizeof(T), hipMemcpyHostToDevice));
+  *dst = static_cast<const T*>(p);
+  return RTX_OK;
+}
+
+double scene_extent(const RtxSceneDesc* d) {
+  double e = 1.0;
+  for (int i = 0; i < d->n_objects; ++i)
+    for (int k = 0; k < 3; ++k) {
+      e = std::fmax(e, std::fabs(d->objects[i].wmin[k]));
+      e = std::fmax(e, std::fabs(d->objects[i].wmax[k]));
+    }
+  for (int k = 0; k < 3; ++k) e = std::fmax(e, std::fabs(d->camera.eye[k]));
+  for (int i = 0; i < d->n_lights; ++i)
+    for (int k = 0; k < 3; ++k) e = std::fmax(e, std::fabs(d->lights[i].pos[k]));
+  return e;
+}
+
+double mesh_extent(const RtxSceneDesc* d) {
+  double e = 1.0;
+  for (int i = 0; i < d->n_mesh_nodes; ++i)
+    for (int k = 0; k < 3; ++k) {
+      e = std::fmax(e, std::fabs(d->mesh_nodes[i].bmin[k]));
+      e = std::fmax(e, std::fabs(d->mesh_nodes[i].bmax[k]));
+    }
+  return e;
+}
+
+// Area-light sample positions (AreaLightRect::pick / AreaLightCirc::pick,
+// light.cpp:106-131): host glibc cos/sin, exactly as the CPU restatement.
+std::vector<double> make_picks(const std::vector<RtxLight>& lights, int res) {
+  const double PI = 3.1415926535897932384626433832795028841971;
+  std::vector<double> out(lights.size() * size_t(res > 0 ? res : 0) * 3, 0.0);
+  for (size_t li = 0; li < lights.size(); ++li) {
+    const RtxLight& L = lights[li];
+    for (int i = 0; i < res; ++i) {
+      dvec3 p = mk3(0, 0, 0);
+      if (L.type == RTX_LIGHT_AREA_RECT) {
+        double mul = 0.5, result = 0.0;
+        int n = i;
+        while (n > 0) {
+          result += (n % 2) ? mul : 0;
+          n /= 2;
+          mul /= 2.0;
+        }
+        double px = result, py = ((double)n) / res;
+        double a = (px - 0.5) * L.width, b = (py - 0.5) * L.height;
+        p = mk3(L.u[0] * a + L.v[0] * b, L.u[1] * a + L.v[1] * b, L.u[2] * a + L.v[2] * b);
+      } else if (L.type == RTX_LIGHT_AREA_CIRC || L.type == RTX_LIGHT_SPOT) {
+        double ang_rad = 2 * PI / res * i;
+        double dist = 0.5 * L.radius;
+        double x = std::cos(ang_rad) * dist;
+        double y = std::sin(ang_rad) * dist;
+        const dvec3 ori = ld3(L.orient);
+        const dvec3 ab = mk3(std::fabs(ori.x), std::fabs(ori.y), std::fabs(ori.z));
+        dvec3 u = mk3(0.0, 0.0, 0.0);
+        if (ab.x < ab.y && ab.x < ab.z) u = mk3(0.0, -ori.z, ori.y);
+        else if (ab.y < ab.z) u = mk3(-ori.z, 0.0, ori.x);
+        else u = mk3(-ori.y, ori.x, 0.0);
+        u = rtm::normalize(u);
+        const dvec3 v = rtm::cross(ori, u);
+        p = x * u + y * v + ld3(L.pos);
+      }
+      out[(li * res + i) * 3 + 0] = p.x;
+      out[(li * res + i) * 3 + 1] = p.y;
+      out[(li * res + i) * 3 + 2] = p.z;
+    }
+  }
+  return out;
+}
+
+int isqrt_floor(int v) {
+  int r = 0;
+  while ((r + 1) * (r + 1) <= v) ++r;
+  return r;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* rtx_last_error(void) { return g_err.c_str(); }
+
+rtx_status rtx_device_count(int* n) {
+  int c = 0;
+  hipError_t e = hipGetDeviceCount(&c);
+  if (e != hipSuccess) c = 0;
+  *n = c;
+  return RTX_OK;
+}
+
+rtx_status rtx_scene_create(int device, const RtxSceneDesc* d, void** out) {
+  if (!d || !out) {
+    g_err = "rtx_scene_create: null argument";
+    return RTX_ERR_INVALID;
+  }
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) {
+    g_err = "rtx_scene_create: no HIP device visible";
+    return RTX_ERR_NODEVICE;
+  }
+  if (device < 0 || device >= ndev) {
+    g_err = "rtx_scene_create: bad device index";
+    return RTX_ERR_INVALID;
+  }
+  HIP_TRY(hipSetDevice(device));
+  hipDeviceProp_t prop;
+  HIP_TRY(hipGetDeviceProperties(&prop, device));
+  if (std::string(prop.gcnArchName).find("gfx950") == std::string::npos) {
+    g_err = std::string("rtx_scene_create: device is ") + prop.gcnArchName + ", this build targets gfx950";
+    return RTX_ERR_NODEVICE;
+  }
+  SceneState* st = new SceneState();
+  st->device = device;
+  st->n_cu = prop.multiProcessorCount;
+  std::memset(&st->S, 0, sizeof(st->S));
+  DevScene& S = st->S;
+  rtx_status rc = RTX_OK;
+#define UP(src, n, dst) \
+  if ((rc = upload(*st, src, size_t(n), &dst)) != RTX_OK) { rtx_scene_destroy(st); return rc; }
+  UP(d->scene_nodes, d->n_scene_nodes, S.snodes);
+  UP(d->objects, d->n_objects, S.objs);
+  UP(d->materials, d->n_materials, S.mats);
+  UP(d->meshes, d->n_meshes, S.meshes);
+  UP(d->mesh_nodes, d->n_mesh_nodes, S.mnodes);
+  UP(d->faces, d->n_faces, S.faces);
+  UP(d->face_ids, d->n_faces, S.fids);
+  UP(d->vnormals, size_t(d->n_vnormals) * 3, S.vnormals);
+  UP(d->vmats, d->n_vmats, S.vmats);
+  UP(d->lights, d->n_lights, S.lights);
+  UP(d->textures, d->n_textures, S.texs);
+  UP(d->texels, d->n_texels, S.texels);
+#undef UP
+  S.n_snodes = d->n_scene_nodes;
+  S.n_objs = d->n_objects;
+  S.n_lights = d->n_lights;
+  S.margin = 1e-9 * scene_extent(d);
+  S.lmargin = 1e-9 * mesh_extent(d);
+  S.cos45 = std::cos(3.1415926535897932384626433832795028841971 / 4);
+  for (int k = 0; k < 3; ++k) S.ambient[k] = d->ambient[k];
+  S.air_index = (0.299 * 1.0) + (0.587 * 1.0) + (0.114 * 1.0);
+  st->cam = d->camera;
+  st->lights.assign(d->lights, d->lights + d->n_lights);
+  st->stack_cap = d->scene_depth + d->mesh_depth + 4;
+  if (hipMalloc(&st->d_frame, sizeof(FrameParams)) != hipSuccess ||
+      hipMalloc(&st->d_work, sizeof(unsigned long long)) != hipSuccess ||
+      hipMalloc(&st->d_stats, 8 * sizeof(unsigned long long)) != hipSuccess) {
+    g_err = "rtx_scene_create: hipMalloc failed";
+    rtx_scene_destroy(st);
+    return RTX_ERR_HIP;
+  }
+  *out = st;
+  return RTX_OK;
+}
+
+rtx_status rtx_scene_destroy(void* scene) {
+  if (!scene) return RTX_OK;
+  SceneState* st = static_cast<SceneState*>(scene);
+  (void)hipSetDevice(st->device);
+  for (void* p : st->allocs) (void)hipFree(p);
+  if (st->d_frame) (void)hipFree(st->d_frame);
+  if (st->d_work) (void)hipFree(st->d_work);
+  if (st->d_stats) (void)hipFree(st->d_stats);
+  if (st->d_picks) (void)hipFree(st->d_picks);
+  if (st->d_sbuf) (void)hipFree(st->d_sbuf);
+  if (st->d_pbuf) (void)hipFree(st->d_pbuf);
+  for (auto e : st->ev_start) (void)hipEventDestroy(e);
+  for (auto e : st->ev_stop) (void)hipEventDestroy(e);
+  delete st;
+  return RTX_OK;
+}
+
+static rtx_status build_frame(const SceneState* st, const RtxRenderParams* p, FrameParams& F) {
+  std::memset(&F, 0, sizeof(F));
+  F.P = *p;
+  F.cam = st->cam;
+  if (p->width <= 0 || p->height <= 0) {
+    g_err = "rtx_render: width/height must be positive";
+    return RTX_ERR_INVALID;
+  }
+  if (p->overlapping) {
+    g_err = "rtx_render: -O o (overlapping objects) is not supported on the GPU path";
+    return RTX_ERR_INVALID;
+  }
+  if (p->depth > MAX_DEPTH) {
+    g_err = "rtx_render: recursion depth above 16 is not supported by this build";
+    return RTX_ERR_CAPACITY;
+  }
+  if (p->dof && (p->dof_div < 0 || p->dof_div > MAX_DOF)) {
+    g_err = "rtx_render: DoF samples must be in [0, 64]";
+    return RTX_ERR_CAPACITY;
+  }
+  if (p->aa_mode != RTX_AA_NONE && p->aa_samples <= 0) {
+    g_err = "rtx_render: AA samples must be positive";
+    return RTX_ERR_INVALID;
+  }
+  const int s = p->aa_mode == RTX_AA_NONE ? 1 : p->aa_samples;
+  F.s = s;
+  F.spp = s * s;
+  if (p->aa_mode != RTX_AA_ADAPTIVE && F.spp > 64) {
+    g_err = "rtx_render: regular AA with more than 8x8 samples is not supported";
+    return RTX_ERR_CAPACITY;
+  }
+  if (p->aa_mode == RTX_AA_ADAPTIVE && F.spp > 1024) {
+    g_err = "rtx_render: adaptive AA with more than 32x32 samples is not supported";
+    return RTX_ERR_CAPACITY;
+  }
+  if (p->aa_mode == RTX_AA_ADAPTIVE) {
+    F.ppw = 1;
+  } else {
+    F.ppw = 64 / F.spp;
+  }
+  const int r = isqrt_floor(F.ppw);
+  if (r * r == F.ppw) {
+    F.bw = r;
+    F.bh = r;
+  } else {
+    F.bw = F.ppw;
+    F.bh = 1;
+  }
+  if (p->tile > 0) {
+    if (p->nshards <= 0 || p->shard < 0 || p->shard >= p->nshards) {
+      g_err = "rtx_render: bad shard";
+      return RTX_ERR_INVALID;
+    }
+    F.tw = p->tile;
+    F.th = p->tile;
+    F.tiles_x = (p->width + p->tile - 1) / p->tile;
+    F.tiles_y = (p->height + p->tile - 1) / p->tile;
+    const int nt = F.tiles_x * F.tiles_y;
+    F.n_owned = nt > p->shard ? (nt - p->shard + p->nshards - 1) / p->nshards : 0;
+  } else {
+    F.tw = p->width;
+    F.th = p->height;
+    F.tiles_x = 1;
+    F.tiles_y = 1;
+    F.n_owned = 1;
+  }
+  F.bx_per_tile = (F.tw + F.bw - 1) / F.bw;
+  F.items_per_tile = F.bx_per_tile * ((F.th + F.bh - 1) / F.bh);
+  F.n_items = static_cast<int64_t>(F.items_per_tile) * F.n_owned;
+  F.n_samples = F.n_items * F.ppw * F.spp;
+  // DoF eye offsets: (cos(a) * V + sin(a) * U) * sz (RayTracer.cpp:62-67)
+  if (p->dof) {
+    const double PI = 3.1415926535897932384626433832795028841971;
+    const double sz = p->dof_apsz / 2;
+    const int divs = p->dof_div;
+    const double baseAngle = PI / divs;
+    const dvec3 V = ld3(st->cam.v), U = ld3(st->cam.u);
+    for (int k = 0; k < divs; k++) {
+      double offsetAngle = PI / 2;
+      offsetAngle = offsetAngle / divs + (k - 1) * baseAngle;
+      dvec3 o = (std::cos(offsetAngle) * V + std::sin(offsetAngle) * U) * sz;
+      F.offv[k * 3 + 0] = o.x;
+      F.offv[k * 3 + 1] = o.y;
+      F.offv[k * 3 + 2] = o.z;
+    }
+  }
+  return RTX_OK;
+}
+
+rtx_status rtx_shard_pixels(const RtxRenderParams* p, int64_t* npix) {
+  if (!p || !npix) return RTX_ERR_INVALID;
+  if (p->tile > 0 && p->packed) {
+    const int tx = (p->width + p->tile - 1) / p->tile, ty = (p->height + p->tile - 1) / p->tile;
+    const int nt = tx * ty;
+    const int owned = nt > p->shard ? (nt - p->shard + p->nshards - 1) / p->nshards : 0;
+    *npix = static_cast<int64_t>(owned) * p->tile * p->tile;
+  } else {
+    *npix = static_cast<int64_t>(p->width) * p->height;
+  }
+  return RTX_OK;
+}
+
+rtx_status rtx_render(void* scene, const RtxRenderParams* params, uint8_t* rgb8, double* rgb_f64,
+                      RtxHitRecord* hits, int device_ptrs, void* stream_v, RtxStats* stats) {
+  if (!scene || !params) {
+    g_err = "rtx_render: null argument";
+    return RTX_ERR_INVALID;
+  }
+  SceneState* st = static_cast<SceneState*>(scene);
+  HIP_TRY(hipSetDevice(st->device));
+  hipStream_t stream = static_cast<hipStream_t>(stream_v);
+  FrameParams F;
+  rtx_status rc = build_frame(st, params, F);
+  if (rc != RTX_OK) return rc;
+  // area-light pick tables depend on ss_res
+  st->S_launch = st->S;
+  DevScene& S = st->S_launch;
+  S.ss_res = params->ss_res;
+  bool need_picks = false;
+  for (const auto& L : st->lights) need_picks |= L.type >= RTX_LIGHT_AREA_RECT;
+  if (need_picks && st->picks_res != params->ss_res) {
+    std::vector<double> pk = make_picks(st->lights, params->ss_res);
+    if (st->d_picks) (void)hipFree(st->d_picks);
+    st->d_picks = nullptr;
+    if (!pk.empty()) {
+      HIP_TRY(hipMalloc(&st->d_picks, pk.size() * sizeof(double)));
+      HIP_TRY(hipMemcpy(st->d_picks, pk.data(), pk.size() * sizeof(double), hipMemcpyHostToDevice));
+    }
+    st->picks_res = params->ss_res;
+  }
+  S.picks = st->d_picks;
+
+  int64_t npix = 0;
+  rtx_shard_pixels(params, &npix);
+  uint8_t* d_rgb8 = rgb8;
+  double* d_rgbf = rgb_f64;
+  RtxHitRecord* d_hits = hits;
+  std::vector<void*> tmp;
+  if (!device_ptrs) {
+    if (rgb8) { HIP_TRY(hipMalloc(&d_rgb8, npix * 3)); tmp.push_back(d_rgb8); HIP_TRY(hipMemsetAsync(d_rgb8, 0, npix * 3, stream)); }
+    if (rgb_f64) { HIP_TRY(hipMalloc(&d_rgbf, npix * 3 * sizeof(double))); tmp.push_back(d_rgbf); HIP_TRY(hipMemsetAsync(d_rgbf, 0, npix * 3 * sizeof(double), stream)); }
+    if (hits) {
+      HIP_TRY(hipMalloc(&d_hits, npix * F.spp * sizeof(RtxHitRecord)));
+      tmp.push_back(d_hits);
+      HIP_TRY(hipMemsetAsync(d_hits, 0xff, npix * F.spp * sizeof(RtxHitRecord), stream));
+    }
+  }
+  const bool adaptive = params->aa_mode == RTX_AA_ADAPTIVE;
+  if (!adaptive) {
+    const size_t need = size_t(npix) * F.spp * 3 * sizeof(double);
+    if (need > st->sbuf_bytes) {
+      if (st->d_sbuf) (void)hipFree(st->d_sbuf);
+      st->d_sbuf = nullptr;
+      st->sbuf_bytes = 0;
+      HIP_TRY(hipMalloc(&st->d_sbuf, need));
+      st->sbuf_bytes = need;
+    }
+  }
+  HIP_TRY(hipMemcpyAsync(st->d_frame, &F, sizeof(FrameParams), hipMemcpyHostToDevice, stream));
+  HIP_TRY(hipMemsetAsync(st->d_work, 0, sizeof(unsigned long long), stream));
+  if (stats) HIP_TRY(hipMemsetAsync(st->d_stats, 0, 8 * sizeof(unsigned long long), stream));
+
+  const int cslots = adaptive ? (F.spp > 64 ? F.spp : 64) : 0;
+  const int fslots = adaptive ? 16 * 8 : 0;
+  const size_t lds_per_wave =
+      size_t(cslots * 3 + fslots) * sizeof(double) + size_t(st->stack_cap) * 64 * sizeof(int);
+  const size_t lds = lds_per_wave * WAVES_PER_WG;
+  if (lds > 160 * 1024) {
+    g_err = "rtx_render: LDS budget exceeded (BVH too deep or too many AA samples)";
+    for (void* p : tmp) (void)hipFree(p);
+    return RTX_ERR_CAPACITY;
+  }
+  // persistent grid: as many resident workgroups as the occupancy allows
+  const void* kfn = stats ? (adaptive ? reinterpret_cast<const void*>(render_kernel<true, true>)
+                                      : reinterpret_cast<const void*>(render_kernel<true, false>))
+                          : (adaptive ? reinterpret_cast<const void*>(render_kernel<false, true>)
+                                      : reinterpret_cast<const void*>(render_kernel<false, false>));
+  int per_cu = 0;
+  HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kfn, WG, lds));
+  if (per_cu < 1) per_cu = 1;
+  int64_t grid = static_cast<int64_t>(st->n_cu) * per_cu;
+  const int64_t waves_needed = adaptive ? F.n_items : (F.n_samples + 63) / 64;
+  const int64_t grid_needed = (waves_needed + WAVES_PER_WG - 1) / WAVES_PER_WG;
+  if (grid > grid_needed) grid = grid_needed;
+  if (grid < 1) grid = 1;
+  const int pend_cap = (params->depth > 0 ? params->depth : 0) + 2;
+  {
+    const size_t need = size_t(grid) * WG * pend_cap * 13 * sizeof(double);
+    if (need > st->pbuf_bytes) {
+      if (st->d_pbuf) (void)hipFree(st->d_pbuf);
+      st->d_pbuf = nullptr;
+      st->pbuf_bytes = 0;
+      HIP_TRY(hipMalloc(&st->d_pbuf, need));
+      st->pbuf_bytes = need;
+    }
+  }
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  HIP_TRY(hipEventCreate(&e0));
+  HIP_TRY(hipEventCreate(&e1));
+  HIP_TRY(hipEventRecord(e0, stream));
+  double* sb = adaptive ? nullptr : st->d_sbuf;
+  if (stats) {
+    if (adaptive)
+      hipLaunchKernelGGL((render_kernel<true, true>), dim3(grid), dim3(WG), lds, stream, st->S_launch, st->d_frame,
+                         st->d_work, sb, d_hits, d_rgb8, d_rgbf, st->d_stats, st->stack_cap, st->d_pbuf, pend_cap);
+    else
+      hipLaunchKernelGGL((render_kernel<true, false>), dim3(grid), dim3(WG), lds, stream, st->S_launch, st->d_frame,
+                         st->d_work, sb, d_hits, d_rgb8, d_rgbf, st->d_stats, st->stack_cap, st->d_pbuf, pend_cap);
+  } else {
+    if (adaptive)
+      hipLaunchKernelGGL((render_kernel<false, true>), dim3(grid), dim3(WG), lds, stream, st->S_launch, st->d_frame,
+                         st->d_work, sb, d_hits, d_rgb8, d_rgbf, st->d_stats, st->stack_cap, st->d_pbuf, pend_cap);
+    else
+      hipLaunchKernelGGL((render_kernel<false, false>), dim3(grid), dim3(WG), lds, stream, st->S_launch,
+                         st->d_frame, st->d_work, sb, d_hits, d_rgb8, d_rgbf, st->d_stats, st->stack_cap, st->d_pbuf, pend_cap);
+  }
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipEventRecord(e1, stream));
+  if (!adaptive) {
+    const int64_t rblocks = (npix + WG - 1) / WG;
+    hipLaunchKernelGGL(reduce_kernel, dim3(rblocks), dim3(WG), 0, stream, st->d_frame, sb, d_rgb8, d_rgbf, npix);
+    HIP_TRY(hipGetLastError());
+  }
+  st->ev_start.push_back(e0);
+  st->ev_stop.push_back(e1);
+  if (!device_ptrs) {
+    if (rgb8) HIP_TRY(hipMemcpyAsync(rgb8, d_rgb8, npix * 3, hipMemcpyDeviceToHost, stream));
+    if (rgb_f64) HIP_TRY(hipMemcpyAsync(rgb_f64, d_rgbf, npix * 3 * sizeof(double), hipMemcpyDeviceToHost, stream));
+    if (hits) HIP_TRY(hipMemcpyAsync(hits, d_hits, npix * F.spp * sizeof(RtxHitRecord), hipMemcpyDeviceToHost, stream));
+    HIP_TRY(hipStreamSynchronize(stream));
+    for (void* p : tmp) (void)hipFree(p);
+  }
+  if (stats) {
+    unsigned long long c[8];
+    HIP_TRY(hipMemcpyAsync(c, st->d_stats, sizeof(c), hipMemcpyDeviceToHost, stream));
+    HIP_TRY(hipStreamSynchronize(stream));
+    std::memset(stats, 0, sizeof(*stats));
+    stats->camera_rays = c[0];
+    stats->secondary_rays = c[1];
+    stats->shadow_rays = c[2];
+    stats->rays = c[0] + c[1] + c[2];
+    stats->node_visits = c[3];
+    stats->object_tests = c[4];
+    stats->tri_tests = c[5];
+    stats->shades = c[6];
+    float ms = 0.0f;
+    HIP_TRY(hipEventElapsedTime(&ms, e0, e1));
+    stats->kernel_ms = ms;
+  }
+  return RTX_OK;
+}
+
+rtx_status rtx_kernel_time(void* scene, double* total_ms, int* launches) {
+  if (!scene) return RTX_ERR_INVALID;
+  SceneState* st = static_cast<SceneState*>(scene);
+  HIP_TRY(hipSetDevice(st->device));
+  double tot = 0.0;
+  for (size_t k = 0; k < st->ev_start.size(); ++k) {
+    HIP_TRY(hipEventSynchronize(st->ev_stop[k]));
+    float ms = 0.0f;
+    HIP_TRY(hipEventElapsedTime(&ms, st->ev_start[k], st->ev_stop[k]));
+    tot += ms;
+    (void)hipEventDestroy(st->ev_start[k]);
+    (void)hipEventDestroy(st->ev_stop[k]);
+  }
+  if (total_ms) *total_ms = tot;
+  if (launches) *launches = static_cast<int>(st->ev_start.size());
+  st->ev_start.clear();
+  st->ev_stop.clear();
+  return RTX_OK;
+}
+
+}  // extern "C"

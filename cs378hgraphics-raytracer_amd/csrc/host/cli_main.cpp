@@ -1,0 +1,80 @@
+// cli_main.cpp — `ray [options] in.ray out.png`, the drop-in for the
+// reference CLI (ray/src/main.cpp:23-42, ui/CommandLineUI.cpp:23-190).
+//
+// Same getopt surface and exit codes; the render goes through the C ABI:
+// rtx_host_load (RayTracer::loadScene) -> rtx_scene_create -> rtx_render
+// (traceSetup + traceImage) -> rtx_write_image (writeImage).  There is no CPU
+// fallback: without a gfx950 device the command fails loudly.
+#include <chrono>
+#include <cstdio>
+#include <vector>
+
+#include "cli_opts.h"
+#include "rtx.h"
+#include "rtx_host.h"
+
+int main(int argc, char** argv) {
+  rtxh::CliOptions o;
+  int rc = rtxh::cli_parse(argc, argv, o);
+  if (rc) return rc;
+
+  void* hs = nullptr;
+  if (rtx_host_load(o.ray_name.c_str(), &hs) != RTX_OK) {
+    std::cerr << rtx_host_last_error() << std::endl;
+    std::cerr << "Unable to load ray file '" << o.ray_name << "'" << std::endl;
+    return 1;
+  }
+  RtxHostInfo info;
+  rtx_host_info(hs, &info);
+  RtxSceneDesc desc;
+  rtx_host_desc(hs, &desc);
+  void* scene = nullptr;
+  if (rtx_scene_create(o.device, &desc, &scene) != RTX_OK) {
+    std::cerr << "rtx: " << rtx_last_error() << std::endl;
+    rtx_host_free(hs);
+    return 2;
+  }
+  const int width = o.size;
+  const int height = rtx_image_height(width, info.aspect);  // CommandLineUI.cpp:156
+  RtxRenderParams p = rtxh::cli_params(o, width, height);
+  std::vector<uint8_t> rgb(size_t(width) * height * 3, 0);
+  std::vector<double> f64;
+  if (!o.dump_f64.empty()) f64.assign(size_t(width) * height * 3, 0.0);
+  const int spp = o.aa_mode == RTX_AA_NONE ? 1 : o.aa_samples * o.aa_samples;
+  std::vector<RtxHitRecord> hits;
+  if (!o.dump_hits.empty()) hits.resize(size_t(width) * height * spp);
+  RtxStats st;
+  auto t0 = std::chrono::steady_clock::now();
+  rtx_status r = rtx_render(scene, &p, rgb.data(), f64.empty() ? nullptr : f64.data(),
+                            hits.empty() ? nullptr : hits.data(), 0, nullptr, o.stats ? &st : nullptr);
+  const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  if (r != RTX_OK) {
+    std::cerr << "rtx: " << rtx_last_error() << std::endl;
+    rtx_scene_destroy(scene);
+    rtx_host_free(hs);
+    return 2;
+  }
+  if (rtx_write_image(o.img_name.c_str(), width, height, rgb.data()) != RTX_OK) {
+    std::cerr << rtx_host_last_error() << std::endl;
+    return 1;
+  }
+  if (!o.dump_f64.empty()) {
+    FILE* f = std::fopen(o.dump_f64.c_str(), "wb");
+    std::fwrite(f64.data(), sizeof(double), f64.size(), f);
+    std::fclose(f);
+  }
+  if (!o.dump_hits.empty()) {
+    FILE* f = std::fopen(o.dump_hits.c_str(), "wb");
+    std::fwrite(hits.data(), sizeof(RtxHitRecord), hits.size(), f);
+    std::fclose(f);
+  }
+  if (o.stats)
+    std::printf("{\"backend\": \"hip-gfx950\", \"ms\": %.3f, \"kernel_ms\": %.3f, \"rays\": %lld, "
+                "\"mrays_per_s\": %.3f, \"node_visits\": %lld, \"object_tests\": %lld, \"tri_tests\": %lld, "
+                "\"shades\": %lld}\n",
+                ms, st.kernel_ms, (long long)st.rays, st.rays / st.kernel_ms / 1e3, (long long)st.node_visits,
+                (long long)st.object_tests, (long long)st.tri_tests, (long long)st.shades);
+  rtx_scene_destroy(scene);
+  rtx_host_free(hs);
+  return 0;
+}

@@ -1,0 +1,1103 @@
+// parser.cpp — .ray scene loader (host plumbing, not accelerated).
+//
+// Restates the grammar and the observable quirks of the reference parser:
+//   tokenizer   ray/src/parser/Tokenizer.cpp:70-237, Token.cpp:121-196,
+//               fileio/buffer.cpp (line-at-a-time reading, '\0' at EOF)
+//   parser      ray/src/parser/Parser.cpp:26-1308
+//   scene build scene/scene.cpp:78-153 (world boxes), SceneObjects/trimesh.cpp
+//               (addFace degeneracy, generateNormals), camera.cpp, light.h ctors
+// Errors are reported as ParseError carrying the message RayTracer::loadScene
+// would print (RayTracer.cpp:216-234).
+#include <cmath>
+#include <cstdlib>
+#include <fstream>
+#include <list>
+#include <map>
+#include <memory>
+#include <sstream>
+
+#include "scene_model.h"
+
+namespace rtxh {
+
+using rtm::mk3;
+
+// ---------------------------------------------------------------- Material
+void Material::setBools() {
+  // isZero(): glm::length(_value) == 0.0 (material.h:129)
+  auto isZero = [](const MatParam& q) { return rtm::length(q.v) == 0.0; };
+  refl = !isZero(p[P_KR]);
+  trans = !isZero(p[P_KT]);
+  recur = refl || trans;
+  spec = refl || !isZero(p[P_KS]);
+  both = refl && trans;
+}
+
+// ---------------------------------------------------------------- Camera
+// camera.cpp:4 defines its own PI
+static const double CAM_PI = 3.14159265359;
+
+Camera::Camera() { m = mat3_identity(); }
+
+void Camera::update() {  // camera.cpp:94-99
+  dvec3 ex = rtm::mat3_mul(m.m, mk3(1, 0, 0));
+  dvec3 ey = rtm::mat3_mul(m.m, mk3(0, 1, 0));
+  dvec3 ez = rtm::mat3_mul(m.m, mk3(0, 0, -1));
+  u = (ex * normalizedHeight) * aspectRatio;
+  v = ey * normalizedHeight;
+  look = ez;
+}
+
+void Camera::setFOV(double fov) {  // camera.cpp:77-84
+  fov /= (180.0 / CAM_PI);
+  normalizedHeight = 2 * std::tan(fov / 2);
+  update();
+}
+
+void Camera::setAspectRatio(double ar) {
+  aspectRatio = ar;
+  update();
+}
+
+void Camera::setLook(const dvec3& viewDir, const dvec3& upDir) {  // camera.cpp:64-74
+  dvec3 z = -viewDir;
+  const dvec3& y = upDir;
+  dvec3 x = rtm::cross(y, z);
+  // dmat3x3(x, y, z): columns
+  m.m[0] = x.x; m.m[1] = x.y; m.m[2] = x.z;
+  m.m[3] = y.x; m.m[4] = y.y; m.m[5] = y.z;
+  m.m[6] = z.x; m.m[7] = z.y; m.m[8] = z.z;
+  update();
+}
+
+void Camera::setLookQuat(double r, double i, double j, double k) {  // camera.cpp:39-62
+  double a[3][3];  // a[c][r] as in the reference's m[c][r]
+  a[0][0] = 1.0 - 2.0 * (i * i + j * j);
+  a[0][1] = 2.0 * (r * i - j * k);
+  a[0][2] = 2.0 * (j * r + i * k);
+  a[1][0] = 2.0 * (r * i + j * k);
+  a[1][1] = 1.0 - 2.0 * (j * j + r * r);
+  a[1][2] = 2.0 * (i * j - r * k);
+  a[2][0] = 2.0 * (j * r - i * k);
+  a[2][1] = 2.0 * (i * j + r * k);
+  a[2][2] = 1.0 - 2.0 * (i * i + r * r);
+  Mat3 t;
+  for (int c = 0; c < 3; ++c)
+    for (int rr = 0; rr < 3; ++rr) t.m[c * 3 + rr] = a[c][rr];
+  m = mat3_transpose(t);
+  update();
+}
+
+// ---------------------------------------------------------------- Tokenizer
+namespace {
+
+enum Sym {
+  EOFSYM, SBT_RAYTRACER, IDENT, SCALAR, SYMTRUE, SYMFALSE, LPAREN, RPAREN, LBRACE, RBRACE, COMMA,
+  EQUALS, SEMICOLON, CAMERA, AMBIENT_LIGHT, POINT_LIGHT, DIRECTIONAL_LIGHT, AREA_LIGHT_RECT,
+  AREA_LIGHT_CIRC, SPOT_LIGHT, CONSTANT_ATTENUATION_COEFF, LINEAR_ATTENUATION_COEFF,
+  QUADRATIC_ATTENUATION_COEFF, SPHERE, BOX, SQUARE, CYLINDER, CONE, TRIMESH, POSITION, VIEWDIR,
+  UPDIR, ASPECTRATIO, FOV, COLOR, DIRECTION, CAPPED, HEIGHT, WIDTH, ANGLE, BOTTOM_RADIUS,
+  TOP_RADIUS, RADIUS, QUATERNIAN, POLYPOINTS, NORMALS, MATERIALS, FACES, GENNORMALS, TRANSLATE,
+  SCALE, ROTATE, TRANSFORM, MATERIAL, EMISSIVE, AMBIENT, SPECULAR, REFLECTIVE, DIFFUSE,
+  TRANSMISSIVE, SHININESS, INDEX, NAME, MAP, BUMP, GLOSS, UNKNOWN
+};
+
+const std::map<std::string, Sym>& reserved() {  // Token.cpp:121-196
+  static const std::map<std::string, Sym> w = {
+      {"ambient_light", AMBIENT_LIGHT}, {"ambient", AMBIENT}, {"aspectratio", ASPECTRATIO},
+      {"bottom_radius", BOTTOM_RADIUS}, {"box", BOX}, {"camera", CAMERA}, {"capped", CAPPED},
+      {"color", COLOR}, {"colour", COLOR}, {"cone", CONE},
+      {"constant_attenuation_coeff", CONSTANT_ATTENUATION_COEFF}, {"cylinder", CYLINDER},
+      {"diffuse", DIFFUSE}, {"direction", DIRECTION}, {"directional_light", DIRECTIONAL_LIGHT},
+      {"emissive", EMISSIVE}, {"faces", FACES}, {"false", SYMFALSE}, {"fov", FOV},
+      {"gennormals", GENNORMALS}, {"height", HEIGHT}, {"index", INDEX},
+      {"linear_attenuation_coeff", LINEAR_ATTENUATION_COEFF}, {"material", MATERIAL},
+      {"materials", MATERIALS}, {"map", MAP}, {"name", NAME}, {"normals", NORMALS},
+      {"point_light", POINT_LIGHT}, {"points", POLYPOINTS}, {"polymesh", TRIMESH},
+      {"position", POSITION}, {"quadratic_attenuation_coeff", QUADRATIC_ATTENUATION_COEFF},
+      {"quaternian", QUATERNIAN}, {"reflective", REFLECTIVE}, {"rotate", ROTATE},
+      {"SBT-raytracer", SBT_RAYTRACER}, {"scale", SCALE}, {"shininess", SHININESS},
+      {"specular", SPECULAR}, {"sphere", SPHERE}, {"square", SQUARE}, {"top_radius", TOP_RADIUS},
+      {"transform", TRANSFORM}, {"translate", TRANSLATE}, {"transmissive", TRANSMISSIVE},
+      {"trimesh", TRIMESH}, {"true", SYMTRUE}, {"updir", UPDIR}, {"viewdir", VIEWDIR},
+      {"bump", BUMP}, {"gloss", GLOSS}, {"angle", ANGLE}, {"width", WIDTH}, {"radius", RADIUS},
+      {"area_light_rect", AREA_LIGHT_RECT}, {"area_light_circ", AREA_LIGHT_CIRC},
+      {"spot_light", SPOT_LIGHT}};
+  return w;
+}
+
+const char* sym_name(Sym s) {  // Token.cpp:9-92 (subset used in messages)
+  switch (s) {
+    case EOFSYM: return "EOF";
+    case SBT_RAYTRACER: return "SBT-raytracer";
+    case IDENT: return "Identifier";
+    case SCALAR: return "Scalar";
+    case LPAREN: return "Left paren";
+    case RPAREN: return "Right paren";
+    case LBRACE: return "Left brace";
+    case RBRACE: return "Right brace";
+    case COMMA: return "Comma";
+    case EQUALS: return "Equals";
+    case SEMICOLON: return "Semicolon";
+    case MATERIAL: return "material";
+    default: return "Unknown token type";
+  }
+}
+
+struct Token {
+  Sym kind = EOFSYM;
+  double value = 0.0;
+  std::string ident;
+};
+
+class Tokenizer {
+ public:
+  explicit Tokenizer(const std::string& text) {
+    // Buffer reads line by line and re-appends '\n' to every line
+    // (buffer.cpp GetLine); emulate by splitting on '\n'.
+    size_t start = 0;
+    while (start <= text.size()) {
+      size_t nl = text.find('\n', start);
+      if (nl == std::string::npos) {
+        if (start < text.size()) lines_.push_back(text.substr(start) + "\n");
+        break;
+      }
+      lines_.push_back(text.substr(start, nl - start) + "\n");
+      start = nl + 1;
+    }
+    getCh();  // CurrentCh = ' ' then first GetCh happens in SkipWhiteSpace
+  }
+
+  Token get() {
+    if (has_unget_) {
+      has_unget_ = false;
+      return unget_;
+    }
+    skipWhite();
+    Token t;
+    if (eof_) {
+      t.kind = EOFSYM;
+      return t;
+    }
+    unsigned char c = static_cast<unsigned char>(cur_);
+    if (std::isalpha(c) || cur_ == '_') {
+      std::string id;
+      while (std::isalnum(static_cast<unsigned char>(cur_)) || cur_ == '_' || cur_ == '-') {
+        id += cur_;
+        getCh();
+      }
+      auto it = reserved().find(id);
+      if (it == reserved().end()) {
+        t.kind = IDENT;
+        t.ident = id;
+      } else {
+        t.kind = it->second;
+      }
+    } else if (cur_ == '"') {
+      getCh();
+      std::string id;
+      while (cur_ != '"') {
+        if (cur_ == '\n') syntax("Unterminated string constant");
+        if (eof_) syntax("Unterminated string constant");
+        id += cur_;
+        getCh();
+      }
+      getCh();
+      t.kind = IDENT;
+      t.ident = id;
+    } else if (std::isdigit(c) || cur_ == '-' || cur_ == '.') {
+      std::string s;
+      while (std::isdigit(static_cast<unsigned char>(cur_)) || cur_ == '-' || cur_ == '.' || cur_ == 'e') {
+        s += cur_;
+        getCh();
+      }
+      t.kind = SCALAR;
+      t.value = std::atof(s.c_str());
+    } else {
+      switch (cur_) {
+        case '(': t.kind = LPAREN; break;
+        case ')': t.kind = RPAREN; break;
+        case '{': t.kind = LBRACE; break;
+        case '}': t.kind = RBRACE; break;
+        case ',': t.kind = COMMA; break;
+        case '=': t.kind = EQUALS; break;
+        case ';': t.kind = SEMICOLON; break;
+        default: {
+          std::ostringstream o;
+          o << "unexpected character: '" << cur_ << "'";
+          syntax(o.str());
+        }
+      }
+      getCh();
+    }
+    return t;
+  }
+
+  const Token& peek() {
+    Token t = get();
+    unget_ = t;
+    has_unget_ = true;
+    return unget_;
+  }
+
+  Token read(Sym kind) {
+    Token t = get();
+    if (t.kind != kind) syntax(std::string(sym_name(kind)) + " expected");
+    return t;
+  }
+
+  bool condRead(Sym kind) {
+    if (peek().kind == kind) {
+      get();
+      return true;
+    }
+    return false;
+  }
+
+  [[noreturn]] void syntax(const std::string& msg) const {
+    std::ostringstream o;
+    o << "Line " << line_ << ": syntax error: " << msg;
+    throw ParseError(o.str());
+  }
+
+ private:
+  void getCh() {
+    if (eof_) {
+      cur_ = '\0';
+      return;
+    }
+    if (li_ < lines_.size() && ci_ + 1 < lines_[li_].size() && started_) {
+      ++ci_;
+    } else if (!started_) {
+      started_ = true;
+      li_ = 0;
+      ci_ = 0;
+      if (lines_.empty()) {
+        eof_ = true;
+        cur_ = '\0';
+        return;
+      }
+    } else {
+      ++li_;
+      ci_ = 0;
+      if (li_ >= lines_.size()) {
+        eof_ = true;
+        cur_ = '\0';
+        return;
+      }
+    }
+    line_ = static_cast<int>(li_) + 1;
+    cur_ = lines_[li_][ci_];
+  }
+
+  void skipWhite() {
+    for (;;) {
+      while (!eof_ && std::isspace(static_cast<unsigned char>(cur_))) getCh();
+      if (cur_ != '/') return;
+      int startLine = line_;
+      getCh();
+      if (cur_ == '/') {
+        while (!eof_ && cur_ != '\n') getCh();
+      } else if (cur_ == '*') {
+        for (;;) {
+          getCh();
+          if (cur_ == '*') {
+            getCh();
+            if (cur_ == '/') {
+              getCh();
+              break;
+            } else if (eof_) {
+              std::ostringstream o;
+              o << "Unterminated comment in line " << startLine;
+              syntax(o.str());
+            }
+          } else if (eof_) {
+            std::ostringstream o;
+            o << "Unterminated comment in line " << startLine;
+            syntax(o.str());
+          }
+        }
+      } else {
+        std::ostringstream o;
+        o << "unexpected character: '" << cur_ << "'";
+        syntax(o.str());
+      }
+    }
+  }
+
+  std::vector<std::string> lines_;
+  size_t li_ = 0, ci_ = 0;
+  bool started_ = false;
+  bool eof_ = false;
+  char cur_ = ' ';
+  int line_ = 0;
+  Token unget_;
+  bool has_unget_ = false;
+};
+
+// ---------------------------------------------------------------- Parser
+class Parser {
+ public:
+  Parser(Tokenizer& tk, const std::string& base) : tk_(tk), base_(base) {}
+
+  SceneModel parseScene() {  // Parser.cpp:26-95
+    sc_.base_path = base_;
+    tk_.read(SBT_RAYTRACER);
+    Token ver = tk_.read(SCALAR);
+    if (ver.value > 1.1) {
+      std::ostringstream o;
+      o << "Parser: fatal exception SBT-raytracer version number " << ver.value
+        << " too high; only able to parse v1.1 and below.";
+      throw ParseError(o.str());
+    }
+    Material mat;  // root material: Material() (Parser.cpp:39)
+    for (;;) {
+      switch (tk_.peek().kind) {
+        case SPHERE: case BOX: case SQUARE: case CYLINDER: case CONE: case TRIMESH:
+        case TRANSLATE: case ROTATE: case SCALE: case TRANSFORM: case LBRACE:
+          parseTransformableElement(nullptr, mat);
+          break;
+        case POINT_LIGHT: sc_.lights.push_back(parsePointLight()); break;
+        case DIRECTIONAL_LIGHT: sc_.lights.push_back(parseDirectionalLight()); break;
+        case AREA_LIGHT_RECT: sc_.lights.push_back(parseAreaLightRect()); break;
+        case AREA_LIGHT_CIRC: sc_.lights.push_back(parseAreaLightCirc()); break;
+        case SPOT_LIGHT: sc_.lights.push_back(parseSpotLight()); break;
+        case AMBIENT_LIGHT: parseAmbientLight(); break;
+        case CAMERA: parseCamera(); break;
+        case MATERIAL: mat = parseMaterialExpression(mat); break;
+        case SEMICOLON: tk_.read(SEMICOLON); break;
+        case EOFSYM: return std::move(sc_);
+        default: tk_.syntax("Expected: geometry, camera, or light information");
+      }
+    }
+  }
+
+ private:
+  // ------------------------------------------------------------ camera
+  void parseCamera() {  // Parser.cpp:97-154
+    bool hasViewDir = false, hasUpDir = false;
+    dvec3 viewDir{0, 0, 0}, upDir{0, 0, 0};
+    tk_.read(CAMERA);
+    tk_.read(LBRACE);
+    for (;;) {
+      switch (tk_.peek().kind) {
+        case POSITION: sc_.camera.eye = parseVec3dExpression(); break;
+        case FOV: sc_.camera.setFOV(parseScalarExpression()); break;
+        case QUATERNIAN: {
+          double q[4];
+          parseVec4dExpression(q);
+          sc_.camera.setLookQuat(q[0], q[1], q[2], q[3]);
+          break;
+        }
+        case ASPECTRATIO: sc_.camera.setAspectRatio(parseScalarExpression()); break;
+        case VIEWDIR: viewDir = parseVec3dExpression(); hasViewDir = true; break;
+        case UPDIR: upDir = parseVec3dExpression(); hasUpDir = true; break;
+        case RBRACE:
+          if (hasViewDir) {
+            if (!hasUpDir) tk_.syntax("Expected: 'updir'");
+            sc_.camera.setLook(viewDir, upDir);
+          } else if (hasUpDir) {
+            tk_.syntax("Expected: 'viewdir'");
+          }
+          tk_.read(RBRACE);
+          return;
+        default: tk_.syntax("Expected: camera attribute");
+      }
+    }
+  }
+
+  // ------------------------------------------------------------ geometry
+  void parseTransformableElement(const Transform* tf, const Material& mat) {
+    switch (tk_.peek().kind) {
+      case SPHERE: case BOX: case SQUARE: case CYLINDER: case CONE: case TRIMESH:
+      case TRANSLATE: case ROTATE: case SCALE: case TRANSFORM:
+        parseGeometry(tf, mat);
+        break;
+      case LBRACE: parseGroup(tf, mat); break;
+      default: tk_.syntax("Expected: transformable element");
+    }
+  }
+
+  void parseGroup(const Transform* tf, const Material& mat) {  // Parser.cpp:180-211
+    tk_.read(LBRACE);
+    for (;;) {
+      switch (tk_.peek().kind) {
+        case SPHERE: case BOX: case SQUARE: case CYLINDER: case CONE: case TRIMESH:
+        case TRANSLATE: case ROTATE: case SCALE: case TRANSFORM: case LBRACE:
+          parseTransformableElement(tf, mat);
+          break;
+        case RBRACE: tk_.read(RBRACE); return;
+        case MATERIAL:
+          // U19: the reference parses the material, then falls through into
+          // the default branch and throws (Parser.cpp:202-208).
+          parseMaterialExpression(mat);
+          tk_.syntax("Expected: '}' or geometry");
+        default: tk_.syntax("Expected: '}' or geometry");
+      }
+    }
+  }
+
+  void parseGeometry(const Transform* tf, const Material& mat) {
+    switch (tk_.peek().kind) {
+      case SPHERE: parseSimple(tf, mat, SPHERE, OBJ_SPHERE, "sphere"); return;
+      case BOX: parseSimple(tf, mat, BOX, OBJ_BOX, "box"); return;
+      case SQUARE: parseSimple(tf, mat, SQUARE, OBJ_SQUARE, "square"); return;
+      case CYLINDER: parseSimple(tf, mat, CYLINDER, OBJ_CYLINDER, "cylinder"); return;
+      case CONE: parseCone(tf, mat); return;
+      case TRIMESH: parseTrimesh(tf, mat); return;
+      case TRANSLATE: parseTranslate(tf, mat); return;
+      case ROTATE: parseRotate(tf, mat); return;
+      case SCALE: parseScale(tf, mat); return;
+      case TRANSFORM: parseTransform(tf, mat); return;
+      default: throw ParseError("Parser: fatal exception Unrecognized geometry type.");
+    }
+  }
+
+  // Each transform node is created before the child is parsed and lives for
+  // the whole parse (TransformNode::createChild, scene.h:85-90).
+  const Transform* child(const Transform* parent, const Mat4& local) {
+    nodes_.emplace_back(new Transform(make_transform(parent, local)));
+    return nodes_.back().get();
+  }
+  const Transform* rootOr(const Transform* tf) {
+    if (tf) return tf;
+    if (!root_) root_.reset(new Transform(make_transform(nullptr, mat4_identity())));
+    return root_.get();
+  }
+
+  void parseTranslate(const Transform* tf, const Material& mat) {
+    tk_.read(TRANSLATE);
+    tk_.read(LPAREN);
+    double x = parseScalar(); tk_.read(COMMA);
+    double y = parseScalar(); tk_.read(COMMA);
+    double z = parseScalar(); tk_.read(COMMA);
+    parseTransformableElement(child(rootOr(tf), mat4_translate(mk3(x, y, z))), mat);
+    tk_.read(RPAREN);
+    tk_.condRead(SEMICOLON);
+  }
+
+  void parseRotate(const Transform* tf, const Material& mat) {
+    tk_.read(ROTATE);
+    tk_.read(LPAREN);
+    double x = parseScalar(); tk_.read(COMMA);
+    double y = parseScalar(); tk_.read(COMMA);
+    double z = parseScalar(); tk_.read(COMMA);
+    double w = parseScalar(); tk_.read(COMMA);
+    parseTransformableElement(child(rootOr(tf), mat4_rotate(w, mk3(x, y, z))), mat);
+    tk_.read(RPAREN);
+    tk_.condRead(SEMICOLON);
+  }
+
+  void parseScale(const Transform* tf, const Material& mat) {
+    tk_.read(SCALE);
+    tk_.read(LPAREN);
+    double x = parseScalar(), y, z;
+    tk_.read(COMMA);
+    if (tk_.peek().kind == SCALAR) {
+      y = parseScalar(); tk_.read(COMMA);
+      z = parseScalar(); tk_.read(COMMA);
+    } else {
+      y = x;
+      z = x;
+    }
+    parseTransformableElement(child(rootOr(tf), mat4_scale(mk3(x, y, z))), mat);
+    tk_.read(RPAREN);
+    tk_.condRead(SEMICOLON);
+  }
+
+  void parseTransform(const Transform* tf, const Material& mat) {
+    tk_.read(TRANSFORM);
+    tk_.read(LPAREN);
+    double rows[4][4];
+    for (int r = 0; r < 4; ++r) {
+      parseVec4d(rows[r]);
+      tk_.read(COMMA);
+    }
+    // glm::transpose(dmat4x4(row1..row4)): dmat4x4 takes the rows as columns
+    Mat4 a;
+    for (int c = 0; c < 4; ++c)
+      for (int r = 0; r < 4; ++r) a.m[c * 4 + r] = rows[c][r];
+    parseTransformableElement(child(rootOr(tf), mat4_transpose(a)), mat);
+    tk_.read(RPAREN);
+    tk_.condRead(SEMICOLON);
+  }
+
+  // sphere / box / square / cylinder (Parser.cpp:348-470)
+  void parseSimple(const Transform* tf, const Material& mat, Sym kw, int type, const char* what) {
+    tk_.read(kw);
+    tk_.read(LBRACE);
+    bool haveMat = false;
+    Material newMat;
+    for (;;) {
+      switch (tk_.peek().kind) {
+        case MATERIAL: newMat = parseMaterialExpression(mat); haveMat = true; break;
+        case NAME: parseIdentExpression(); break;
+        case RBRACE: {
+          tk_.read(RBRACE);
+          Object o;
+          o.type = type;
+          o.tf = *rootOr(tf);
+          addObject(o, haveMat ? newMat : mat);
+          return;
+        }
+        default: tk_.syntax(std::string("Expected: ") + what + " attributes");
+      }
+    }
+  }
+
+  void parseCone(const Transform* tf, const Material& mat) {  // Parser.cpp:472-518
+    tk_.read(CONE);
+    tk_.read(LBRACE);
+    for (;;) {
+      switch (tk_.peek().kind) {
+        case MATERIAL: parseMaterialExpression(mat); break;
+        case NAME: parseIdentExpression(); break;
+        case CAPPED: parseBooleanExpression(); break;
+        case BOTTOM_RADIUS: case TOP_RADIUS: case HEIGHT: parseScalarExpression(); break;
+        case RBRACE:
+          tk_.read(RBRACE);
+          (void)tf;
+          throw ParseError("Parser: fatal exception cone primitives are not supported by this build (SURVEY 8(f) rank 2)");
+        default: tk_.syntax("Expected: cone attributes");
+      }
+    }
+  }
+
+  // local bounds + world box (scene.cpp:78-116)
+  void addObject(Object& o, const Material& m) {
+    dvec3 lmin, lmax;
+    bool empty = false;
+    switch (o.type) {
+      case OBJ_SPHERE: lmin = mk3(-1, -1, -1); lmax = mk3(1, 1, 1); break;
+      case OBJ_BOX: lmin = mk3(-0.5, -0.5, -0.5); lmax = mk3(0.5, 0.5, 0.5); break;
+      case OBJ_CYLINDER: lmin = mk3(-1, -1, 0); lmax = mk3(1, 1, 1); break;
+      case OBJ_SQUARE: lmin = mk3(-0.5, -0.5, -0.00000001); lmax = mk3(0.5, 0.5, 0.00000001); break;
+      case OBJ_TRIMESH: {
+        const Mesh& me = sc_.meshes[o.mesh];
+        lmin = me.lmin;
+        lmax = me.lmax;
+        empty = me.lbox_empty;
+        break;
+      }
+      default: lmin = lmax = mk3(0, 0, 0);
+    }
+    (void)empty;  // an empty local box still yields corners at (0,0,0)
+    const dvec3 c[8] = {mk3(lmin.x, lmin.y, lmin.z), mk3(lmax.x, lmin.y, lmin.z),
+                        mk3(lmin.x, lmax.y, lmin.z), mk3(lmax.x, lmax.y, lmin.z),
+                        mk3(lmin.x, lmin.y, lmax.z), mk3(lmax.x, lmin.y, lmax.z),
+                        mk3(lmin.x, lmax.y, lmax.z), mk3(lmax.x, lmax.y, lmax.z)};
+    double nmax[4], nmin[4];
+    for (int k = 0; k < 8; ++k) {
+      double in[4] = {c[k].x, c[k].y, c[k].z, 1.0}, v[4];
+      mat4_mul_vec4(o.tf.xform, in, v);
+      if (k == 0) {
+        for (int a = 0; a < 4; ++a) nmax[a] = nmin[a] = v[a];
+      } else {
+        for (int a = 0; a < 4; ++a) {
+          nmax[a] = rtm::gmax(nmax[a], v[a]);
+          nmin[a] = rtm::gmin(nmin[a], v[a]);
+        }
+      }
+    }
+    o.wmax = mk3(nmax[0], nmax[1], nmax[2]);
+    o.wmin = mk3(nmin[0], nmin[1], nmin[2]);
+    o.material = static_cast<int>(sc_.materials.size());
+    sc_.materials.push_back(m);
+    sc_.objects.push_back(o);
+  }
+
+  void parseTrimesh(const Transform* tf, const Material& mat) {  // Parser.cpp:520-653
+    Material meshMat = mat;
+    tk_.read(TRIMESH);
+    tk_.read(LBRACE);
+    bool genNormals = false;
+    std::list<std::array<double, 3>> faces;
+    Mesh me;
+    std::vector<Material> vmats;
+    for (;;) {
+      switch (tk_.peek().kind) {
+        case GENNORMALS: tk_.read(GENNORMALS); tk_.read(SEMICOLON); genNormals = true; break;
+        case MATERIAL: meshMat = parseMaterialExpression(mat); break;
+        case NAME: parseIdentExpression(); break;
+        case MATERIALS:
+          tk_.read(MATERIALS); tk_.read(EQUALS); tk_.read(LPAREN);
+          if (tk_.peek().kind != RPAREN) {
+            vmats.push_back(parseMaterial(meshMat));
+            for (;;) {
+              if (tk_.peek().kind == RPAREN) break;
+              tk_.read(COMMA);
+              vmats.push_back(parseMaterial(meshMat));
+            }
+          }
+          tk_.read(RPAREN); tk_.read(SEMICOLON);
+          break;
+        case NORMALS:
+          tk_.read(NORMALS); tk_.read(EQUALS); tk_.read(LPAREN);
+          if (tk_.peek().kind != RPAREN) {
+            me.normals.push_back(parseVec3d());
+            for (;;) {
+              if (tk_.peek().kind == RPAREN) break;
+              tk_.read(COMMA);
+              me.normals.push_back(parseVec3d());
+            }
+          }
+          tk_.read(RPAREN); tk_.read(SEMICOLON);
+          break;
+        case FACES:
+          tk_.read(FACES); tk_.read(EQUALS); tk_.read(LPAREN);
+          if (tk_.peek().kind != RPAREN) {
+            parseFaces(faces);
+            for (;;) {
+              if (tk_.peek().kind == RPAREN) break;
+              tk_.read(COMMA);
+              parseFaces(faces);
+            }
+          }
+          tk_.read(RPAREN); tk_.read(SEMICOLON);
+          break;
+        case POLYPOINTS:
+          tk_.read(POLYPOINTS); tk_.read(EQUALS); tk_.read(LPAREN);
+          if (tk_.peek().kind != RPAREN) {
+            me.verts.push_back(parseVec3d());
+            for (;;) {
+              if (tk_.peek().kind == RPAREN) break;
+              tk_.read(COMMA);
+              me.verts.push_back(parseVec3d());
+            }
+          }
+          tk_.read(RPAREN); tk_.read(SEMICOLON);
+          break;
+        case RBRACE: {
+          tk_.read(RBRACE);
+          const int vcnt = static_cast<int>(me.verts.size());
+          for (const auto& f : faces) {
+            int a = static_cast<int>(f[0]), b = static_cast<int>(f[1]), c = static_cast<int>(f[2]);
+            if (a >= vcnt || b >= vcnt || c >= vcnt || a < 0 || b < 0 || c < 0) {
+              std::ostringstream o;
+              o << "Parser: fatal exception Bad face in trimesh: (" << f[0] << ", " << f[1] << ", " << f[2] << ")";
+              throw ParseError(o.str());
+            }
+            addFace(me, a, b, c);
+          }
+          if (genNormals) generateNormals(me);
+          if (!vmats.empty() && vmats.size() != me.verts.size())
+            throw ParseError("Parser: fatal exception Bad Trimesh: Wrong number of materials.");
+          if (!me.normals.empty() && me.normals.size() != me.verts.size())
+            throw ParseError("Parser: fatal exception Bad Trimesh: Wrong number of normals.");
+          me.vmats = vmats;
+          // ComputeLocalBoundingBox (trimesh.h:63-80)
+          if (!me.verts.empty()) {
+            me.lmax = me.verts[0];
+            me.lmin = me.verts[0];
+            for (const auto& v : me.verts) {
+              me.lmax = rtm::gmax3(me.lmax, v);
+              me.lmin = rtm::gmin3(me.lmin, v);
+            }
+            me.lbox_empty = false;
+          }
+          Object o;
+          o.type = OBJ_TRIMESH;
+          o.tf = *rootOr(tf);
+          o.mesh = static_cast<int>(sc_.meshes.size());
+          sc_.meshes.push_back(std::move(me));
+          addObject(o, meshMat);
+          return;
+        }
+        default: tk_.syntax("Expected: trimesh attributes");
+      }
+    }
+  }
+
+  // TrimeshFace ctor + Trimesh::addFace (trimesh.h:100-130, trimesh.cpp:38-56)
+  static void addFace(Mesh& me, int a, int b, int c) {
+    const dvec3 A = me.verts[a], B = me.verts[b], C = me.verts[c];
+    dvec3 vab = B - A, vac = C - A, vcb = B - C;
+    if (rtm::length(vab) == 0.0 || rtm::length(vac) == 0.0 || rtm::length(vcb) == 0.0) return;  // degen
+    dvec3 n = rtm::normalize(rtm::cross(B - A, C - A));
+    // ComputeLocalBoundingBox (trimesh.h:149-161)
+    dvec3 bmax = rtm::gmax3(A, B), bmin = rtm::gmin3(A, B);
+    bmax = rtm::gmax3(C, bmax);
+    bmin = rtm::gmin3(C, bmin);
+    me.faces.push_back({a, b, c});
+    me.face_normals.push_back(n);
+    me.face_boxes.push_back({bmin, bmax});
+  }
+
+  static void generateNormals(Mesh& me) {  // trimesh.cpp:192-217
+    const size_t cnt = me.verts.size();
+    me.normals.resize(cnt, dvec3{0, 0, 0});
+    std::vector<int> numFaces(cnt, 0);
+    for (size_t f = 0; f < me.faces.size(); ++f) {
+      for (int i = 0; i < 3; ++i) {
+        me.normals[me.faces[f][i]] += me.face_normals[f];
+        ++numFaces[me.faces[f][i]];
+      }
+    }
+    for (size_t i = 0; i < cnt; ++i)
+      if (numFaces[i]) me.normals[i] = me.normals[i] / static_cast<double>(numFaces[i]);
+  }
+
+  void parseFaces(std::list<std::array<double, 3>>& faces) {  // Parser.cpp:655-671
+    std::list<double> pts = parseScalarList();
+    if (pts.size() < 3) tk_.syntax("Faces must have at least 3 vertices.");
+    auto it = pts.begin();
+    double a = *it++;
+    double b = *it++;
+    while (it != pts.end()) {
+      double c = *it++;
+      faces.push_back({a, b, c});
+      b = c;
+    }
+  }
+
+  // ------------------------------------------------------------ lights
+  void parseAmbientLight() {
+    tk_.read(AMBIENT_LIGHT);
+    tk_.read(LBRACE);
+    if (tk_.peek().kind != COLOR) tk_.syntax("Expected color attribute");
+    sc_.ambient += parseVec3dExpression();
+    tk_.read(RBRACE);
+  }
+
+  Light parsePointLight() {  // Parser.cpp:688-746
+    Light L;
+    L.type = L_POINT;
+    float c = 0.0f, l = 0.0f, q = 1.0f;
+    bool hasPos = false, hasCol = false;
+    tk_.read(POINT_LIGHT);
+    tk_.read(LBRACE);
+    for (;;) {
+      switch (tk_.peek().kind) {
+        case POSITION:
+          if (hasPos) tk_.syntax("Repeated 'position' attribute");
+          L.pos = parseVec3dExpression(); hasPos = true; break;
+        case COLOR:
+          if (hasCol) tk_.syntax("Repeated 'color' attribute");
+          L.color = parseVec3dExpression(); hasCol = true; break;
+        case CONSTANT_ATTENUATION_COEFF: c = static_cast<float>(parseScalarExpression()); break;
+        case LINEAR_ATTENUATION_COEFF: l = static_cast<float>(parseScalarExpression()); break;
+        case QUADRATIC_ATTENUATION_COEFF: q = static_cast<float>(parseScalarExpression()); break;
+        case RBRACE:
+          if (!hasCol) tk_.syntax("Expected: 'color'");
+          if (!hasPos) tk_.syntax("Expected: 'position'");
+          tk_.read(RBRACE);
+          L.c = c; L.l = l; L.q = q;
+          return L;
+        default:
+          tk_.syntax("expecting 'position' or 'color' attribute, or 'constant_attenuation_coeff', "
+                     "'linear_attenuation_coeff', or 'quadratic_attenuation_coeff'");
+      }
+    }
+  }
+
+  Light parseDirectionalLight() {  // Parser.cpp:748-787
+    Light L;
+    L.type = L_DIRECTIONAL;
+    bool hasDir = false, hasCol = false;
+    dvec3 dir{0, 0, 0};
+    tk_.read(DIRECTIONAL_LIGHT);
+    tk_.read(LBRACE);
+    for (;;) {
+      switch (tk_.peek().kind) {
+        case DIRECTION:
+          if (hasDir) tk_.syntax("Repeated 'direction' attribute");
+          dir = parseVec3dExpression(); hasDir = true; break;
+        case COLOR:
+          if (hasCol) tk_.syntax("Repeated 'color' attribute");
+          L.color = parseVec3dExpression(); hasCol = true; break;
+        case RBRACE:
+          if (!hasCol) tk_.syntax("Expected: 'color'");
+          if (!hasDir) tk_.syntax("Expected: 'position'");
+          tk_.read(RBRACE);
+          L.orient = rtm::normalize(dir);  // DirectionalLight ctor (light.h:39-40)
+          return L;
+        default: tk_.syntax("expecting 'position' or 'color' attribute");
+      }
+    }
+  }
+
+  // Shared attribute loop for the area / spot lights (Parser.cpp:790-1058).
+  Light parseAreaLike(Sym kw, int type) {
+    Light L;
+    L.type = type;
+    float c = 0.0f, l = 0.0f, q = 1.0f;
+    bool hasPos = false, hasCol = false, hasDir = false, hasRadius = false, hasAngle = false,
+         hasW = false, hasH = false, hasUp = false;
+    dvec3 dir{0, 0, 0}, up{0, 0, 0};
+    tk_.read(kw);
+    tk_.read(LBRACE);
+    for (;;) {
+      Sym k = tk_.peek().kind;
+      switch (k) {
+        case DIRECTION:
+          if (hasDir) tk_.syntax("Repeated 'direction' attribute");
+          dir = parseVec3dExpression(); hasDir = true; break;
+        case POSITION:
+          if (hasPos) tk_.syntax("Repeated 'position' attribute");
+          L.pos = parseVec3dExpression(); hasPos = true; break;
+        case COLOR:
+          if (hasCol) tk_.syntax("Repeated 'color' attribute");
+          L.color = parseVec3dExpression(); hasCol = true; break;
+        case CONSTANT_ATTENUATION_COEFF: c = static_cast<float>(parseScalarExpression()); break;
+        case LINEAR_ATTENUATION_COEFF: l = static_cast<float>(parseScalarExpression()); break;
+        case QUADRATIC_ATTENUATION_COEFF: q = static_cast<float>(parseScalarExpression()); break;
+        case RADIUS:
+          if (type == L_AREA_RECT) goto bad;
+          if (hasRadius) tk_.syntax("Repeated 'radius' attribute");
+          L.radius = parseScalarExpression(); hasRadius = true; break;
+        case ANGLE:
+          if (type != L_SPOT) goto bad;
+          if (hasAngle) tk_.syntax("Repeated 'angle' attribute");
+          L.angle = parseScalarExpression(); hasAngle = true; break;
+        case WIDTH:
+          if (type != L_AREA_RECT) goto bad;
+          if (hasW) tk_.syntax("Repeated 'width' attribute");
+          L.width = parseScalarExpression(); hasW = true; break;
+        case HEIGHT:
+          if (type != L_AREA_RECT) goto bad;
+          if (hasH) tk_.syntax("Repeated 'height' attribute");
+          L.height = parseScalarExpression(); hasH = true; break;
+        case UPDIR:
+          if (type != L_AREA_RECT) goto bad;
+          if (hasUp) tk_.syntax("Repeated 'updir' attribute");
+          up = parseVec3dExpression(); hasUp = true; break;
+        case RBRACE: {
+          if (type == L_AREA_RECT) {
+            if (!hasW) tk_.syntax("Expected: 'width'");
+            if (!hasH) tk_.syntax("Expected: 'height'");
+            if (!hasUp) tk_.syntax("Expected: 'updir'");
+          }
+          if (type == L_SPOT && !hasAngle) tk_.syntax("Expected: 'angle'");
+          if (type != L_AREA_RECT && !hasRadius) tk_.syntax("Expected: 'radius'");
+          if (!hasCol) tk_.syntax("Expected: 'color'");
+          if (!hasPos) tk_.syntax("Expected: 'position'");
+          if (!hasDir) tk_.syntax("Expected: 'direction'");
+          tk_.read(RBRACE);
+          L.c = c; L.l = l; L.q = q;
+          L.orient = rtm::normalize(dir);  // AreaLight ctor (light.h:102-104)
+          if (type == L_AREA_RECT) {
+            // AreaLightRect ctor (light.h:120-127): u(normalize(u)),
+            // v(cross(ori, u)) where ori/u are the constructor PARAMETERS.
+            L.u = rtm::normalize(up);
+            L.v = rtm::cross(dir, up);
+          }
+          if (type == L_SPOT) {
+            // SpotLight ctor (light.h:153-155), PI from util.h
+            const double PI = 3.1415926535897932384626433832795028841971;
+            L.ang_tan = std::tan(L.angle / 360 * PI);
+            L.offset = L.ang_tan * L.radius;
+          }
+          return L;
+        }
+        default:
+        bad:
+          tk_.syntax("expecting 'position' or 'color' attribute, or 'constant_attenuation_coeff', "
+                     "'linear_attenuation_coeff', or 'quadratic_attenuation_coeff'");
+      }
+    }
+  }
+  Light parseAreaLightRect() { return parseAreaLike(AREA_LIGHT_RECT, L_AREA_RECT); }
+  Light parseAreaLightCirc() { return parseAreaLike(AREA_LIGHT_CIRC, L_AREA_CIRC); }
+  Light parseSpotLight() { return parseAreaLike(SPOT_LIGHT, L_SPOT); }
+
+  // ------------------------------------------------------------ values
+  double parseScalarExpression() {
+    tk_.get();
+    tk_.read(EQUALS);
+    double v = parseScalar();
+    tk_.condRead(SEMICOLON);
+    return v;
+  }
+  bool parseBooleanExpression() {
+    tk_.get();
+    tk_.read(EQUALS);
+    Sym k = tk_.peek().kind;
+    bool v;
+    if (k == SYMTRUE) { tk_.read(SYMTRUE); v = true; }
+    else if (k == SYMFALSE) { tk_.read(SYMFALSE); v = false; }
+    else tk_.syntax("Expected boolean");
+    tk_.condRead(SEMICOLON);
+    return v;
+  }
+  dvec3 parseVec3dExpression() {
+    tk_.get();
+    tk_.read(EQUALS);
+    dvec3 v = parseVec3d();
+    tk_.condRead(SEMICOLON);
+    return v;
+  }
+  void parseVec4dExpression(double out[4]) {
+    tk_.get();
+    tk_.read(EQUALS);
+    parseVec4d(out);
+    tk_.condRead(SEMICOLON);
+  }
+  std::string parseIdentExpression() {
+    tk_.get();
+    tk_.read(EQUALS);
+    std::string s = tk_.read(IDENT).ident;
+    tk_.condRead(SEMICOLON);
+    return s;
+  }
+  double parseScalar() { return tk_.read(SCALAR).value; }
+  std::list<double> parseScalarList() {
+    std::list<double> r;
+    tk_.read(LPAREN);
+    if (tk_.peek().kind != RPAREN) {
+      r.push_back(parseScalar());
+      for (;;) {
+        if (tk_.peek().kind == RPAREN) break;
+        tk_.read(COMMA);
+        r.push_back(parseScalar());
+      }
+    }
+    tk_.read(RPAREN);
+    return r;
+  }
+  dvec3 parseVec3d() {
+    tk_.read(LPAREN);
+    double a = tk_.read(SCALAR).value; tk_.read(COMMA);
+    double b = tk_.read(SCALAR).value; tk_.read(COMMA);
+    double c = tk_.read(SCALAR).value;
+    tk_.read(RPAREN);
+    return mk3(a, b, c);
+  }
+  void parseVec4d(double out[4]) {
+    tk_.read(LPAREN);
+    for (int i = 0; i < 4; ++i) {
+      out[i] = tk_.read(SCALAR).value;
+      if (i < 3) tk_.read(COMMA);
+    }
+    tk_.read(RPAREN);
+  }
+
+  // ------------------------------------------------------------ materials
+  Material parseMaterialExpression(const Material& parent) {  // Parser.cpp:1095-1101
+    tk_.read(MATERIAL);
+    tk_.read(EQUALS);
+    Material m = parseMaterial(parent);
+    tk_.condRead(SEMICOLON);
+    return m;
+  }
+
+  Material parseMaterial(const Material& parent) {  // Parser.cpp:1188-1274
+    if (tk_.peek().kind == IDENT) {
+      // U19: returns a copy of the named material WITHOUT consuming the
+      // identifier; the caller then trips over it.
+      auto it = named_.find(tk_.peek().ident);
+      return it == named_.end() ? Material() : it->second;
+    }
+    tk_.read(LBRACE);
+    Material m = parent;
+    std::string name;
+    for (;;) {
+      switch (tk_.peek().kind) {
+        case EMISSIVE: m.p[P_KE] = parseVec3Param(); break;
+        case AMBIENT: m.p[P_KA] = parseVec3Param(); break;
+        case SPECULAR: m.p[P_KS] = parseVec3Param(); break;          // no setBools (material.h:233)
+        case DIFFUSE: m.p[P_KD] = parseVec3Param(); break;
+        case REFLECTIVE: m.p[P_KR] = parseVec3Param(); m.setBools(); break;
+        case TRANSMISSIVE: m.p[P_KT] = parseVec3Param(); m.setBools(); break;
+        case INDEX: m.p[P_INDEX] = parseScalarParam(); break;
+        case SHININESS: m.p[P_SHININESS] = parseScalarParam(); break;
+        case GLOSS: m.p[P_GLOSS] = parseScalarParam(); break;
+        case BUMP: m.p[P_BUMP] = parseVec3Param(); break;
+        case NAME:
+          tk_.read(NAME);
+          name = tk_.read(IDENT).ident;
+          tk_.read(SEMICOLON);
+          break;
+        case RBRACE:
+          tk_.read(RBRACE);
+          if (!name.empty()) {
+            if (named_.find(name) == named_.end()) {
+              named_[name] = m;
+            } else {
+              tk_.syntax("Redefinition of material '" + name + "'.");
+            }
+          }
+          return m;
+        default: tk_.syntax("Expected: material attribute");
+      }
+    }
+  }
+
+  MatParam parseVec3Param() {  // Parser.cpp:1276-1292
+    tk_.get();
+    tk_.read(EQUALS);
+    MatParam q;
+    if (tk_.condRead(MAP)) {
+      tk_.read(LPAREN);
+      std::string fn = base_ + "/" + tk_.read(IDENT).ident;
+      tk_.read(RPAREN);
+      tk_.condRead(SEMICOLON);
+      q.tex = texture(fn);
+    } else {
+      q.v = parseVec3d();
+      tk_.condRead(SEMICOLON);
+    }
+    return q;
+  }
+
+  MatParam parseScalarParam() {  // Parser.cpp:1294-1308 (no base path for maps)
+    tk_.get();
+    tk_.read(EQUALS);
+    MatParam q;
+    if (tk_.condRead(MAP)) {
+      tk_.read(LPAREN);
+      std::string fn = tk_.read(IDENT).ident;
+      tk_.read(RPAREN);
+      tk_.condRead(SEMICOLON);
+      q.tex = texture(fn);
+    } else {
+      double s = parseScalar();
+      q.v = mk3(s, s, s);
+      tk_.condRead(SEMICOLON);
+    }
+    return q;
+  }
+
+  // Scene::getTexture cache + TextureMap ctor (scene.cpp:199-206, material.cpp:70-81)
+  int texture(const std::string& fn) {
+    auto it = tex_cache_.find(fn);
+    if (it != tex_cache_.end()) return it->second;
+    Texture t;
+    t.path = fn;
+    t.data = read_image(fn, t.width, t.height);
+    if (t.data.empty())
+      throw ParseError("Texture mapping exception: Unable to load texture map '" + fn + "'.");
+    int id = static_cast<int>(sc_.textures.size());
+    sc_.textures.push_back(std::move(t));
+    tex_cache_[fn] = id;
+    return id;
+  }
+
+  Tokenizer& tk_;
+  std::string base_;
+  SceneModel sc_;
+  std::map<std::string, Material> named_;
+  std::map<std::string, int> tex_cache_;
+  std::vector<std::unique_ptr<Transform>> nodes_;
+  std::unique_ptr<Transform> root_;
+};
+
+}  // namespace
+
+SceneModel parse_ray_text(const std::string& text, const std::string& base_path) {
+  Tokenizer tk(text);
+  Parser p(tk, base_path);
+  return p.parseScene();
+}
+
+SceneModel load_ray_file(const std::string& path) {  // RayTracer::loadScene (RayTracer.cpp:196-240)
+  std::ifstream ifs(path, std::ios::binary);
+  if (!ifs) throw ParseError("Error: couldn't read scene file " + path);
+  std::stringstream ss;
+  ss << ifs.rdbuf();
+  std::string base;
+  size_t slash = path.find_last_of("\\/");
+  base = (slash == std::string::npos) ? std::string(".") : path.substr(0, slash);
+  return parse_ray_text(ss.str(), base);
+}
+
+}  // namespace rtxh

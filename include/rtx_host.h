@@ -1,0 +1,49 @@
+/*
+ * rtx_host.h — C ABI of librtx_host.so: host-side scene loading for the
+ * MI355X hot path.  Replaces RayTracer::loadScene (ray/src/RayTracer.cpp:
+ * 196-240: Tokenizer + Parser::parseScene, Parser.cpp:26-95), the BVH
+ * builds done at load time (Scene::conclude, scene/scene.cpp:145-153;
+ * Trimesh::conclude, SceneObjects/trimesh.cpp:69-77) and the image writer
+ * used by CommandLineUI::run (fileio/images.cc:59-68).
+ *
+ * rtx_host_load parses a .ray file, builds both BVH levels exactly like
+ * KdTree<T> (scene/kdTree.h:27-78) and flattens the scene into the
+ * RtxSceneDesc layout of rtx.h, ready for rtx_scene_create.
+ */
+#ifndef RTX_HOST_H_
+#define RTX_HOST_H_
+
+#include <stdint.h>
+#include "rtx.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct RtxHostInfo {
+  int32_t n_objects, n_lights, n_meshes, n_faces, n_textures;
+  int32_t n_scene_nodes, n_mesh_nodes;
+  int32_t scene_depth, mesh_depth;
+  int32_t n_cones, n_area_lights;
+  double aspect;                  /* RayTracer::aspectRatio (RayTracer.cpp:191-194) */
+  uint64_t scene_bvh_hash;        /* FNV-1a over DFS pre-order node boxes + leaf items */
+  uint64_t mesh_bvh_hash;         /* same over every mesh BVH, in object order       */
+} RtxHostInfo;
+
+const char* rtx_host_last_error(void);
+/* Parse + build + flatten.  On error returns RTX_ERR_INVALID and the
+ * message RayTracer::loadScene would alert (rtx_host_last_error). */
+rtx_status rtx_host_load(const char* ray_path, void** handle);
+rtx_status rtx_host_desc(void* handle, RtxSceneDesc* desc);   /* pointers into handle */
+rtx_status rtx_host_info(void* handle, RtxHostInfo* info);
+rtx_status rtx_host_free(void* handle);
+/* writeImage (fileio/images.cc:59-68): .png / .bmp by extension, RGB8 with
+ * buffer row 0 at the bottom. */
+rtx_status rtx_write_image(const char* path, int32_t w, int32_t h, const uint8_t* rgb);
+/* height the CLI derives from -w (CommandLineUI.cpp:156) */
+int32_t rtx_image_height(int32_t width, double aspect);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* RTX_HOST_H_ */

@@ -1,0 +1,1305 @@
+// oracle.cpp — CPU restatement of the reference's per-pixel ray-trace path.
+//
+// TEST INFRASTRUCTURE (see oracle.h).  Structure deliberately follows the
+// reference, not the GPU design: pointer-based KdTree, exhaustive candidate
+// lists, virtual primitives, recursive traceRay, std::sort'ed shadow hit
+// lists, OpenMP collapse(2) pixel loop.  Every function cites the reference
+// file:line it restates (paths relative to /root/reference/ray/src).
+// Arithmetic uses rt_math.h (glm 0.9.8 operation order); build with
+// -ffp-contract=off.
+#include "oracle.h"
+
+#include <omp.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <memory>
+#include <numeric>
+#include <string>
+#include <vector>
+
+#include "../cs378hgraphics-raytracer_amd/csrc/host/scene_model.h"
+
+using rtm::dvec2;
+using rtm::dvec3;
+using rtm::mk3;
+
+namespace orc {
+
+const double RAY_EPSILON = 0.00000001;                            // scene/ray.h:136
+const double PI = 3.1415926535897932384626433832795028841971;     // util.h:11
+const double EPS_BACKUP = 0.0000000001;                           // light.cpp:13
+
+thread_local std::string g_err;
+
+// ---------------------------------------------------------------- counters
+struct Counters {
+  int64_t camera = 0, secondary = 0, shadow = 0, nodes = 0, objects = 0, tris = 0, shades = 0;
+};
+thread_local Counters tl;
+
+// ---------------------------------------------------------------- ray / isect (scene/ray.h)
+struct Ray {
+  dvec3 p, d;
+  Ray(const dvec3& pp, const dvec3& dd) : p(pp), d(dd) {}
+  dvec3 at(double t) const { return p + (t * d); }  // ray.h:40
+};
+
+struct Geom;
+struct Isect {  // ray.h:61-134
+  const Geom* obj = nullptr;
+  double t = 0.0;
+  dvec3 N{0, 0, 0};
+  dvec2 uv{0, 0};
+  dvec3 bary{0, 0, 0};
+  std::shared_ptr<rtxh::Material> material;  // interpolated material (trimesh)
+  int face = -1;                             // orig face id (hit records only)
+  const rtxh::Material& getMaterial() const;
+};
+
+// ---------------------------------------------------------------- textures (material.cpp:84-138)
+struct Tex {
+  const rtxh::Texture* t;
+  dvec3 getPixelAt(int x, int y) const {
+    if (0 <= x && x < t->width && 0 <= y && y < t->height) {
+      size_t idx = (size_t(x) + size_t(y) * t->width) * 3;
+      return mk3(t->data[idx + 0], t->data[idx + 1], t->data[idx + 2]);
+    }
+    return mk3(0.0, 0.0, 0.0);
+  }
+  dvec3 getMappedValue(const dvec2& coord) const {
+    double x = coord.x, y = coord.y;
+    if (0.0 <= x && x <= 1.0 && 0.0 <= y && y <= 1.0) {
+      x *= t->width - 1;
+      y *= t->height - 1;
+      int ix = (int)x, iy = (int)y;
+      x -= ix;
+      y -= iy;
+      dvec3 prows[2];
+      for (int i = 0; i < 2; i++) {
+        dvec3 pl = getPixelAt(i + ix, 0 + iy);
+        dvec3 pr = getPixelAt(i + ix, 1 + iy);
+        prows[i] = y * (pr - pl) + pl;
+      }
+      return (x * (prows[1] - prows[0]) + prows[0]) / 255.0;
+    }
+    return mk3(0.0, 1.0, 0.0);
+  }
+};
+
+struct Scene;
+thread_local const Scene* tl_scene = nullptr;
+
+// MaterialParameter::value / intensityValue (material.cpp:140-158)
+dvec3 pvalue(const rtxh::MatParam& q, const Isect& is);
+double pintensity(const rtxh::MatParam& q, const Isect& is) {
+  dvec3 v = pvalue(q, is);
+  return (0.299 * v.x) + (0.587 * v.y) + (0.114 * v.z);
+}
+double mshininess(const rtxh::Material& m, const Isect& i) {  // material.h:204-209
+  return m.p[rtxh::P_SHININESS].tex >= 0 ? 128.0 * pintensity(m.p[rtxh::P_SHININESS], i)
+                                          : pintensity(m.p[rtxh::P_SHININESS], i);
+}
+double mindex(const rtxh::Material& m, const Isect& i) { return pintensity(m.p[rtxh::P_INDEX], i); }
+dvec3 mk(const rtxh::Material& m, int k, const Isect& i) { return pvalue(m.p[k], i); }
+
+// air (material.cpp:17-21): kt = 1, index = 1, setBools => trans, recur
+rtxh::Material make_air() {
+  rtxh::Material a;
+  a.p[rtxh::P_KT].v = mk3(1.0, 1.0, 1.0);
+  a.p[rtxh::P_INDEX].v = mk3(1.0, 1.0, 1.0);
+  a.setBools();
+  return a;
+}
+const rtxh::Material g_air = make_air();
+
+// ---------------------------------------------------------------- bbox (bbox.cc)
+struct BBox {
+  bool empty = true;
+  dvec3 bmin{0, 0, 0}, bmax{0, 0, 0};
+  bool intersect(const Ray& r, double& tMin, double& tMax) const {  // bbox.cc:33-70
+    dvec3 R0 = r.p, Rd = r.d;
+    tMin = -1.0e308;
+    tMax = 1.0e308;
+    double ttemp;
+    for (int currentaxis = 0; currentaxis < 3; currentaxis++) {
+      double vd = Rd[currentaxis];
+      if (vd == 0.0) continue;
+      double v1 = bmin[currentaxis] - R0[currentaxis];
+      double v2 = bmax[currentaxis] - R0[currentaxis];
+      double t1 = v1 / vd;
+      double t2 = v2 / vd;
+      if (t1 > t2) {
+        ttemp = t1;
+        t1 = t2;
+        t2 = ttemp;
+      }
+      if (t1 > tMin) tMin = t1;
+      if (t2 < tMax) tMax = t2;
+      if (tMin > tMax) return false;
+      if (tMax < RAY_EPSILON) return false;
+    }
+    return true;
+  }
+  void merge(const BBox& b) {  // bbox.cc:107-119
+    if (b.empty) return;
+    double mn[3] = {bmin.x, bmin.y, bmin.z}, mx[3] = {bmax.x, bmax.y, bmax.z};
+    for (int axis = 0; axis < 3; axis++) {
+      if (empty || b.bmin[axis] < mn[axis]) mn[axis] = b.bmin[axis];
+      if (empty || b.bmax[axis] > mx[axis]) mx[axis] = b.bmax[axis];
+    }
+    bmin = mk3(mn[0], mn[1], mn[2]);
+    bmax = mk3(mx[0], mx[1], mx[2]);
+    empty = false;
+  }
+};
+
+// ---------------------------------------------------------------- KdTree (kdTree.h:19-130)
+struct KdTree {
+  KdTree* child[2] = {nullptr, nullptr};
+  BBox bound;
+  std::vector<int> it_idxs;
+  int id = -1;  // DFS pre-order id (hit records)
+
+  KdTree(const std::vector<BBox>& boxes, const std::vector<int>& indexes, int& counter) {
+    id = counter++;
+    if (indexes.size() == 0) return;
+    BBox b = boxes[indexes[0]];
+    for (const auto& ix : indexes) b.merge(boxes[ix]);
+    bound = b;
+    if (indexes.size() <= 3) {
+      for (int x : indexes) it_idxs.push_back(x);
+    } else {
+      dvec3 bmax = b.bmax, bmin = b.bmin;
+      int mx_idx = 0;
+      for (int i = 1; i < 3; i++)
+        if (bmax[mx_idx] - bmin[mx_idx] < bmax[i] - bmin[i]) mx_idx = i;
+      std::vector<int> idxs(indexes.size());
+      std::iota(idxs.begin(), idxs.end(), 0);
+      std::sort(idxs.begin(), idxs.end(), [&](const int a, const int c) {
+        const BBox& box_a = boxes[indexes[a]];
+        const BBox& box_b = boxes[indexes[c]];
+        return (box_a.bmax[mx_idx] + box_a.bmin[mx_idx]) < (box_b.bmax[mx_idx] + box_b.bmin[mx_idx]);
+      });
+      int mid = static_cast<int>(indexes.size() / 2);
+      std::vector<int> it_split[2];
+      for (int i = 0; i < (int)indexes.size(); i++) it_split[i < mid ? 0 : 1].push_back(indexes[idxs[i]]);
+      for (int i = 0; i < 2; i++) child[i] = new KdTree(boxes, it_split[i], counter);
+    }
+  }
+  ~KdTree() {
+    delete child[0];
+    delete child[1];
+  }
+  bool intersectList(const Ray& r, std::vector<int>& hits) const {  // kdTree.h:100-117
+    bool have_one = false;
+    double tmin, tmax;
+    tl.nodes++;
+    if (bound.intersect(r, tmin, tmax)) {
+      if (it_idxs.size() > 0) {
+        for (int it : it_idxs) {
+          hits.push_back(it);
+          have_one = true;
+        }
+      } else if (child[0]) {
+        have_one |= child[0]->intersectList(r, hits);
+        have_one |= child[1]->intersectList(r, hits);
+      }
+    }
+    return have_one;
+  }
+  void leaf_of(std::vector<int>& out) const {
+    for (int it : it_idxs) out[it] = id;
+    if (child[0]) {
+      child[0]->leaf_of(out);
+      child[1]->leaf_of(out);
+    }
+  }
+  uint64_t hash(uint64_t h, const std::vector<int>& orig) const;
+};
+
+uint64_t fnv(uint64_t h, const void* p, size_t n) {
+  const uint8_t* b = static_cast<const uint8_t*>(p);
+  for (size_t i = 0; i < n; ++i) {
+    h ^= b[i];
+    h *= 1099511628211ull;
+  }
+  return h;
+}
+uint64_t KdTree::hash(uint64_t h, const std::vector<int>& orig) const {
+  if (bound.empty && it_idxs.empty() && !child[0]) return h;  // empty tree: no node
+  double mn[3] = {bound.bmin.x, bound.bmin.y, bound.bmin.z}, mx[3] = {bound.bmax.x, bound.bmax.y, bound.bmax.z};
+  h = fnv(h, mn, sizeof(mn));
+  h = fnv(h, mx, sizeof(mx));
+  int32_t c = static_cast<int32_t>(it_idxs.size());
+  h = fnv(h, &c, 4);
+  for (int it : it_idxs) {
+    int32_t o = orig[it];
+    h = fnv(h, &o, 4);
+  }
+  if (child[0]) {
+    h = child[0]->hash(h, orig);
+    h = child[1]->hash(h, orig);
+  }
+  return h;
+}
+
+// ---------------------------------------------------------------- geometry (scene.h, scene.cpp)
+struct Mesh;
+struct Geom {
+  int type = 0;
+  int orig_id = -1;
+  const rtxh::Transform* tf = nullptr;
+  const rtxh::Material* material = nullptr;
+  BBox bounds;
+  const Mesh* mesh = nullptr;
+  virtual ~Geom() {}
+  virtual bool intersectLocal(Ray& r, Isect& i) const = 0;
+  virtual void intersectLocalList(Ray& r, std::vector<Isect>& iv) const = 0;
+
+  dvec3 globalToLocal(const dvec3& v) const { return rtxh::mat4_mul_point(tf->inverse, v); }
+  dvec3 localToGlobalNormal(const dvec3& v) const { return rtm::normalize(rtm::mat3_mul(tf->normi.m, v)); }
+
+  bool intersect(Ray& r, Isect& i) const {  // scene.cpp:13-38
+    tl.objects++;
+    double tmin, tmax;
+    if (!(bounds.intersect(r, tmin, tmax))) return false;
+    dvec3 pos = globalToLocal(r.p);
+    dvec3 dir = globalToLocal(r.p + r.d) - pos;
+    double length = rtm::length(dir);
+    dir = rtm::normalize(dir);
+    dvec3 Wpos = r.p, Wdir = r.d;
+    r.p = pos;
+    r.d = dir;
+    bool rtrn = false;
+    if (intersectLocal(r, i)) {
+      i.N = localToGlobalNormal(i.N);
+      i.t = i.t / length;
+      rtrn = true;
+    }
+    r.p = Wpos;
+    r.d = Wdir;
+    return rtrn;
+  }
+
+  std::vector<Isect> intersectList(Ray& r) const {  // scene.cpp:40-64
+    std::vector<Isect> buf;
+    tl.objects++;
+    double tmin, tmax;
+    if (!(bounds.intersect(r, tmin, tmax))) return buf;
+    dvec3 pos = globalToLocal(r.p);
+    dvec3 dir = globalToLocal(r.p + r.d) - pos;
+    double length = rtm::length(dir);
+    dir = rtm::normalize(dir);
+    dvec3 Wpos = r.p, Wdir = r.d;
+    r.p = pos;
+    r.d = dir;
+    intersectLocalList(r, buf);
+    for (auto& i : buf) {
+      i.N = localToGlobalNormal(i.N);
+      i.t = i.t / length;
+    }
+    r.p = Wpos;
+    r.d = Wdir;
+    return buf;
+  }
+};
+
+const rtxh::Material& Isect::getMaterial() const { return material ? *material : *obj->material; }
+
+struct Sphere : Geom {
+  bool intersectLocal(Ray& r, Isect& i) const override {  // Sphere.cpp:9-40
+    r.d = rtm::normalize(r.d);
+    dvec3 v = -r.p;
+    double b = rtm::dot(v, r.d);
+    double discriminant = b * b - rtm::dot(v, v) + 1;
+    if (discriminant < 0.0) return false;
+    discriminant = sqrt(discriminant);
+    double t2 = b + discriminant;
+    if (t2 <= RAY_EPSILON) return false;
+    i.obj = this;
+    double t1 = b - discriminant;
+    if (t1 > RAY_EPSILON) {
+      i.t = t1;
+      i.N = rtm::normalize(r.at(t1));
+    } else {
+      i.t = t2;
+      i.N = rtm::normalize(r.at(t2));
+    }
+    return true;
+  }
+  void intersectLocalList(Ray& r, std::vector<Isect>& iv) const override {  // Sphere.cpp:42-72
+    r.d = rtm::normalize(r.d);
+    dvec3 v = -r.p;
+    double b = rtm::dot(v, r.d);
+    double discriminant = b * b - rtm::dot(v, v) + 1;
+    if (discriminant < 0.0) return;
+    discriminant = sqrt(discriminant);
+    double t1 = b - discriminant;
+    double t2 = b + discriminant;
+    if (t1 > RAY_EPSILON) {
+      Isect i;
+      i.obj = this;
+      i.t = t1;
+      i.N = rtm::normalize(r.at(t1));
+      iv.push_back(i);
+    }
+    if (t2 > RAY_EPSILON) {
+      Isect i;
+      i.obj = this;
+      i.t = t2;
+      i.N = rtm::normalize(r.at(t2));
+      iv.push_back(i);
+    }
+  }
+};
+
+struct Box : Geom {
+  dvec3 computeNormal(int bestIndex, const Isect& i) const {  // Box.cpp:99-108
+    dvec3 b_norm = mk(*material, rtxh::P_BUMP, i);
+    if (rtm::length(b_norm) > 0.0001) return rtm::normalize(b_norm - mk3(0.5, 0.5, 0.5));
+    if (bestIndex < 3) return mk3(-double(bestIndex == 0), -double(bestIndex == 1), -double(bestIndex == 2));
+    return mk3(double(bestIndex == 3), double(bestIndex == 4), double(bestIndex == 5));
+  }
+  bool intersectLocal(Ray& r, Isect& i) const override {  // Box.cpp:11-63
+    dvec3 p = r.p, d = r.d;
+    double x, y, t, bestT = 1e100;
+    int bestIndex = -1;
+    for (int it = 0; it < 6; it++) {
+      int mod0 = it % 3;
+      if (d[mod0] == 0) continue;
+      t = ((it / 3) - 0.5 - p[mod0]) / d[mod0];
+      if (t < RAY_EPSILON || t > bestT) continue;
+      int mod1 = (it + 1) % 3, mod2 = (it + 2) % 3;
+      x = p[mod1] + t * d[mod1];
+      y = p[mod2] + t * d[mod2];
+      if (x <= 0.5 && x >= -0.5 && y <= 0.5 && y >= -0.5) {
+        if (bestT > t) {
+          bestT = t;
+          bestIndex = it;
+        }
+      }
+    }
+    if (bestIndex < 0) return false;
+    i.t = bestT;
+    i.obj = this;
+    dvec3 ip = r.at(i.t);
+    int i1 = (bestIndex + 1) % 3, i2 = (bestIndex + 2) % 3;
+    if (bestIndex < 3) {
+      i.uv = rtm::mk2(0.5 - ip[std::min(i1, i2)], 0.5 + ip[std::max(i1, i2)]);
+    } else {
+      i.uv = rtm::mk2(0.5 + ip[std::min(i1, i2)], 0.5 + ip[std::max(i1, i2)]);
+    }
+    i.N = computeNormal(bestIndex, i);
+    return true;
+  }
+  void intersectLocalList(Ray& r, std::vector<Isect>& iv) const override {  // Box.cpp:65-97
+    const dvec3 p = r.p, d = r.d;
+    for (int it = 0; it < 6; it++) {
+      int mod0 = it % 3;
+      if (d[mod0] == 0) continue;
+      double t = ((it / 3) - 0.5 - p[mod0]) / d[mod0];
+      if (t < RAY_EPSILON) continue;
+      int mod1 = (it + 1) % 3, mod2 = (it + 2) % 3;
+      double x = p[mod1] + t * d[mod1];
+      double y = p[mod2] + t * d[mod2];
+      if (x <= 0.5 && x >= -0.5 && y <= 0.5 && y >= -0.5) {
+        Isect i;
+        i.t = t;
+        i.obj = this;
+        dvec3 ip = r.at(i.t);
+        i.uv = rtm::mk2(0.5 + ((it < 3) ? -1.0 : 1.0) * ip[std::min(mod1, mod2)], 0.5 + ip[std::max(mod1, mod2)]);
+        i.N = computeNormal(it, i);
+        iv.push_back(i);
+      }
+    }
+  }
+};
+
+struct Cylinder : Geom {
+  const bool capped = true;  // Cylinder.h:11
+  bool intersectBody(const Ray& r, Isect& i) const {  // Cylinder.cpp:30-93
+    double x0 = r.p[0], y0 = r.p[1], x1 = r.d[0], y1 = r.d[1];
+    double a = x1 * x1 + y1 * y1;
+    double b = 2.0 * (x0 * x1 + y0 * y1);
+    double c = x0 * x0 + y0 * y0 - 1.0;
+    if (0.0 == a) return false;
+    double discriminant = b * b - 4.0 * a * c;
+    if (discriminant < 0.0) return false;
+    discriminant = sqrt(discriminant);
+    double t2 = (-b + discriminant) / (2.0 * a);
+    if (t2 <= RAY_EPSILON) return false;
+    double t1 = (-b - discriminant) / (2.0 * a);
+    if (t1 > RAY_EPSILON) {
+      dvec3 P = r.at(t1);
+      double z = P[2];
+      if (z >= 0.0 && z <= 1.0) {
+        i.t = t1;
+        i.N = rtm::normalize(mk3(P[0], P[1], 0.0));
+        return true;
+      }
+    }
+    dvec3 P = r.at(t2);
+    double z = P[2];
+    if (z >= 0.0 && z <= 1.0) {
+      i.t = t2;
+      dvec3 normal = mk3(P[0], P[1], 0.0);
+      if (!capped && rtm::dot(normal, r.d) > 0) normal = -normal;
+      i.N = rtm::normalize(normal);
+      return true;
+    }
+    return false;
+  }
+  bool intersectCaps(const Ray& r, Isect& i) const {  // Cylinder.cpp:95-153
+    if (!capped) return false;
+    double pz = r.p[2], dz = r.d[2];
+    if (0.0 == dz) return false;
+    double t1, t2;
+    if (dz > 0.0) {
+      t1 = (-pz) / dz;
+      t2 = (1.0 - pz) / dz;
+    } else {
+      t1 = (1.0 - pz) / dz;
+      t2 = (-pz) / dz;
+    }
+    if (t2 < RAY_EPSILON) return false;
+    if (t1 >= RAY_EPSILON) {
+      dvec3 p = r.at(t1);
+      if ((p[0] * p[0] + p[1] * p[1]) <= 1.0) {
+        i.t = t1;
+        i.N = dz > 0.0 ? mk3(0.0, 0.0, -1.0) : mk3(0.0, 0.0, 1.0);
+        return true;
+      }
+    }
+    dvec3 p = r.at(t2);
+    if ((p[0] * p[0] + p[1] * p[1]) <= 1.0) {
+      i.t = t2;
+      i.N = dz > 0.0 ? mk3(0.0, 0.0, 1.0) : mk3(0.0, 0.0, -1.0);
+      return true;
+    }
+    return false;
+  }
+  bool intersectLocal(Ray& r, Isect& i) const override {  // Cylinder.cpp:8-28
+    i.obj = this;
+    if (intersectCaps(r, i)) {
+      Isect ii;
+      if (intersectBody(r, ii)) {
+        if (ii.t < i.t) {
+          i = ii;
+          i.obj = this;
+        }
+      }
+      return true;
+    }
+    return intersectBody(r, i);
+  }
+  void intersectBodyList(const Ray& r, std::vector<Isect>& iv) const {  // Cylinder.cpp:160-207
+    double x0 = r.p[0], y0 = r.p[1], x1 = r.d[0], y1 = r.d[1];
+    double a = x1 * x1 + y1 * y1;
+    double b = 2.0 * (x0 * x1 + y0 * y1);
+    double c = x0 * x0 + y0 * y0 - 1.0;
+    if (0.0 == a) return;
+    double discriminant = b * b - 4.0 * a * c;
+    if (discriminant < 0.0) return;
+    discriminant = sqrt(discriminant);
+    double t1 = (-b - discriminant) / (2.0 * a);
+    double t2 = (-b + discriminant) / (2.0 * a);
+    if (t1 > RAY_EPSILON) {
+      dvec3 P = r.at(t1);
+      double z = P[2];
+      if (z >= 0.0 && z <= 1.0) {
+        Isect i;
+        i.obj = this;
+        i.t = t1;
+        i.N = rtm::normalize(mk3(P[0], P[1], 0.0));
+        iv.push_back(i);
+      }
+    }
+    if (t2 > RAY_EPSILON) {
+      dvec3 P = r.at(t2);
+      double z = P[2];
+      if (z >= 0.0 && z <= 1.0) {
+        Isect i;
+        i.obj = this;
+        i.t = t2;
+        dvec3 normal = mk3(P[0], P[1], 0.0);
+        if (!capped && rtm::dot(normal, r.d) > 0) normal = -normal;
+        i.N = rtm::normalize(normal);
+        iv.push_back(i);
+      }
+    }
+  }
+  void intersectCapsList(const Ray& r, std::vector<Isect>& iv) const {  // Cylinder.cpp:208-263
+    if (!capped) return;
+    double pz = r.p[2], dz = r.d[2];
+    if (0.0 == dz) return;
+    double t1, t2;
+    if (dz > 0.0) {
+      t1 = (-pz) / dz;
+      t2 = (1.0 - pz) / dz;
+    } else {
+      t1 = (1.0 - pz) / dz;
+      t2 = (-pz) / dz;
+    }
+    if (t1 >= RAY_EPSILON) {
+      dvec3 p = r.at(t1);
+      if ((p[0] * p[0] + p[1] * p[1]) <= 1.0) {
+        Isect i;
+        i.obj = this;
+        i.t = t1;
+        i.N = dz > 0.0 ? mk3(0.0, 0.0, -1.0) : mk3(0.0, 0.0, 1.0);
+        iv.push_back(i);
+      }
+    }
+    if (t2 >= RAY_EPSILON) {
+      dvec3 p = r.at(t2);
+      if ((p[0] * p[0] + p[1] * p[1]) <= 1.0) {
+        Isect i;
+        i.obj = this;
+        i.t = t2;
+        i.N = dz > 0.0 ? mk3(0.0, 0.0, 1.0) : mk3(0.0, 0.0, -1.0);
+        iv.push_back(i);
+      }
+    }
+  }
+  void intersectLocalList(Ray& r, std::vector<Isect>& iv) const override {  // Cylinder.cpp:155-158
+    intersectCapsList(r, iv);
+    intersectBodyList(r, iv);
+  }
+};
+
+struct Square : Geom {
+  bool intersectLocal(Ray& r, Isect& i) const override {  // Square.cpp:9-46
+    dvec3 p = r.p, d = r.d;
+    if (d[2] == 0.0) return false;
+    double t = -p[2] / d[2];
+    if (t <= RAY_EPSILON) return false;
+    dvec3 P = r.at(t);
+    if (P[0] < -0.5 || P[0] > 0.5) return false;
+    if (P[1] < -0.5 || P[1] > 0.5) return false;
+    i.obj = this;
+    i.t = t;
+    i.N = d[2] > 0.0 ? mk3(0.0, 0.0, -1.0) : mk3(0.0, 0.0, 1.0);
+    i.uv = rtm::mk2(P[0] + 0.5, P[1] + 0.5);
+    return true;
+  }
+  void intersectLocalList(Ray& r, std::vector<Isect>& iv) const override {  // Square.cpp:48-51
+    Isect i;
+    if (intersectLocal(r, i)) iv.push_back(i);
+  }
+};
+
+struct Mesh {
+  const rtxh::Mesh* m = nullptr;
+  std::unique_ptr<KdTree> kd;
+  std::vector<int> face_leaf;
+};
+
+struct Trimesh : Geom {
+  // TrimeshFace::intersectLocal (trimesh.cpp:119-188)
+  bool faceIntersect(int f, const Ray& r, Isect& i) const {
+    tl.tris++;
+    const rtxh::Mesh& M = *mesh->m;
+    const auto& ids = M.faces[f];
+    const dvec3 verts[3] = {M.verts[ids[0]], M.verts[ids[1]], M.verts[ids[2]]};
+    const dvec3 normal = M.face_normals[f];
+    double t = rtm::dot(normal, r.d);
+    if (t < RAY_EPSILON / 32 && t > -RAY_EPSILON / 32) return false;  // ZCHK
+    t = rtm::dot(verts[0] - r.p, normal) / t;
+    if (t < RAY_EPSILON / 32) return false;  // BTTC
+    dvec3 p_isect = r.at(t);
+    for (int k = 0; k < 3; k++) {
+      dvec3 prime = verts[k];
+      dvec3 edgev = verts[(k + 1) % 3];
+      if (rtm::dot(rtm::cross(edgev - prime, p_isect - prime), normal) < RAY_EPSILON / 32) return false;
+    }
+    double faceArea = rtm::dot(rtm::cross(verts[1] - verts[0], verts[2] - verts[0]), normal);
+    double baryU = rtm::dot(rtm::cross(verts[1] - p_isect, verts[2] - p_isect), normal);
+    double baryV = rtm::dot(rtm::cross(verts[2] - p_isect, verts[0] - p_isect), normal);
+    if (faceArea < RAY_EPSILON / 32 && faceArea > -RAY_EPSILON / 32) return false;
+    dvec3 bary = mk3(baryU / faceArea, baryV / faceArea, 0);
+    bary.z = 1 - bary.x - bary.y;
+    i.obj = this;
+    i.face = f;
+    i.t = t;
+    i.bary = bary;
+    if (M.vmats.size()) {
+      // Material() += b * M_k (material.h:177-189, 281-293).  Decision U2:
+      // the flags of Material() stay refl = trans = false and the
+      // indeterminate _recur is false (no recursion, opaque in shadows).
+      auto im = std::make_shared<rtxh::Material>();
+      for (int k = 0; k < rtxh::P_COUNT; ++k) im->p[k].v = mk3(0, 0, 0);
+      const double bw[3] = {bary.x, bary.y, bary.z};
+      const int scaled[] = {rtxh::P_KE, rtxh::P_KA, rtxh::P_KS, rtxh::P_KD, rtxh::P_KR,
+                            rtxh::P_KT, rtxh::P_INDEX, rtxh::P_SHININESS, rtxh::P_GLOSS};
+      // Material() index starts at 1.0 (material.h:163) before the sums.
+      im->p[rtxh::P_INDEX].v = mk3(1.0, 1.0, 1.0);
+      for (int k = 0; k < 3; ++k) {
+        const rtxh::Material& vm = M.vmats[ids[k]];
+        for (int s : scaled) {
+          dvec3 sv = vm.p[s].v;
+          sv *= bw[k];
+          im->p[s].v += sv;
+        }
+      }
+      im->refl = im->trans = im->recur = im->spec = im->both = false;
+      i.material = im;
+    }
+    if (M.normals.size() != 0) {
+      const dvec3 n0 = M.normals[ids[0]], n1 = M.normals[ids[1]], n2 = M.normals[ids[2]];
+      const double mm[9] = {n0.x, n0.y, n0.z, n1.x, n1.y, n1.z, n2.x, n2.y, n2.z};
+      i.N = rtm::normalize(rtm::mat3_mul(mm, bary));
+    } else {
+      i.N = normal;
+    }
+    return true;
+  }
+  bool intersectLocal(Ray& r, Isect& i) const override {  // trimesh.cpp:79-95
+    bool have_one = false;
+    std::vector<int> potenlist;
+    if (mesh->kd) mesh->kd->intersectList(r, potenlist);
+    for (auto face_i : potenlist) {
+      Isect cur;
+      if (faceIntersect(face_i, r, cur)) {
+        if (!have_one || (cur.t < i.t)) {
+          i = cur;
+          have_one = true;
+        }
+      }
+    }
+    if (!have_one) i.t = 1000.0;
+    return have_one;
+  }
+  void intersectLocalList(Ray& r, std::vector<Isect>& iv) const override {  // trimesh.cpp:97-105
+    std::vector<int> potenlist;
+    if (mesh->kd) mesh->kd->intersectList(r, potenlist);
+    for (auto face_i : potenlist) {
+      Isect cur;
+      if (faceIntersect(face_i, r, cur)) iv.push_back(cur);
+    }
+  }
+};
+
+// ---------------------------------------------------------------- lights (light.h, light.cpp)
+struct Light {
+  const rtxh::Light* L;
+  virtual ~Light() {}
+  virtual double distanceAttenuation(const dvec3& P) const = 0;
+  virtual dvec3 getDirection(const dvec3& P) const = 0;
+  virtual bool sattnLimitCheck(const Ray& r, const Isect& i) const = 0;
+  virtual dvec3 shadowAttenuation(const Ray& r, const dvec3& pos) const {  // light.cpp:16-20
+    dvec3 pb = pos - r.d * EPS_BACKUP;
+    return srsAttenuation(pb, getDirection(pb));
+  }
+  dvec3 srsAttenuation(const dvec3& pos, const dvec3& dir) const;
+  dvec3 getColor() const { return L->color; }
+};
+
+struct DirectionalLight : Light {  // light.cpp:56-59
+  double distanceAttenuation(const dvec3&) const override { return 1.0; }
+  dvec3 getDirection(const dvec3&) const override { return -L->orient; }
+  bool sattnLimitCheck(const Ray&, const Isect&) const override { return false; }
+};
+
+struct PointLight : Light {  // light.cpp:61-73
+  double distanceAttenuation(const dvec3& P) const override {
+    double d = rtm::distance(L->pos, P);
+    return rtm::gclamp(1.0 / (double(L->c) + double(L->l) * d + double(L->q) * d * d), 0.0, 1.0);
+  }
+  dvec3 getDirection(const dvec3& P) const override { return rtm::normalize(L->pos - P); }
+  bool sattnLimitCheck(const Ray& r, const Isect& i) const override {
+    return rtm::dot(L->pos - r.at(i.t), r.d) <= 0;
+  }
+};
+
+// Hammersley (util.cpp:3-11): y is always 0 because n is consumed (U7)
+dvec2 hammersley(int n, int N) {
+  double mul = 0.5, result = 0.0;
+  while (n > 0) {
+    result += (n % 2) ? mul : 0;
+    n /= 2;
+    mul /= 2.0;
+  }
+  return rtm::mk2(result, ((double)n) / N);
+}
+
+thread_local int tl_ss_res = 5;
+
+struct AreaLight : PointLight {  // light.cpp:76-104
+  virtual bool validImpact(const Ray&, const dvec3&) const { return true; }
+  virtual bool validImpact(const Ray&, const dvec3&, const dvec3&) const { return true; }
+  virtual dvec3 pick(int i) const = 0;
+  virtual dvec3 impact(const Ray& r) const = 0;
+  dvec3 shadowAttenuation(const Ray& r, const dvec3& p) const override {
+    if (!validImpact(r, p)) return mk3(0.0, 0.0, 0.0);
+    dvec3 sattn = mk3(1.0, 1.0, 1.0);
+    dvec3 pb = p - r.d * EPS_BACKUP;
+    for (int i = 0; i < tl_ss_res; i++) {
+      dvec3 lpos = pick(i);
+      if (validImpact(r, pb, lpos)) sattn += srsAttenuation(pb, rtm::normalize(lpos - pb));
+    }
+    sattn *= (1.0 / (tl_ss_res - 1));
+    return sattn;
+  }
+  bool sattnLimitCheck(const Ray& r, const Isect& i) const override {
+    dvec3 imp = impact(r);
+    return rtm::dot(imp - r.at(i.t), r.d) <= 0;
+  }
+};
+
+struct AreaLightRect : AreaLight {  // light.cpp:100-110
+  dvec3 pick(int i) const override {
+    dvec2 point = hammersley(i, tl_ss_res);
+    double a = (point.x - 0.5) * L->width, b = (point.y - 0.5) * L->height;
+    // glm dmat2x3(u, v) * dvec2(a, b)
+    return mk3(L->u.x * a + L->v.x * b, L->u.y * a + L->v.y * b, L->u.z * a + L->v.z * b);
+  }
+  dvec3 impact(const Ray& r) const override {
+    double t = rtm::dot(L->orient, r.d);
+    t = rtm::dot(L->pos - r.p, L->orient) / t;
+    return r.at(t);
+  }
+};
+
+struct AreaLightCirc : AreaLight {  // light.cpp:112-141
+  dvec3 pick(int i) const override {
+    double ang_rad = 2 * PI / tl_ss_res * i;
+    double dist = 0.5 * L->radius;
+    double x = std::cos(ang_rad) * dist;
+    double y = std::sin(ang_rad) * dist;
+    const dvec3 ori = L->orient;
+    dvec3 ab = mk3(std::fabs(ori.x), std::fabs(ori.y), std::fabs(ori.z));
+    dvec3 u = mk3(0.0, 0.0, 0.0);
+    if (ab.x < ab.y && ab.x < ab.z) u = mk3(0.0, -ori.z, ori.y);
+    else if (ab.y < ab.z) u = mk3(-ori.z, 0.0, ori.x);
+    else u = mk3(-ori.y, ori.x, 0.0);
+    u = rtm::normalize(u);
+    dvec3 v = rtm::cross(ori, u);
+    return x * u + y * v + L->pos;
+  }
+  dvec3 impact(const Ray& r) const override {
+    double t = rtm::dot(L->orient, r.d);
+    t = rtm::dot(L->pos - r.p, L->orient) / t;
+    dvec3 colpos = r.at(t);
+    if (rtm::dot(colpos - L->pos, colpos - L->pos) < (L->radius * L->radius)) return r.at(t);
+    return mk3(0.0, 0.0, 0.0);
+  }
+};
+
+struct SpotLight : AreaLightCirc {  // light.cpp:143-149
+  bool validImpact(const Ray&, const dvec3& p) const override {
+    return (rtm::dot(getDirection(p), L->orient) <= 0) &&
+           (rtm::dot(rtm::normalize(p - (L->pos - L->offset * L->orient)), L->orient) > std::cos(PI / 4));
+  }
+  bool validImpact(const Ray&, const dvec3& p, const dvec3& lp) const override {
+    return (rtm::dot(getDirection(p), L->orient) <= 0) &&
+           (rtm::dot(rtm::normalize(p - lp), L->orient) > std::cos(PI / 4));
+  }
+};
+
+// ---------------------------------------------------------------- scene (scene.cpp)
+struct Scene {
+  rtxh::SceneModel model;
+  std::vector<std::unique_ptr<Geom>> objects;
+  std::vector<Mesh> meshes;
+  std::vector<std::unique_ptr<Light>> lights;
+  std::vector<Tex> texs;
+  std::unique_ptr<KdTree> kdtree;
+  std::vector<int> obj_leaf;
+  double aterm_thresh = 0.0;
+
+  bool intersect(Ray& r, Isect& i) const {  // scene.cpp:157-180
+    bool have_one = false;
+    std::vector<int> potenlist;
+    if (kdtree) kdtree->intersectList(r, potenlist);
+    for (const auto& obj_i : potenlist) {
+      auto& obj = objects[obj_i];
+      Isect cur;
+      if (obj->intersect(r, cur)) {
+        if (!have_one || (cur.t < i.t)) {
+          i = cur;
+          have_one = true;
+        }
+      }
+    }
+    if (!have_one) i.t = 1000.0;
+    return have_one;
+  }
+
+  std::vector<Isect> intersectList(Ray& r) const {  // scene.cpp:182-197
+    std::vector<Isect> iv;
+    std::vector<int> potenlist;
+    if (kdtree) kdtree->intersectList(r, potenlist);
+    for (const auto obj_i : potenlist) {
+      auto niv = objects[obj_i]->intersectList(r);
+      iv.insert(iv.end(), niv.begin(), niv.end());
+    }
+    return iv;
+  }
+};
+
+dvec3 pvalue(const rtxh::MatParam& q, const Isect& is) {
+  if (q.tex >= 0) return tl_scene->texs[q.tex].getMappedValue(is.uv);
+  return q.v;
+}
+
+// Light::srsAttenuation (light.cpp:21-53)
+dvec3 Light::srsAttenuation(const dvec3& pos, const dvec3& dir) const {
+  tl.shadow++;
+  dvec3 sattn = mk3(1.0, 1.0, 1.0);
+  Ray r2l(pos, dir);
+  std::vector<Isect> iv = tl_scene->intersectList(r2l);
+  std::sort(iv.begin(), iv.end(), [](const Isect& a, const Isect& b) { return a.t < b.t; });
+  double last_t = 0.0;
+  for (auto iv_it : iv) {
+    double t = iv_it.t - last_t;
+    last_t = iv_it.t;
+    iv_it.t = t;
+    const rtxh::Material& m_in = iv_it.getMaterial();
+    const bool is_inside = rtm::dot(iv_it.N, r2l.d) > 0;
+    r2l.p = r2l.at(iv_it.t);
+    const rtxh::Material& m_out = g_air;  // -O o (overlapping media) not restated
+    const rtxh::Material& curr_m = is_inside ? m_in : m_out;
+    const rtxh::Material& next_m = is_inside ? m_out : m_in;
+    if (sattnLimitCheck(r2l, iv_it)) return sattn;
+    if (!next_m.trans) return mk3(0.0, 0.0, 0.0);
+    const double th = tl_scene->aterm_thresh;
+    if (th > 0.0 && rtm::dot(sattn, sattn) < th * th) return mk3(0.0, 0.0, 0.0);
+    sattn *= rtm::pow3(mk(curr_m, rtxh::P_KT, iv_it), iv_it.t);
+  }
+  return sattn;
+}
+
+// Material::shade (material.cpp:34-69)
+dvec3 shade(const rtxh::Material& m, const Scene* scene, const Ray& r, const Isect& i) {
+  tl.shades++;
+  const dvec3 isect_p = r.at(i.t);
+  const dvec3 surf_n = i.N;
+  const dvec3 v = r.d;
+  const double sh = mshininess(m, i);
+  const dvec3 kd = mk(m, rtxh::P_KD, i);
+  const dvec3 ks = mk(m, rtxh::P_KS, i);
+  const bool trans = m.trans;
+  dvec3 i_out = mk(m, rtxh::P_KE, i) + mk(m, rtxh::P_KA, i) * scene->model.ambient;
+  for (size_t l_idx = 0; l_idx < scene->lights.size(); ++l_idx) {
+    const Light& L = *scene->lights[l_idx];
+    const dvec3 l_i = L.getDirection(isect_p);
+    const dvec3 l_r = (l_i - 2 * (rtm::dot(l_i, surf_n)) * surf_n);
+    double dot = rtm::dot(l_i, surf_n);
+    if (trans) dot = std::fabs(dot);
+    const dvec3 d_comp = kd * rtm::gmax(0.0, dot);
+    const dvec3 s_comp = ks * rtm::pow3(rtm::splat3(rtm::gmax(0.0, rtm::dot(l_r, v))), sh);
+    const double dattn = L.distanceAttenuation(isect_p);
+    const dvec3 sattn = L.shadowAttenuation(r, isect_p);
+    i_out += dattn * sattn * L.getColor() * (d_comp + s_comp);
+  }
+  return i_out;
+}
+
+// ---------------------------------------------------------------- ray tracer (RayTracer.cpp)
+struct HitCapture {
+  bool armed = false;
+  RtxHitRecord* rec = nullptr;
+};
+thread_local HitCapture tl_cap;
+
+struct Tracer {
+  const Scene* scene;
+  RtxRenderParams P;
+  int buffer_width, buffer_height;
+
+  void record(const Isect& i, bool hit) const {
+    if (!tl_cap.armed) return;
+    tl_cap.armed = false;
+    RtxHitRecord* h = tl_cap.rec;
+    if (!h) return;
+    h->t = i.t;
+    if (!hit) {
+      h->object = h->face = h->scene_leaf = h->mesh_leaf = -1;
+      return;
+    }
+    const Geom* g = i.obj;  // faces report through their Trimesh
+    h->object = g->orig_id;
+    h->scene_leaf = scene->obj_leaf[g->orig_id];
+    if (g->type == rtxh::OBJ_TRIMESH) {
+      h->face = i.face;
+      h->mesh_leaf = g->mesh->face_leaf[i.face];
+    } else {
+      h->face = -1;
+      h->mesh_leaf = -1;
+    }
+  }
+
+  // RayTracer::traceRay (RayTracer.cpp:108-174).  Decision U3: t of a
+  // child ray that misses is 0 (kt^0 = 1).
+  dvec3 traceRay(Ray& r, double thresh, int depth, double& t) const {
+    dvec3 colorC = mk3(0.0, 0.0, 0.0);
+    Isect i;
+    bool hit = depth >= 0 && scene->intersect(r, i);
+    if (depth >= 0) record(i, hit);
+    if (hit) {
+      depth -= 1;
+      const rtxh::Material& m_in = i.getMaterial();
+      t = i.t;
+      colorC = shade(m_in, scene, r, i);
+      if (thresh > 0.0 && rtm::dot(colorC, colorC) < thresh) return colorC;
+      if (m_in.recur && depth > 0) {
+        const rtxh::Material& m_out = g_air;
+        bool leaving = rtm::dot(i.N, r.d) >= 0;
+        const rtxh::Material& curr_m = leaving ? m_in : m_out;
+        const rtxh::Material& next_m = leaving ? m_out : m_in;
+        dvec3 normal = (leaving ? -1.0 : 1.0) * i.N;
+        double c = -1 * rtm::dot(normal, r.d);
+        double eta = next_m.trans ? mindex(curr_m, i) / mindex(next_m, i) : 0;
+        double radicand = 1 - eta * eta * (1 - c * c);
+        bool tir = next_m.trans && radicand < 0;
+        if (m_in.refl || tir) {
+          double reflT = 0.0;
+          dvec3 reflDir = r.d + 2 * c * normal;
+          dvec3 reflStart = r.at(i.t - RAY_EPSILON);
+          Ray reflRay(reflStart, reflDir);
+          tl.secondary++;
+          dvec3 reflCol = traceRay(reflRay, thresh, depth, reflT) * mk(m_in, rtxh::P_KR, i);
+          reflCol *= rtm::gmax3(rtm::gmin3(rtm::pow3(mk(curr_m, rtxh::P_KT, i), reflT), rtm::splat3(1.0)),
+                                rtm::splat3(0.0));
+          colorC += reflCol;
+        }
+        if (next_m.trans && !tir) {
+          double transT = 0.0;
+          Ray transRay(r.at(i.t + RAY_EPSILON), eta * r.d + (eta * c - sqrt(radicand)) * normal);
+          tl.secondary++;
+          dvec3 transCol = traceRay(transRay, thresh, depth, transT);
+          transCol *= rtm::pow3(mk(next_m, rtxh::P_KT, i), transT);
+          colorC += transCol;
+        }
+      }
+    }
+    // miss: no cube map in this restatement (-c not supported) => black
+    return colorC;
+  }
+
+  // RayTracer::trace (RayTracer.cpp:35-79)
+  dvec3 trace(double x, double y, bool anaglyph_eye) const {
+    const rtxh::Camera& cam = scene->model.camera;
+    const dvec3 eye = anaglyph_eye ? cam.eye + mk3(0.25, 0.0, 0.0) : cam.eye;  // ANAGLYPH_DELTA
+    x -= 0.5;
+    y -= 0.5;
+    dvec3 dir = rtm::normalize(cam.look + x * cam.u + y * cam.v);  // camera.cpp:21-31
+    Ray r(eye, dir);
+    double dummy = 0.0;
+    tl.camera++;
+    dvec3 ret = traceRay(r, P.aterm_thresh, P.depth, dummy);
+    if (P.dof) {
+      double fd = rtm::gmax(P.dof_fd, 1.0);
+      dvec3 fp_n = -r.d;
+      dvec3 fp_pt = r.at(fd);
+      double t = rtm::dot(fp_n, r.d);
+      t = rtm::dot(fp_pt - r.p, fp_n) / t;
+      dvec3 dest = r.at(t);
+      double sz = P.dof_apsz / 2;
+      int divs = P.dof_div;
+      double baseAngle = PI / divs;
+      for (int k = 0; k < divs; k++) {
+        double offsetAngle = PI / 2;
+        offsetAngle = offsetAngle / divs + (k - 1) * baseAngle;
+        dvec3 offVec = (std::cos(offsetAngle) * cam.v + std::sin(offsetAngle) * cam.u) * sz;
+        r.p = eye + offVec;
+        r.d = rtm::normalize(dest - r.p);
+        tl.camera++;
+        ret += traceRay(r, P.aterm_thresh, P.depth, dummy);
+      }
+      ret *= (1.0 / (divs + 1.0));
+    }
+    ret = rtm::gclamp3(ret, 0.0, 1.0);
+    return ret;
+  }
+
+  // RayTracer::tracePixel (RayTracer.cpp:81-102); decision U5: the anaglyph
+  // eye shift is per call, the shared camera is not mutated.
+  dvec3 tracePixel(int i, int j) const {
+    const bool ss = P.aa_mode != RTX_AA_NONE && P.aa_mode != RTX_AA_ADAPTIVE;
+    double x = double(i) / (double(buffer_width) * (ss ? P.aa_samples : 1));
+    double y = double(j) / (double(buffer_height) * (ss ? P.aa_samples : 1));
+    dvec3 col = trace(x, y, false);
+    if (P.anaglyph) {
+      dvec3 col_red = trace(x, y, true);
+      col.x = col_red.x;
+    }
+    return col;
+  }
+
+  // RayTracer::adaptaa (RayTracer.cpp:316-365)
+  int adaptaa(double x1, double x2, double y1, double y2, dvec3& val, RtxHitRecord* hits) const {
+    const double adaa_eps = 0.0001;
+    if (x1 + adaa_eps >= x2 || y1 + adaa_eps >= y2) return 0;  // U8: val left untouched
+    double xs[] = {x1, (x1 + x2) / 2.0, x2};
+    double ys[] = {y1, (y1 + y2) / 2.0, y2};
+    double w = x2 - x1, h = y2 - y1;
+    std::vector<dvec3> s;
+    dvec3 mu = mk3(0.0, 0.0, 0.0), sd = mk3(0.0, 0.0, 0.0);
+    const int samples = P.aa_samples;
+    for (int k = 0; k < samples * samples; k++) {
+      dvec2 s_xy = hammersley(k, samples * samples);
+      int64_t before = tl.camera + tl.secondary + tl.shadow;
+      if (hits) {
+        tl_cap.armed = true;
+        tl_cap.rec = &hits[k];
+      }
+      dvec3 s_c = trace(s_xy.x * w + x1, s_xy.y * h + y1, false);
+      if (hits) hits[k].nrays = static_cast<int32_t>(tl.camera + tl.secondary + tl.shadow - before);
+      tl_cap.armed = false;
+      s.push_back(s_c);
+      mu += s_c;
+    }
+    mu *= (1.0 / (samples * samples));
+    for (const auto& s_c : s) {
+      dvec3 a = mk3(std::fabs(s_c.x - mu.x), std::fabs(s_c.y - mu.y), std::fabs(s_c.z - mu.z));
+      sd += rtm::mk3(std::pow(a.x, 2.0), std::pow(a.y, 2.0), std::pow(a.z, 2.0));
+    }
+    sd *= (1.0 / (samples * samples - 1));
+    if (rtm::length(sd) > P.aa_thresh) {
+      mu = mk3(0.0, 0.0, 0.0);
+      for (int a = 0; a < 2; a++)
+        for (int b = 0; b < 2; b++) {
+          dvec3 subval = mk3(0.0, 0.0, 0.0);
+          adaptaa(xs[a], xs[a + 1], ys[b], ys[b + 1], subval, nullptr);
+          mu += subval;
+        }
+      mu *= (1.0 / 4.0);
+    }
+    val = mu;
+    return 0;
+  }
+};
+
+std::unique_ptr<Scene> build_scene(const std::string& path) {
+  std::unique_ptr<Scene> S(new Scene());
+  S->model = rtxh::load_ray_file(path);
+  rtxh::SceneModel& M = S->model;
+  for (const auto& t : M.textures) S->texs.push_back(Tex{&t});
+  // trimesh KdTrees over local face boxes (trimesh.cpp:69-77)
+  S->meshes.resize(M.meshes.size());
+  for (size_t k = 0; k < M.meshes.size(); ++k) {
+    Mesh& me = S->meshes[k];
+    me.m = &M.meshes[k];
+    std::vector<BBox> fb(me.m->faces.size());
+    for (size_t f = 0; f < fb.size(); ++f) {
+      fb[f].empty = false;
+      fb[f].bmin = me.m->face_boxes[f][0];
+      fb[f].bmax = me.m->face_boxes[f][1];
+    }
+    if (!fb.empty()) {
+      std::vector<int> idx(fb.size());
+      std::iota(idx.begin(), idx.end(), 0);
+      int counter = 0;
+      me.kd.reset(new KdTree(fb, idx, counter));
+      me.face_leaf.assign(fb.size(), -1);
+      me.kd->leaf_of(me.face_leaf);
+    }
+  }
+  std::vector<BBox> ob(M.objects.size());
+  for (size_t k = 0; k < M.objects.size(); ++k) {
+    const rtxh::Object& o = M.objects[k];
+    Geom* g = nullptr;
+    switch (o.type) {
+      case rtxh::OBJ_SPHERE: g = new Sphere(); break;
+      case rtxh::OBJ_BOX: g = new Box(); break;
+      case rtxh::OBJ_CYLINDER: g = new Cylinder(); break;
+      case rtxh::OBJ_SQUARE: g = new Square(); break;
+      case rtxh::OBJ_TRIMESH: g = new Trimesh(); break;
+      default: throw rtxh::ParseError("unsupported primitive");
+    }
+    g->type = o.type;
+    g->orig_id = static_cast<int>(k);
+    g->tf = &o.tf;
+    g->material = &M.materials[o.material];
+    g->bounds.empty = false;
+    g->bounds.bmin = o.wmin;
+    g->bounds.bmax = o.wmax;
+    if (o.type == rtxh::OBJ_TRIMESH) g->mesh = &S->meshes[o.mesh];
+    S->objects.emplace_back(g);
+    ob[k] = g->bounds;
+  }
+  // Scene::conclude (scene.cpp:145-153); decision U22: empty scene => no tree
+  if (!ob.empty()) {
+    std::vector<int> idx(ob.size());
+    std::iota(idx.begin(), idx.end(), 0);
+    int counter = 0;
+    S->kdtree.reset(new KdTree(ob, idx, counter));
+    S->obj_leaf.assign(ob.size(), -1);
+    S->kdtree->leaf_of(S->obj_leaf);
+  }
+  for (const auto& L : M.lights) {
+    Light* l = nullptr;
+    switch (L.type) {
+      case rtxh::L_DIRECTIONAL: l = new DirectionalLight(); break;
+      case rtxh::L_POINT: l = new PointLight(); break;
+      case rtxh::L_AREA_RECT: l = new AreaLightRect(); break;
+      case rtxh::L_AREA_CIRC: l = new AreaLightCirc(); break;
+      case rtxh::L_SPOT: l = new SpotLight(); break;
+    }
+    l->L = &L;
+    S->lights.emplace_back(l);
+  }
+  return S;
+}
+
+}  // namespace orc
+
+// ================================================================ C ABI
+extern "C" {
+
+const char* oracle_last_error(void) { return orc::g_err.c_str(); }
+
+int oracle_render(const char* ray_path, const RtxRenderParams* params, const OracleRect* rect, uint8_t* rgb8,
+                  double* rgb_f64, RtxHitRecord* hits, RtxStats* stats) {
+  try {
+    std::unique_ptr<orc::Scene> S = orc::build_scene(ray_path);
+    S->aterm_thresh = params->aterm_thresh;
+    orc::Tracer T;
+    T.scene = S.get();
+    T.P = *params;
+    T.buffer_width = params->width;
+    T.buffer_height = params->height;
+    if (params->overlapping) throw rtxh::ParseError("-O o (overlapping objects) is not restated");
+    const int w = params->width, h = params->height;
+    int x0 = 0, y0 = 0, x1 = w, y1 = h;
+    if (rect && rect->x1 > 0) {
+      x0 = rect->x0; y0 = rect->y0; x1 = rect->x1; y1 = rect->y1;
+    }
+    const int threads = (rect && rect->threads > 0) ? rect->threads : omp_get_max_threads();
+    const int S_ = params->aa_mode == RTX_AA_NONE ? 1 : params->aa_samples;
+    const int spp = S_ * S_;
+    int64_t tot[7] = {0, 0, 0, 0, 0, 0, 0};
+    const int ss_res = params->ss_res;
+#pragma omp parallel num_threads(threads) reduction(+ : tot[:7])
+    {
+      orc::tl_scene = S.get();
+      orc::tl_ss_res = ss_res;
+      orc::tl = orc::Counters();
+#pragma omp for collapse(2) schedule(dynamic, 4)
+      for (int i = x0; i < x1; i++) {
+        for (int j = y0; j < y1; j++) {
+          const size_t pix = size_t(i) + size_t(j) * w;
+          RtxHitRecord* ph = hits ? &hits[pix * spp] : nullptr;
+          dvec3 col = mk3(0.0, 0.0, 0.0);
+          if (params->aa_mode != RTX_AA_NONE) {
+            if (params->aa_mode != RTX_AA_ADAPTIVE) {
+              const int samples = params->aa_samples;
+              int modi = i * samples, modj = j * samples;
+              for (double subi = 0; subi < samples; subi += 1) {
+                for (double subj = 0; subj < samples; subj += 1) {
+                  int k = int(subi) * samples + int(subj);
+                  int64_t before = orc::tl.camera + orc::tl.secondary + orc::tl.shadow;
+                  if (ph) {
+                    orc::tl_cap.armed = true;
+                    orc::tl_cap.rec = &ph[k];
+                  }
+                  col += T.tracePixel(int(modi + subi), int(modj + subj));
+                  orc::tl_cap.armed = false;
+                  if (ph) ph[k].nrays = static_cast<int32_t>(orc::tl.camera + orc::tl.secondary + orc::tl.shadow - before);
+                }
+              }
+              col = col / double(samples * samples);
+            } else {
+              double ax1 = double(i) / double(w), ax2 = double(i + 1) / double(w);
+              double ay1 = double(j) / double(h), ay2 = double(j + 1) / double(h);
+              dvec3 val = mk3(0.0, 0.0, 0.0);
+              T.adaptaa(ax1, ax2, ay1, ay2, val, ph);
+              col = val;
+            }
+          } else {
+            int64_t before = orc::tl.camera + orc::tl.secondary + orc::tl.shadow;
+            if (ph) {
+              orc::tl_cap.armed = true;
+              orc::tl_cap.rec = &ph[0];
+            }
+            col = T.tracePixel(i, j);
+            orc::tl_cap.armed = false;
+            if (ph) ph[0].nrays = static_cast<int32_t>(orc::tl.camera + orc::tl.secondary + orc::tl.shadow - before);
+          }
+          // RayTracer::setPixel (RayTracer.cpp:388-394)
+          if (rgb8) {
+            uint8_t* pixel = rgb8 + pix * 3;
+            pixel[0] = (int)(255.0 * col.x);
+            pixel[1] = (int)(255.0 * col.y);
+            pixel[2] = (int)(255.0 * col.z);
+          }
+          if (rgb_f64) {
+            rgb_f64[pix * 3 + 0] = col.x;
+            rgb_f64[pix * 3 + 1] = col.y;
+            rgb_f64[pix * 3 + 2] = col.z;
+          }
+        }
+      }
+      tot[0] += orc::tl.camera;
+      tot[1] += orc::tl.secondary;
+      tot[2] += orc::tl.shadow;
+      tot[3] += orc::tl.nodes;
+      tot[4] += orc::tl.objects;
+      tot[5] += orc::tl.tris;
+      tot[6] += orc::tl.shades;
+    }
+    if (stats) {
+      std::memset(stats, 0, sizeof(*stats));
+      stats->camera_rays = tot[0];
+      stats->secondary_rays = tot[1];
+      stats->shadow_rays = tot[2];
+      stats->rays = tot[0] + tot[1] + tot[2];
+      stats->node_visits = tot[3];
+      stats->object_tests = tot[4];
+      stats->tri_tests = tot[5];
+      stats->shades = tot[6];
+    }
+    return 0;
+  } catch (const std::exception& e) {
+    orc::g_err = e.what();
+    return -1;
+  }
+}
+
+int oracle_bvh_hash(const char* ray_path, uint64_t* scene_hash, uint64_t* mesh_hash) {
+  try {
+    std::unique_ptr<orc::Scene> S = orc::build_scene(ray_path);
+    std::vector<int> ident(S->objects.size());
+    std::iota(ident.begin(), ident.end(), 0);
+    uint64_t h = 1469598103934665603ull;
+    if (S->kdtree) h = S->kdtree->hash(h, ident);
+    *scene_hash = h;
+    uint64_t mh = 1469598103934665603ull;
+    for (const auto& o : S->model.objects) {
+      if (o.type != rtxh::OBJ_TRIMESH) continue;
+      const orc::Mesh& me = S->meshes[o.mesh];
+      std::vector<int> fid(me.m->faces.size());
+      std::iota(fid.begin(), fid.end(), 0);
+      if (me.kd) mh = me.kd->hash(mh, fid);
+    }
+    *mesh_hash = mh;
+    return 0;
+  } catch (const std::exception& e) {
+    orc::g_err = e.what();
+    return -1;
+  }
+}
+
+int oracle_probe(const char* ray_path, const double p[3], const double d[3], double* t, double n[3],
+                 int32_t* object, int32_t* face) {
+  try {
+    std::unique_ptr<orc::Scene> S = orc::build_scene(ray_path);
+    orc::tl_scene = S.get();
+    orc::Ray r(mk3(p[0], p[1], p[2]), mk3(d[0], d[1], d[2]));
+    orc::Isect i;
+    bool hit = S->intersect(r, i);
+    *t = i.t;
+    n[0] = i.N.x; n[1] = i.N.y; n[2] = i.N.z;
+    *object = hit ? i.obj->orig_id : -1;
+    *face = hit ? i.face : -1;
+    return hit ? 1 : 0;
+  } catch (const std::exception& e) {
+    orc::g_err = e.what();
+    return -1;
+  }
+}
+
+}  // extern "C"

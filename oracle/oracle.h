@@ -1,0 +1,50 @@
+/*
+ * oracle.h — CPU restatement of the reference ray-trace path.
+ *
+ * TEST INFRASTRUCTURE ONLY.  Only tests/, __graft_entry__.smoke() and
+ * bench.py's cpu_baseline leg may load liboracle.so, and only as the checker
+ * (or as the timed CPU baseline).  The product (librtx_hip.so, bin/ray) never
+ * links or calls it.
+ *
+ * PARITY STATUS vs the original binary: UNPINNED.  The reference cannot be
+ * built here (glm 0.9.8.4 is not vendored, <FL/gl.h> is absent, see
+ * SURVEY.md 8(c)) and ships no golden vectors or known-answer tests for this
+ * path; the only shipped renders are of scenes that are not in the repo.
+ * This oracle is pinned instead by (a) line-by-line restatement of the
+ * reference sources cited at every function, (b) analytic known-answer tests
+ * (tests/test_oracle_kat.py) and (c) committed fixtures it generates
+ * (tests/golden/).
+ */
+#ifndef RTX_ORACLE_H_
+#define RTX_ORACLE_H_
+
+#include <stdint.h>
+#include "../include/rtx.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct OracleRect {
+  int32_t x0, y0, x1, y1;  /* pixel rectangle [x0,x1) x [y0,y1); x1 == 0 => full image */
+  int32_t threads;         /* OpenMP threads, 0 = default                           */
+} OracleRect;
+
+const char* oracle_last_error(void);
+/* Render `ray_path` with the reference algorithm.  Outputs are full-frame
+ * (reference buffer indexing (i + j*w)*3); only pixels inside `rect` are
+ * written.  hits: aa-samples-per-pixel records (NULL allowed). */
+int oracle_render(const char* ray_path, const RtxRenderParams* params, const OracleRect* rect,
+                  uint8_t* rgb8, double* rgb_f64, RtxHitRecord* hits, RtxStats* stats);
+/* Structural hashes of the oracle's own KdTree builds (same definition as
+ * RtxHostInfo.scene_bvh_hash / mesh_bvh_hash). */
+int oracle_bvh_hash(const char* ray_path, uint64_t* scene_hash, uint64_t* mesh_hash);
+/* Single-ray probe for known-answer tests: closest hit of the world ray
+ * (p, d) against the scene.  Returns 1 on hit. */
+int oracle_probe(const char* ray_path, const double p[3], const double d[3], double* t, double n[3],
+                 int32_t* object, int32_t* face);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,96 @@
+"""ctypes binding of oracle/_build/liboracle.so — the CPU restatement of the
+reference path (see oracle.h).
+
+TEST INFRASTRUCTURE ONLY: imported by tests/, __graft_entry__.smoke() and
+bench.py's cpu_baseline leg, as the checker / the timed CPU baseline.  The
+product (librtx_hip.so, bin/ray) never uses it.  Parity vs the original
+binary is UNPINNED (the reference cannot be built here: SURVEY.md 8(c)).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB = os.path.join(HERE, "_build", "liboracle.so")
+CLI = os.path.join(HERE, "_build", "ray_oracle")
+
+_lib = None
+
+
+def build(quiet: bool = True):
+    subprocess.run(["make", "-C", HERE, "-j4"], check=True, capture_output=quiet)
+
+
+class OracleRect(C.Structure):
+    _fields_ = [("x0", C.c_int32), ("y0", C.c_int32), ("x1", C.c_int32), ("y1", C.c_int32),
+                ("threads", C.c_int32)]
+
+
+def lib(pkg):
+    """Load liboracle.so; `pkg` is the loaded cs378hgraphics-raytracer_amd
+    module (for the shared struct definitions of rtx.h)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB):
+            build()
+        L = C.CDLL(LIB)
+        L.oracle_last_error.restype = C.c_char_p
+        L.oracle_render.argtypes = [C.c_char_p, C.POINTER(pkg.RtxRenderParams), C.POINTER(OracleRect), C.c_void_p,
+                                    C.c_void_p, C.c_void_p, C.POINTER(pkg.RtxStats)]
+        L.oracle_bvh_hash.argtypes = [C.c_char_p, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]
+        L.oracle_probe.argtypes = [C.c_char_p, C.POINTER(C.c_double), C.POINTER(C.c_double),
+                                   C.POINTER(C.c_double), C.POINTER(C.c_double), C.POINTER(C.c_int32),
+                                   C.POINTER(C.c_int32)]
+        _lib = L
+    return _lib
+
+
+def render(pkg, path: str, opts, rect=None, threads: int = 0, want_hits: bool = True):
+    """Render with the restatement.  Returns dict(rgb8, rgb, hits, stats) in
+    the same layout as DeviceScene.render (full frame)."""
+    L = lib(pkg)
+    host = pkg.HostScene(path)
+    h = host.height_for(opts.width)
+    host.close()
+    p = opts.params(h)
+    w = opts.width
+    rgb8 = np.zeros((h, w, 3), np.uint8)
+    rgb = np.zeros((h, w, 3), np.float64)
+    hits = np.zeros((h, w, opts.spp), pkg.HIT_DTYPE) if want_hits else None
+    if hits is not None:
+        hits["object"] = -1
+    r = OracleRect(0, 0, 0, 0, threads)
+    if rect is not None:
+        r.x0, r.y0, r.x1, r.y1 = rect
+    st = pkg.RtxStats()
+    rc = L.oracle_render(path.encode(), C.byref(p), C.byref(r), rgb8.ctypes.data, rgb.ctypes.data,
+                         hits.ctypes.data if hits is not None else None, C.byref(st))
+    if rc != 0:
+        raise RuntimeError(L.oracle_last_error().decode())
+    return {"rgb8": rgb8, "rgb": rgb, "hits": hits, "stats": st.as_dict(), "height": h, "width": w}
+
+
+def bvh_hash(pkg, path: str):
+    L = lib(pkg)
+    a, b = C.c_uint64(), C.c_uint64()
+    if L.oracle_bvh_hash(path.encode(), C.byref(a), C.byref(b)) != 0:
+        raise RuntimeError(L.oracle_last_error().decode())
+    return a.value, b.value
+
+
+def probe(pkg, path: str, p, d):
+    L = lib(pkg)
+    pp = (C.c_double * 3)(*p)
+    dd = (C.c_double * 3)(*d)
+    t = C.c_double()
+    n = (C.c_double * 3)()
+    o = C.c_int32()
+    f = C.c_int32()
+    rc = L.oracle_probe(path.encode(), pp, dd, C.byref(t), n, C.byref(o), C.byref(f))
+    if rc < 0:
+        raise RuntimeError(L.oracle_last_error().decode())
+    return bool(rc), t.value, tuple(n), o.value, f.value

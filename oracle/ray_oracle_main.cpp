@@ -1,0 +1,64 @@
+// ray_oracle_main.cpp — reference-style CLI over the CPU restatement
+// (TEST INFRASTRUCTURE; see oracle.h).  Same flags as bin/ray
+// (CommandLineUI.cpp:23-147); used by tools/raycheck.py as the "--ref" side
+// and by bench.py for the CPU baseline.
+#include <chrono>
+#include <cstdio>
+#include <vector>
+
+#include "../cs378hgraphics-raytracer_amd/csrc/host/cli_opts.h"
+#include "../cs378hgraphics-raytracer_amd/csrc/host/scene_model.h"
+#include "oracle.h"
+
+int main(int argc, char** argv) {
+  rtxh::CliOptions o;
+  int rc = rtxh::cli_parse(argc, argv, o);
+  if (rc) return rc;
+  double aspect = 1.0;
+  try {
+    aspect = rtxh::load_ray_file(o.ray_name).camera.aspectRatio;
+  } catch (const std::exception& e) {
+    std::cerr << e.what() << std::endl;
+    std::cerr << "Unable to load ray file '" << o.ray_name << "'" << std::endl;
+    return 1;
+  }
+  const int w = o.size;
+  const int h = static_cast<int>(w / aspect + 0.5);
+  RtxRenderParams p = rtxh::cli_params(o, w, h);
+  std::vector<uint8_t> rgb(size_t(w) * h * 3, 0);
+  std::vector<double> f64(size_t(w) * h * 3, 0.0);
+  const int spp = o.aa_mode == RTX_AA_NONE ? 1 : o.aa_samples * o.aa_samples;
+  std::vector<RtxHitRecord> hits;
+  if (!o.dump_hits.empty()) hits.resize(size_t(w) * h * spp);
+  OracleRect rect = {0, 0, 0, 0, o.threads};
+  RtxStats st;
+  auto t0 = std::chrono::steady_clock::now();
+  if (oracle_render(o.ray_name.c_str(), &p, &rect, rgb.data(), f64.data(), hits.empty() ? nullptr : hits.data(),
+                    &st) != 0) {
+    std::cerr << oracle_last_error() << std::endl;
+    std::cerr << "Unable to load ray file '" << o.ray_name << "'" << std::endl;
+    return 1;
+  }
+  double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  std::string err;
+  if (!rtxh::write_image(o.img_name, w, h, rgb.data(), &err)) {
+    std::cerr << err << std::endl;
+    return 1;
+  }
+  if (!o.dump_f64.empty()) {
+    FILE* f = std::fopen(o.dump_f64.c_str(), "wb");
+    std::fwrite(f64.data(), sizeof(double), f64.size(), f);
+    std::fclose(f);
+  }
+  if (!o.dump_hits.empty()) {
+    FILE* f = std::fopen(o.dump_hits.c_str(), "wb");
+    std::fwrite(hits.data(), sizeof(RtxHitRecord), hits.size(), f);
+    std::fclose(f);
+  }
+  if (o.stats)
+    std::printf("{\"backend\": \"oracle-cpu\", \"ms\": %.3f, \"rays\": %lld, \"mrays_per_s\": %.4f, "
+                "\"node_visits\": %lld, \"object_tests\": %lld, \"tri_tests\": %lld, \"shades\": %lld}\n",
+                ms, (long long)st.rays, st.rays / ms / 1e3, (long long)st.node_visits, (long long)st.object_tests,
+                (long long)st.tri_tests, (long long)st.shades);
+  return 0;
+}

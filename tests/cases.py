@@ -1,0 +1,20 @@
+"""Parity cases: (name, scene, reference CLI flags).  Sizes are small so the
+CPU restatement finishes in seconds; each case exercises a reference feature."""
+
+CASES = [
+    ("spheres_r5", "spheres_overlap.ray", "-w 64 -r 5"),
+    ("distance_r3", "distance.ray", "-w 64 -r 3"),
+    ("concrete2_bump", "concrete_2.ray", "-w 64 -r 5"),
+    ("concrete1_r1", "concrete_1.ray", "-w 48 -r 1"),
+    ("spotlight", "box_cyl_opaque_shadow_spotlight.ray", "-w 64 -r 2"),
+    ("lava_arealight", "lava_box.ray", "-w 48 -r 3 -O s -A 4"),
+    ("hitchcock_c2", "hitchcock.ray", "-w 64 -r 3 -O r -A 2"),
+    ("hitchcock_c1", "hitchcock.ray", "-w 64 -r 1"),
+    ("trimesh2_aa", "trimesh2_square.ray", "-w 40 -r 5 -O r -A 2"),
+    ("trimesh2_dof", "trimesh2.ray", "-w 48 -r 3 -O d -A 2.5 -B 4 -C 0.05"),
+    ("hitchcock_adaptive", "hitchcock.ray", "-w 24 -r 2 -O a -A 3 -B 0.02"),
+    ("spheres_anaglyph", "spheres_overlap.ray", "-w 48 -r 3 -O g"),
+    ("spheres_aterm", "spheres_overlap.ray", "-w 48 -r 5 -O c -A 0.01"),
+    ("spheres_r0", "spheres_overlap.ray", "-w 32 -r 0"),
+    ("distance_aa3", "distance.ray", "-w 24 -r 2 -O r -A 3"),
+]
