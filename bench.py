@@ -1,0 +1,215 @@
+#!/usr/bin/env python3
+"""Benchmark: Mrays/s + frame ms of the headline config (BASELINE.json):
+trimesh2.ray (stand-in, tools/gen_scenes.py) at 1920x1080, depth 5, 4x4
+regular AA (`ray -w 1920 -r 5 -O r -A 4`).
+
+One step = one frame.  On N GPUs (one process per GPU, torch.distributed over
+RCCL) the frame is cut into 32x32 tiles dealt round-robin (tile % N == rank),
+each rank renders its tiles into a packed HBM buffer and rank 0 gathers them
+over xGMI (dist.gather) — total work is fixed, so scaling is strong.
+
+value = rays of the whole frame (camera + reflection/refraction + shadow
+queries) / frame wall time, taken as the max over ranks between
+barrier+synchronize brackets.  roofline.achieved = algorithmic bytes of one
+render-kernel launch / its HIP-event duration (rtx_kernel_time on the render
+stream).  cpu_baseline = the CPU restatement (oracle/, "port") timed on this
+host's cores over row bands of the same frame.
+"""
+import argparse
+import importlib.util
+import json
+import os
+import subprocess
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+METRIC = "Mrays/sec + frame ms, trimesh2.ray 1920×1080 depth-5 4×AA; 1/2/4/8 MI355X"
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+# algorithmic bytes per unit: ray in + hit out, BVH node, object
+# record, triangle record, material record per shade
+B_RAY, B_NODE, B_OBJ, B_TRI, B_SHADE = 48 + 72, 64, 224, 96, 176
+
+
+def load_package():
+    name = "cs378hgraphics_raytracer_amd"
+    if name in sys.modules:
+        return sys.modules[name]
+    spec = importlib.util.spec_from_file_location(name, os.path.join(ROOT, "cs378hgraphics-raytracer_amd",
+                                                                     "__init__.py"))
+    mod = importlib.util.module_from_spec(spec)
+    sys.modules[name] = mod
+    spec.loader.exec_module(mod)
+    return mod
+
+
+def ensure_built(pkg_dir):
+    if not os.path.exists(os.path.join(pkg_dir, "lib", "librtx_hip.so")):
+        subprocess.run(["make", "-C", pkg_dir, "-j8", "all"], check=True)
+
+
+def cpu_baseline(pkg, path, opts, height, budget_s=15.0):
+    """Time the CPU restatement over row bands of the same frame."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle  # test infrastructure: the CPU baseline leg
+
+    if not os.path.exists(oracle.LIB):
+        oracle.build()
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
+    w = opts.width
+    # calibration band: 2 rows
+    rows_done, rays, secs = 0, 0, 0.0
+    band = 2
+    nb = 4
+    y_centres = [int(height * (k + 0.5) / nb) for k in range(nb)]
+    while True:
+        t_band = 0.0
+        for yc in y_centres:
+            y0 = max(0, min(height - band, yc - band // 2))
+            r = oracle.render(pkg, path, opts, rect=(0, y0, w, y0 + band), threads=threads, want_hits=False)
+            dt = r["stats"]["kernel_ms"] * 1e-3  # render loop only, parse excluded
+            t_band += dt
+            rays += r["stats"]["rays"]
+            secs += dt
+            rows_done += band
+        if secs >= budget_s * 0.4 or rows_done >= height:
+            break
+        band = max(band, int(band * min(8.0, (budget_s - secs) / max(t_band, 1e-3))))
+        band = min(band, height // nb)
+    return {"value": rays / secs / 1e6, "unit": "Mrays/s", "cores": threads, "kind": "port",
+            "sample": f"CPU restatement (oracle/, -O2, OpenMP) on {rows_done} rows x {w} px of the same frame "
+                      f"({nb} bands spread over the image), {rays} rays in {secs:.1f} s"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--scene", default=os.path.join(ROOT, "scenes", "trimesh2.ray"))
+    ap.add_argument("--flags", default="-w 1920 -r 5 -O r -A 4")
+    ap.add_argument("--tile", type=int, default=32)
+    ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
+    ap.add_argument("--cpu-budget", type=float, default=15.0)
+    ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic_latest.json"),
+                    help="PMC-measured HBM bytes per launch (tools/profile_traffic.sh output)")
+    args = ap.parse_args()
+
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    pkg_dir = os.path.join(ROOT, "cs378hgraphics-raytracer_amd")
+    if rank == 0 or world == 1:
+        ensure_built(pkg_dir)
+    if not os.path.exists(args.scene):
+        if rank == 0:
+            subprocess.run([sys.executable, os.path.join(ROOT, "tools", "gen_scenes.py")], check=True,
+                           stdout=subprocess.DEVNULL)
+    import torch
+    import torch.distributed as dist
+
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+    torch.cuda.set_device(local_rank)
+    if world > 1:
+        dist.barrier()
+    pkg = load_package()
+    opts = pkg.RenderOptions.from_cli(args.flags.split())
+    host = pkg.HostScene(args.scene)
+    height = host.height_for(opts.width)
+    dev = pkg.DeviceScene(host, local_rank)
+    tile = args.tile if world > 1 else 0
+    packed = world > 1
+    npix = pkg.shard_pixels(opts, height, tile, rank, world, packed)
+    rgb8 = torch.zeros(npix * 3, dtype=torch.uint8, device="cuda")
+    stream = torch.cuda.current_stream().cuda_stream
+
+    # counting pass (untimed): rays and traversal work of this rank's share
+    st = dev.render(opts, want_f64=False, stats=True, tile=tile, shard=rank, nshards=world, packed=packed)["stats"]
+    dev.kernel_time()  # drop the counting launch's events
+    gather_list = None
+    if world > 1 and rank == 0:
+        gather_list = [torch.zeros(pkg.shard_pixels(opts, height, tile, r, world, True) * 3, dtype=torch.uint8,
+                                   device="cuda") for r in range(world)]
+        # dist.gather needs equal sizes: pad to the largest shard
+        mx = max(g.numel() for g in gather_list)
+        gather_list = [torch.zeros(mx, dtype=torch.uint8, device="cuda") for _ in range(world)]
+    if world > 1:
+        mx = torch.tensor([rgb8.numel()], device="cuda")
+        dist.all_reduce(mx, op=dist.ReduceOp.MAX)
+        send = torch.zeros(int(mx.item()), dtype=torch.uint8, device="cuda")
+
+    def step():
+        dev.render_device(opts, rgb8.data_ptr(), 0, stream, tile=tile, shard=rank, nshards=world, packed=packed)
+        if world > 1:
+            send[: rgb8.numel()].copy_(rgb8)
+            dist.gather(send, gather_list, dst=0)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    dev.kernel_time()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    kms, nlaunch = dev.kernel_time()
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        tot = torch.tensor([st["rays"]], dtype=torch.int64, device="cuda")
+        dist.all_reduce(tot)
+        frame_rays = int(tot.item())
+    else:
+        frame_rays = st["rays"]
+    ms_per_step = elapsed / args.steps * 1e3
+    value = frame_rays * args.steps / elapsed / 1e6
+
+    if rank == 0:
+        avg_kernel_ms = kms / max(1, nlaunch)
+        algo_bytes = (B_RAY * st["rays"] + B_NODE * st["node_visits"] + B_OBJ * st["object_tests"] +
+                      B_TRI * st["tri_tests"] + B_SHADE * st["shades"])
+        achieved = algo_bytes / (avg_kernel_ms * 1e-3) / 1e9
+        traffic = None
+        if os.path.exists(args.traffic):
+            try:
+                with open(args.traffic) as f:
+                    tr = json.load(f)
+                if tr.get("flags") == args.flags and tr.get("n_gpus", 1) == world:
+                    traffic = tr.get("hbm_bytes_per_launch")
+            except Exception:
+                traffic = None
+        cpu = None
+        if not args.no_cpu and world == 1:
+            cpu = cpu_baseline(pkg, args.scene, opts, height, args.cpu_budget)
+        line = {
+            "metric": METRIC, "value": round(value, 3), "unit": "Mrays/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3),
+            "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "f64",
+            "data": "synthetic (procedural trimesh2 stand-in scene, tools/gen_scenes.py seed 2; reference scene absent)",
+            "config": {"workload": f"trimesh2 {opts.width}x{height} {args.flags}", "scene": os.path.basename(args.scene),
+                       "triangles": host.info.n_faces, "rays_per_frame": frame_rays, "tile": tile or None,
+                       "parallelism": f"tile-shard x{world} + RCCL gather" if world > 1 else "single GPU"},
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                         "kernel": "render_kernel<false,false>", "avg_kernel_ms": round(avg_kernel_ms, 3),
+                         "algorithmic_bytes_per_launch": algo_bytes},
+            "cpu_baseline": cpu,
+        }
+        if cpu:
+            line["gpu_over_cpu"] = round(value / cpu["value"], 2)
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -61,6 +61,7 @@ struct FrameParams {
   int bx_per_tile;           // blocks per tile row
   int64_t n_items;           // work items (pixel blocks)
   int64_t n_samples;         // n_items * ppw * spp  (sample ids)
+  int qchunk;                // samples per queue atomic (multiple of 64)
 };
 
 // Work item -> pixel; out_index is the output slot (packed tile order or
@@ -551,14 +552,14 @@ __global__ void __launch_bounds__(WG) render_kernel(DevScene S, const FrameParam
         if (qnext >= qend) {
           if (exhausted) break;
           unsigned long long base = 0;
-          if (lane == 0) base = atomicAdd(work, static_cast<unsigned long long>(QCHUNK));
+          if (lane == 0) base = atomicAdd(work, static_cast<unsigned long long>(F.qchunk));
           base = __shfl(base, 0);
           if (base >= static_cast<unsigned long long>(F.n_samples)) {
             exhausted = true;
             break;
           }
           qnext = base;
-          qend = base + QCHUNK;
+          qend = base + F.qchunk;
           if (qend > static_cast<unsigned long long>(F.n_samples)) qend = F.n_samples;
         }
         const unsigned int rank = __builtin_amdgcn_mbcnt_hi(static_cast<unsigned int>(idle >> 32),
@@ -1491,7 +1492,6 @@ rtx_status rtx_render(void* scene, const RtxRenderParams* params, uint8_t* rgb8,
       st->sbuf_bytes = need;
     }
   }
-  HIP_TRY(hipMemcpyAsync(st->d_frame, &F, sizeof(FrameParams), hipMemcpyHostToDevice, stream));
   HIP_TRY(hipMemsetAsync(st->d_work, 0, sizeof(unsigned long long), stream));
   if (stats) HIP_TRY(hipMemsetAsync(st->d_stats, 0, 8 * sizeof(unsigned long long), stream));
 
@@ -1518,6 +1518,17 @@ rtx_status rtx_render(void* scene, const RtxRenderParams* params, uint8_t* rgb8,
   const int64_t grid_needed = (waves_needed + WAVES_PER_WG - 1) / WAVES_PER_WG;
   if (grid > grid_needed) grid = grid_needed;
   if (grid < 1) grid = 1;
+  {
+    // queue chunk: up to QCHUNK samples per atomic, but small frames must
+    // still spread over every wave
+    const int64_t waves = grid * WAVES_PER_WG;
+    int64_t c = F.n_samples / (waves * 4);
+    c = (c / 64) * 64;
+    if (c < 64) c = 64;
+    if (c > QCHUNK) c = QCHUNK;
+    F.qchunk = static_cast<int>(c);
+  }
+  HIP_TRY(hipMemcpyAsync(st->d_frame, &F, sizeof(FrameParams), hipMemcpyHostToDevice, stream));
   const int pend_cap = (params->depth > 0 ? params->depth : 0) + 2;
   {
     const size_t need = size_t(grid) * WG * pend_cap * 13 * sizeof(double);

@@ -1173,6 +1173,7 @@ int oracle_render(const char* ray_path, const RtxRenderParams* params, const Ora
     const int spp = S_ * S_;
     int64_t tot[7] = {0, 0, 0, 0, 0, 0, 0};
     const int ss_res = params->ss_res;
+    const double t_start = omp_get_wtime();  // render loop only (CommandLineUI.cpp:161-170 window)
 #pragma omp parallel num_threads(threads) reduction(+ : tot[:7])
     {
       orc::tl_scene = S.get();
@@ -1241,8 +1242,10 @@ int oracle_render(const char* ray_path, const RtxRenderParams* params, const Ora
       tot[5] += orc::tl.tris;
       tot[6] += orc::tl.shades;
     }
+    const double t_end = omp_get_wtime();
     if (stats) {
       std::memset(stats, 0, sizeof(*stats));
+      stats->kernel_ms = (t_end - t_start) * 1e3;
       stats->camera_rays = tot[0];
       stats->secondary_rays = tot[1];
       stats->shadow_rays = tot[2];
