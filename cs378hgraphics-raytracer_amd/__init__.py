@@ -382,6 +382,22 @@ def unpack_tiles(packed: np.ndarray, width: int, height: int, tile: int, shard: 
     return out
 
 
+def pack_tiles(full: np.ndarray, width: int, height: int, tile: int, shard: int, nshards: int) -> np.ndarray:
+    """Gather a shard's tiles out of a full (height, width, c) frame into the
+    packed layout the kernel writes with packed=1 (tile order, tile*tile
+    pixels per tile, rows inside a tile from the bottom, zero padding)."""
+    tx = (width + tile - 1) // tile
+    tiles = owned_tiles(width, height, tile, shard, nshards)
+    c = full.shape[2]
+    out = np.zeros((len(tiles), tile, tile, c), full.dtype)
+    for k, t in enumerate(tiles):
+        x0, y0 = (t % tx) * tile, (t // tx) * tile
+        w = min(tile, width - x0)
+        h = min(tile, height - y0)
+        out[k, :h, :w] = full[y0:y0 + h, x0:x0 + w]
+    return out.reshape(-1)
+
+
 def write_image(path: str, rgb8: np.ndarray):
     """writeImage (fileio/images.cc:59-68); rgb8 is (h, w, 3) with row 0 at the bottom."""
     a = np.ascontiguousarray(rgb8, dtype=np.uint8)
