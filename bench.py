@@ -173,7 +173,13 @@ def main():
     value = frame_rays * args.steps / elapsed / 1e6
 
     if rank == 0:
-        avg_kernel_ms = kms / max(1, nlaunch)
+        # one launch of the render megakernel renders the whole frame; the
+        # wavefront path (RTX_WAVEFRONT=1) splits a frame into many launches,
+        # so the figure is priced per frame: algorithmic bytes of one frame /
+        # the HIP-event kernel time of one frame (both identical for the
+        # megakernel, where launches == frames)
+        launches_per_frame = nlaunch / max(1, args.steps)
+        avg_kernel_ms = kms / max(1, args.steps)
         algo_bytes = (B_RAY * st["rays"] + B_NODE * st["node_visits"] + B_OBJ * st["object_tests"] +
                       B_TRI * st["tri_tests"] + B_SHADE * st["shades"])
         achieved = algo_bytes / (avg_kernel_ms * 1e-3) / 1e9
@@ -199,7 +205,9 @@ def main():
                        "parallelism": f"tile-shard x{world} + RCCL gather" if world > 1 else "single GPU"},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                         "kernel": "render_kernel<false,false>", "avg_kernel_ms": round(avg_kernel_ms, 3),
+                         "kernel": ("render_kernel<false,false>" if launches_per_frame <= 1.0 else
+                                    "advance_kernel+trace_kernel (wavefront)"),
+                         "avg_kernel_ms": round(avg_kernel_ms, 3), "launches_per_frame": launches_per_frame,
                          "algorithmic_bytes_per_launch": algo_bytes},
             "cpu_baseline": cpu,
         }

@@ -21,6 +21,7 @@
 #include <hip/hip_runtime.h>
 
 #include <climits>
+#include <cstdlib>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -469,6 +470,350 @@ struct Pending {
   int depth, kind;  // kind 0 camera, 1 reflection, 2 refraction
 };
 
+// Per-lane state of one sample's path (everything the state machine keeps
+// between traversal queries).  Registers in the adaptive megakernel, SoA in
+// HBM (SlotArrays) in the wavefront path.
+struct LaneState {
+  int st, sample_slot, rec_on, pass, camk, nrays, top, rdepth, rkind, first_query, sobj, ssub, m_flags, li, pick,
+      qmode, qrp, qsq, bobj, bsub, bhave, kdone;
+  double sx, sy, st_t, m_sh, dattn, last_t, qtp, bt;
+  dvec3 acc, rp, rd, W, N, i_out, dscomp, m_kd, m_ks, area_sum, sdir, wpos, sattn;
+};
+
+#define LANE_INT_FIELDS(X) X(st) X(sample_slot) X(rec_on) X(pass) X(camk) X(nrays) X(top) X(rdepth) X(rkind) \
+  X(first_query) X(sobj) X(ssub) X(m_flags) X(li) X(pick) X(qmode) X(qrp) X(qsq) X(kdone)
+#define LANE_DBL_FIELDS(X) X(sx) X(sy) X(st_t) X(m_sh) X(dattn) X(last_t) X(qtp)
+#define LANE_VEC_FIELDS(X) X(acc) X(rp) X(rd) X(W) X(N) X(i_out) X(dscomp) X(m_kd) X(m_ks) X(area_sum) X(sdir) \
+  X(wpos) X(sattn)
+
+// Run one lane's state machine (trace / traceRay / shade / srsAttenuation,
+// RayTracer.cpp:35-174, material.cpp:34-69, light.cpp:16-53) until it needs
+// a traversal query (L.qmode != Q_NONE) or its sample is finished (ST_IDLE).
+// The pending-ray stack lives in HBM: entry e, field f at
+// pbuf[(e * 13 + f) * nlanes + glane].
+template <bool STATS, bool ADAPTIVE>
+__device__ __forceinline__ void advance_lane(LaneState& L, const DevScene& S, const FrameParams& F, Counters& C,
+                                             double* __restrict__ sbuf, double* __restrict__ colbuf,
+                                             RtxHitRecord* __restrict__ hits, int64_t apix_out, int an,
+                                             double* __restrict__ pbuf, size_t nlanes, size_t glane, int pend_cap) {
+#define REF(f) auto& f = L.f;
+  LANE_INT_FIELDS(REF)
+  LANE_DBL_FIELDS(REF)
+  LANE_VEC_FIELDS(REF)
+  REF(bt) REF(bobj) REF(bsub) REF(bhave)
+#undef REF
+  const RtxRenderParams& P = F.P;
+  const double aterm = P.aterm_thresh;
+  const int ncam = P.dof ? P.dof_div + 1 : 1;
+  auto push = [&](int& tp, const dvec3& p, const dvec3& d, const dvec3& w, const dvec3& k, int depth, int kind) {
+    double* b = pbuf + static_cast<size_t>(tp) * 13 * nlanes + glane;
+    b[0 * nlanes] = p.x; b[1 * nlanes] = p.y; b[2 * nlanes] = p.z;
+    b[3 * nlanes] = d.x; b[4 * nlanes] = d.y; b[5 * nlanes] = d.z;
+    b[6 * nlanes] = w.x; b[7 * nlanes] = w.y; b[8 * nlanes] = w.z;
+    b[9 * nlanes] = k.x; b[10 * nlanes] = k.y; b[11 * nlanes] = k.z;
+    b[12 * nlanes] = static_cast<double>(depth * 4 + kind);
+    ++tp;
+  };
+  qmode = Q_NONE;
+  while (st != ST_IDLE && qmode == Q_NONE) {
+    switch (st) {
+      case ST_CAM: {
+        // next camera ray of trace(x, y) (RayTracer.cpp:35-79)
+        if (camk == ncam) {
+          dvec3 ret = acc;
+          if (P.dof) ret *= (1.0 / (P.dof_div + 1.0));
+          ret = rtm::gclamp3(ret, 0.0, 1.0);
+          if (ADAPTIVE) {
+            colbuf[sample_slot * 3 + 0] = ret.x;
+            colbuf[sample_slot * 3 + 1] = ret.y;
+            colbuf[sample_slot * 3 + 2] = ret.z;
+            if (rec_on) hits[apix_out * an + sample_slot].nrays = nrays;
+            st = ST_IDLE;
+            break;
+          }
+          double* out = sbuf + static_cast<int64_t>(sample_slot) * 3;
+          if (P.anaglyph && pass == 0) {  // tracePixel (RayTracer.cpp:92-99): park pass 0 in the buffer
+            out[0] = ret.x;
+            out[1] = ret.y;
+            out[2] = ret.z;
+            pass = 1;
+            camk = 0;
+            acc = mk3(0, 0, 0);
+            break;
+          }
+          if (P.anaglyph) {
+            out[0] = ret.x;  // red from the shifted eye, green/blue from pass 0
+          } else {
+            out[0] = ret.x;
+            out[1] = ret.y;
+            out[2] = ret.z;
+          }
+          if (rec_on) hits[sample_slot].nrays = nrays;
+          st = ST_IDLE;
+          break;
+        }
+        const RtxCamera& cam = F.cam;
+        const dvec3 eye = pass ? ld3(cam.eye) + mk3(0.25, 0.0, 0.0) : ld3(cam.eye);
+        const double x = sx - 0.5, y = sy - 0.5;
+        const dvec3 cdir = rtm::normalize(ld3(cam.look) + x * ld3(cam.u) + y * ld3(cam.v));
+        if (camk == 0) {
+          rp = eye;
+          rd = cdir;
+          first_query = rec_on && pass == 0;
+          if (first_query) {  // default record: miss (also what depth < 0 leaves)
+            RtxHitRecord* hr = ADAPTIVE ? &hits[apix_out * an + sample_slot] : &hits[sample_slot];
+            hr->object = hr->face = hr->scene_leaf = hr->mesh_leaf = -1;
+            hr->t = 1000.0;
+            hr->pad = 0;
+          }
+        } else {
+          const double fd = rtm::gmax(P.dof_fd, 1.0);
+          const dvec3 fp_n = -cdir;
+          const dvec3 fp_pt = rtm::ray_at(eye, cdir, fd);
+          double t = rtm::dot(fp_n, cdir);
+          t = rtm::dot(fp_pt - eye, fp_n) / t;
+          const dvec3 dest = rtm::ray_at(eye, cdir, t);
+          rp = eye + ld3(&F.offv[(camk - 1) * 3]);
+          rd = rtm::normalize(dest - rp);
+          first_query = false;
+        }
+        camk++;
+        if (STATS) C.camera++;
+        top = 0;
+        push(top, rp, rd, mk3(1, 1, 1), mk3(1, 1, 1), P.depth, 0);
+        st = ST_POP;
+        break;
+      }
+      case ST_POP: {
+        if (top == 0) {
+          st = ST_CAM;
+          break;
+        }
+        --top;
+        const double* b = pbuf + static_cast<size_t>(top) * 13 * nlanes + glane;
+        const int dk = static_cast<int>(b[12 * nlanes]);
+        nrays++;
+        const int pdepth = dk >= 0 ? dk / 4 : -((-dk + 3) / 4);
+        if (pdepth < 0) break;  // `depth >= 0 &&` (RayTracer.cpp:116)
+        rp = mk3(b[0 * nlanes], b[1 * nlanes], b[2 * nlanes]);
+        rd = mk3(b[3 * nlanes], b[4 * nlanes], b[5 * nlanes]);
+        W = mk3(b[6 * nlanes], b[7 * nlanes], b[8 * nlanes]);
+        area_sum = mk3(b[9 * nlanes], b[10 * nlanes], b[11 * nlanes]);  // kt factor, parked until the hit
+        rdepth = pdepth;
+        rkind = dk - pdepth * 4;
+        qmode = Q_CLOSEST;
+        qtp = -RTX_INF;
+        qrp = -1;
+        qsq = -1;
+        st = ST_HIT;
+        break;
+      }
+      case ST_HIT: {
+        // traceRay after scene->intersect (RayTracer.cpp:116-165)
+        if (first_query) {
+          first_query = false;
+          if (bhave) {
+            RtxHitRecord* hr = ADAPTIVE ? &hits[apix_out * an + sample_slot] : &hits[sample_slot];
+            const RtxObject& o = S.objs[bobj];
+            hr->object = o.orig_id;
+            hr->scene_leaf = o.leaf;
+            hr->t = bt;
+            if (o.type == RTX_OBJ_TRIMESH) {
+              const RtxMesh me = S.meshes[o.mesh];
+              const RtxFaceIds fi = S.fids[me.face_off + bsub];
+              hr->face = fi.orig_id;
+              hr->mesh_leaf = fi.leaf;
+            }
+          }
+        }
+        if (!bhave) {  // miss: no cube map => black
+          st = ST_POP;
+          break;
+        }
+        if (rkind == 1)
+          W = W * rtm::gmax3(rtm::gmin3(rtm::pow3(area_sum, bt), rtm::splat3(1.0)), rtm::splat3(0.0));
+        else if (rkind == 2)
+          W = W * rtm::pow3(area_sum, bt);
+        const Resolved R = resolve_hit(S, rp, rd, bobj, bsub, nullptr, nullptr);
+        N = R.N;
+        m_kd = R.m.kd;
+        m_ks = R.m.ks;
+        m_sh = R.m.sh;
+        m_flags = R.m.flags;
+        st_t = bt;
+        sobj = bobj;
+        ssub = bsub;
+        if (STATS) C.shades++;
+        // Material::shade (material.cpp:34-69)
+        i_out = R.m.ke + R.m.ka * mk3(S.ambient[0], S.ambient[1], S.ambient[2]);
+        li = 0;
+        st = ST_LIGHT;
+        break;
+      }
+      case ST_LIGHT: {
+        if (li == S.n_lights) {
+          // colorC = shade(...); adaptive termination; recursion
+          const dvec3 col = i_out;
+          acc += W * col;
+          const int depth = rdepth - 1;
+          st = ST_POP;
+          if (aterm > 0.0 && rtm::dot(col, col) < aterm) break;
+          if ((m_flags & RTX_MF_RECUR) && depth > 0) {
+            const Resolved R = resolve_hit(S, rp, rd, sobj, ssub, nullptr, nullptr);
+            const bool leaving = rtm::dot(N, rd) >= 0;
+            const bool in_trans = (m_flags & RTX_MF_TRANS) != 0;
+            const bool next_trans = leaving ? true : in_trans;  // air is transmissive
+            const dvec3 normal = (leaving ? -1.0 : 1.0) * N;
+            const double c = -1 * rtm::dot(normal, rd);
+            const double eta =
+                next_trans ? (leaving ? R.m.index : S.air_index) / (leaving ? S.air_index : R.m.index) : 0;
+            const double radicand = 1 - eta * eta * (1 - c * c);
+            const bool tir = next_trans && radicand < 0;
+            // push refraction first so that reflection is traced first
+            if (next_trans && !tir && top < pend_cap) {
+              const dvec3 tp = rtm::ray_at(rp, rd, st_t + RTX_RAY_EPS);
+              const dvec3 td = eta * rd + (eta * c - sqrt(radicand)) * normal;
+              push(top, tp, td, W, leaving ? mk3(1.0, 1.0, 1.0) : R.m.kt, depth, 2);
+              if (STATS) C.secondary++;
+            }
+            if (((m_flags & RTX_MF_REFL) || tir) && top < pend_cap) {
+              const dvec3 rdir = rd + 2 * c * normal;
+              const dvec3 rs = rtm::ray_at(rp, rd, st_t - RTX_RAY_EPS);
+              push(top, rs, rdir, W * R.m.kr, leaving ? R.m.kt : mk3(1.0, 1.0, 1.0), depth, 1);
+              if (STATS) C.secondary++;
+            }
+          }
+          break;
+        }
+        const RtxLight& L = S.lights[li];
+        const dvec3 X = rtm::ray_at(rp, rd, st_t);
+        const dvec3 l_i = light_dir(L, X);
+        const dvec3 l_r = (l_i - 2 * (rtm::dot(l_i, N)) * N);
+        double dt = rtm::dot(l_i, N);
+        if (m_flags & RTX_MF_TRANS) dt = fabs(dt);
+        const dvec3 d_comp = m_kd * rtm::gmax(0.0, dt);
+        const dvec3 s_comp = m_ks * rtm::pow3(rtm::splat3(rtm::gmax(0.0, rtm::dot(l_r, rd))), m_sh);
+        dscomp = d_comp + s_comp;
+        dattn = light_dist_atten(L, X);
+        // shadowAttenuation (light.cpp:16-20) / AreaLight (light.cpp:76-87)
+        if (L.type == RTX_LIGHT_DIRECTIONAL || L.type == RTX_LIGHT_POINT) {
+          sdir = light_dir(L, X - rd * RTX_EPS_BACKUP);
+          pick = -1;
+        } else {
+          const dvec3 ori = ld3(L.orient), lpos = ld3(L.pos);
+          if (L.type == RTX_LIGHT_SPOT &&
+              !((rtm::dot(light_dir(L, X), ori) <= 0) &&
+                (rtm::dot(rtm::normalize(X - (lpos - L.offset * ori)), ori) > S.cos45))) {
+            i_out += dattn * mk3(0.0, 0.0, 0.0) * ld3(L.color) * dscomp;
+            li++;
+            break;
+          }
+          area_sum = mk3(1.0, 1.0, 1.0);
+          pick = 0;
+        }
+        st = ST_SRS;
+        break;
+      }
+      case ST_SRS: {
+        // start one srsAttenuation (light.cpp:21-53), or finish an area light
+        const RtxLight& L = S.lights[li];
+        const dvec3 pb = rtm::ray_at(rp, rd, st_t) - rd * RTX_EPS_BACKUP;
+        if (pick >= 0) {
+          bool started = false;
+          while (pick < S.ss_res) {
+            const dvec3 lp = ld3(S.picks + (size_t(li) * S.ss_res + pick) * 3);
+            pick++;
+            if (L.type == RTX_LIGHT_SPOT &&
+                !((rtm::dot(light_dir(L, pb), ld3(L.orient)) <= 0) &&
+                  (rtm::dot(rtm::normalize(pb - lp), ld3(L.orient)) > S.cos45)))
+              continue;
+            sdir = rtm::normalize(lp - pb);
+            started = true;
+            break;
+          }
+          if (!started) {
+            dvec3 sa = area_sum;
+            sa *= (1.0 / (S.ss_res - 1));
+            i_out += dattn * sa * ld3(L.color) * dscomp;
+            li++;
+            st = ST_LIGHT;
+            break;
+          }
+        }
+        if (STATS) C.shadow++;
+        nrays++;
+        sattn = mk3(1.0, 1.0, 1.0);
+        wpos = pb;
+        last_t = 0.0;
+        qmode = Q_NEXT;
+        qtp = -RTX_INF;
+        qrp = -1;
+        qsq = -1;
+        st = ST_WALK;
+        break;
+      }
+      case ST_WALK: {
+        const RtxLight& L = S.lights[li];
+        bool done = false;
+        dvec3 result = sattn;
+        if (!bhave) {
+          done = true;
+        } else {
+          const double t = bt - last_t;
+          last_t = bt;
+          const dvec3 pb = rtm::ray_at(rp, rd, st_t) - rd * RTX_EPS_BACKUP;
+          const Resolved R = resolve_hit(S, pb, sdir, bobj, bsub, nullptr, nullptr);
+          const bool is_inside = rtm::dot(R.N, sdir) > 0;
+          wpos = rtm::ray_at(wpos, sdir, t);
+          bool limit = false;  // sattnLimitCheck with the relative t (U14)
+          if (L.type == RTX_LIGHT_POINT) {
+            limit = rtm::dot(ld3(L.pos) - rtm::ray_at(wpos, sdir, t), sdir) <= 0;
+          } else if (L.type != RTX_LIGHT_DIRECTIONAL) {
+            const dvec3 ori = ld3(L.orient), lpos = ld3(L.pos);
+            double ti = rtm::dot(ori, sdir);
+            ti = rtm::dot(lpos - wpos, ori) / ti;
+            dvec3 imp = rtm::ray_at(wpos, sdir, ti);
+            if (L.type != RTX_LIGHT_AREA_RECT && !(rtm::dot(imp - lpos, imp - lpos) < (L.radius * L.radius)))
+              imp = mk3(0.0, 0.0, 0.0);
+            limit = rtm::dot(imp - rtm::ray_at(wpos, sdir, t), sdir) <= 0;
+          }
+          if (limit) {
+            done = true;
+          } else {
+            const bool next_trans = is_inside ? true : ((R.m.flags & RTX_MF_TRANS) != 0);
+            if (!next_trans || (aterm > 0.0 && rtm::dot(sattn, sattn) < aterm * aterm)) {
+              result = mk3(0.0, 0.0, 0.0);
+              done = true;
+            } else {
+              const dvec3 kt = is_inside ? R.m.kt : mk3(1.0, 1.0, 1.0);
+              sattn *= rtm::pow3(kt, t);
+              qmode = Q_NEXT;
+              qtp = bt;
+              qrp = bobj;
+              qsq = bsub;
+            }
+          }
+        }
+        if (done) {
+          if (pick < 0) {
+            i_out += dattn * result * ld3(L.color) * dscomp;
+            li++;
+            st = ST_LIGHT;
+          } else {
+            area_sum += result;
+            st = ST_SRS;
+          }
+        }
+        break;
+      }
+      default:
+        st = ST_IDLE;
+        break;
+    }
+  }
+
+}
+
 template <bool STATS, bool ADAPTIVE>
 __global__ void __launch_bounds__(WG) render_kernel(DevScene S, const FrameParams* __restrict__ Fp,
                                                      unsigned long long* __restrict__ work,
@@ -490,49 +835,22 @@ __global__ void __launch_bounds__(WG) render_kernel(DevScene S, const FrameParam
   // pbuf[(e * 13 + f) * nlanes + g]
   const size_t nlanes = static_cast<size_t>(gridDim.x) * WG;
   const size_t glane = static_cast<size_t>(blockIdx.x) * WG + threadIdx.x;
-  auto push = [&](int& tp, const dvec3& p, const dvec3& d, const dvec3& w, const dvec3& k, int depth, int kind) {
-    double* b = pbuf + static_cast<size_t>(tp) * 13 * nlanes + glane;
-    b[0 * nlanes] = p.x; b[1 * nlanes] = p.y; b[2 * nlanes] = p.z;
-    b[3 * nlanes] = d.x; b[4 * nlanes] = d.y; b[5 * nlanes] = d.z;
-    b[6 * nlanes] = w.x; b[7 * nlanes] = w.y; b[8 * nlanes] = w.z;
-    b[9 * nlanes] = k.x; b[10 * nlanes] = k.y; b[11 * nlanes] = k.z;
-    b[12 * nlanes] = static_cast<double>(depth * 4 + kind);
-    ++tp;
-  };
   Counters C = {0, 0, 0, 0, 0, 0, 0};
   const RtxRenderParams& P = F.P;
   const double aterm = P.aterm_thresh;
   const int ncam = P.dof ? P.dof_div + 1 : 1;
 
-  // ---- lane state (kept small: everything recomputable is recomputed)
-  int st = ST_IDLE;
-  int sample_slot = -1;  // sample-buffer / hit-record slot (regular) or k (adaptive)
-  bool rec_on = false;
-  double sx = 0, sy = 0;
-  int pass = 0, camk = 0, nrays = 0;
-  dvec3 acc = mk3(0, 0, 0);  // sum over camera rays of W * colour
-  int top = 0;
-  dvec3 rp = mk3(0, 0, 0), rd = mk3(0, 0, 0), W = mk3(0, 0, 0);
-  int rdepth = 0, rkind = 0;
-  bool first_query = false;
-  // shading of the current hit (re-resolved from (sobj, ssub) when needed)
-  double st_t = 0;
-  int sobj = 0, ssub = 0;
-  dvec3 N = mk3(0, 0, 0), i_out = mk3(0, 0, 0), dscomp = mk3(0, 0, 0);
-  dvec3 m_kd = mk3(0, 0, 0), m_ks = mk3(0, 0, 0);
-  double m_sh = 0, dattn = 0;
-  int m_flags = 0, li = 0, pick = 0;
-  dvec3 area_sum = mk3(0, 0, 0);
-  // shadow walk
-  dvec3 sdir = mk3(0, 0, 0), wpos = mk3(0, 0, 0), sattn = mk3(0, 0, 0);
-  double last_t = 0;
-  // query
-  int qmode = Q_NONE;
-  double qtp = 0;
-  int qrp = 0, qsq = 0;
-  double bt = 0;
-  int bobj = 0, bsub = 0;
-  bool bhave = false;
+  // ---- lane state
+  LaneState L;
+  memset(&L, 0, sizeof(L));
+#define REF(f) auto& f = L.f;
+  LANE_INT_FIELDS(REF)
+  LANE_DBL_FIELDS(REF)
+  LANE_VEC_FIELDS(REF)
+  REF(bt) REF(bobj) REF(bsub) REF(bhave)
+#undef REF
+  st = ST_IDLE;
+  sample_slot = -1;
 
   // ---- wave-uniform scheduler state
   unsigned long long qnext = 0, qend = 0;
@@ -752,303 +1070,7 @@ __global__ void __launch_bounds__(WG) render_kernel(DevScene S, const FrameParam
     }
 
     // ------------------------------------------------ advance lanes to their next query
-    qmode = Q_NONE;
-    while (st != ST_IDLE && qmode == Q_NONE) {
-      switch (st) {
-        case ST_CAM: {
-          // next camera ray of trace(x, y) (RayTracer.cpp:35-79)
-          if (camk == ncam) {
-            dvec3 ret = acc;
-            if (P.dof) ret *= (1.0 / (P.dof_div + 1.0));
-            ret = rtm::gclamp3(ret, 0.0, 1.0);
-            if (ADAPTIVE) {
-              colbuf[sample_slot * 3 + 0] = ret.x;
-              colbuf[sample_slot * 3 + 1] = ret.y;
-              colbuf[sample_slot * 3 + 2] = ret.z;
-              if (rec_on) hits[apix_out * an + sample_slot].nrays = nrays;
-              st = ST_IDLE;
-              break;
-            }
-            double* out = sbuf + static_cast<int64_t>(sample_slot) * 3;
-            if (P.anaglyph && pass == 0) {  // tracePixel (RayTracer.cpp:92-99): park pass 0 in the buffer
-              out[0] = ret.x;
-              out[1] = ret.y;
-              out[2] = ret.z;
-              pass = 1;
-              camk = 0;
-              acc = mk3(0, 0, 0);
-              break;
-            }
-            if (P.anaglyph) {
-              out[0] = ret.x;  // red from the shifted eye, green/blue from pass 0
-            } else {
-              out[0] = ret.x;
-              out[1] = ret.y;
-              out[2] = ret.z;
-            }
-            if (rec_on) hits[sample_slot].nrays = nrays;
-            st = ST_IDLE;
-            break;
-          }
-          const RtxCamera& cam = F.cam;
-          const dvec3 eye = pass ? ld3(cam.eye) + mk3(0.25, 0.0, 0.0) : ld3(cam.eye);
-          const double x = sx - 0.5, y = sy - 0.5;
-          const dvec3 cdir = rtm::normalize(ld3(cam.look) + x * ld3(cam.u) + y * ld3(cam.v));
-          if (camk == 0) {
-            rp = eye;
-            rd = cdir;
-            first_query = rec_on && pass == 0;
-            if (first_query) {  // default record: miss (also what depth < 0 leaves)
-              RtxHitRecord* hr = ADAPTIVE ? &hits[apix_out * an + sample_slot] : &hits[sample_slot];
-              hr->object = hr->face = hr->scene_leaf = hr->mesh_leaf = -1;
-              hr->t = 1000.0;
-              hr->pad = 0;
-            }
-          } else {
-            const double fd = rtm::gmax(P.dof_fd, 1.0);
-            const dvec3 fp_n = -cdir;
-            const dvec3 fp_pt = rtm::ray_at(eye, cdir, fd);
-            double t = rtm::dot(fp_n, cdir);
-            t = rtm::dot(fp_pt - eye, fp_n) / t;
-            const dvec3 dest = rtm::ray_at(eye, cdir, t);
-            rp = eye + ld3(&F.offv[(camk - 1) * 3]);
-            rd = rtm::normalize(dest - rp);
-            first_query = false;
-          }
-          camk++;
-          if (STATS) C.camera++;
-          top = 0;
-          push(top, rp, rd, mk3(1, 1, 1), mk3(1, 1, 1), P.depth, 0);
-          st = ST_POP;
-          break;
-        }
-        case ST_POP: {
-          if (top == 0) {
-            st = ST_CAM;
-            break;
-          }
-          --top;
-          const double* b = pbuf + static_cast<size_t>(top) * 13 * nlanes + glane;
-          const int dk = static_cast<int>(b[12 * nlanes]);
-          nrays++;
-          const int pdepth = dk >= 0 ? dk / 4 : -((-dk + 3) / 4);
-          if (pdepth < 0) break;  // `depth >= 0 &&` (RayTracer.cpp:116)
-          rp = mk3(b[0 * nlanes], b[1 * nlanes], b[2 * nlanes]);
-          rd = mk3(b[3 * nlanes], b[4 * nlanes], b[5 * nlanes]);
-          W = mk3(b[6 * nlanes], b[7 * nlanes], b[8 * nlanes]);
-          area_sum = mk3(b[9 * nlanes], b[10 * nlanes], b[11 * nlanes]);  // kt factor, parked until the hit
-          rdepth = pdepth;
-          rkind = dk - pdepth * 4;
-          qmode = Q_CLOSEST;
-          qtp = -RTX_INF;
-          qrp = -1;
-          qsq = -1;
-          st = ST_HIT;
-          break;
-        }
-        case ST_HIT: {
-          // traceRay after scene->intersect (RayTracer.cpp:116-165)
-          if (first_query) {
-            first_query = false;
-            if (bhave) {
-              RtxHitRecord* hr = ADAPTIVE ? &hits[apix_out * an + sample_slot] : &hits[sample_slot];
-              const RtxObject& o = S.objs[bobj];
-              hr->object = o.orig_id;
-              hr->scene_leaf = o.leaf;
-              hr->t = bt;
-              if (o.type == RTX_OBJ_TRIMESH) {
-                const RtxMesh me = S.meshes[o.mesh];
-                const RtxFaceIds fi = S.fids[me.face_off + bsub];
-                hr->face = fi.orig_id;
-                hr->mesh_leaf = fi.leaf;
-              }
-            }
-          }
-          if (!bhave) {  // miss: no cube map => black
-            st = ST_POP;
-            break;
-          }
-          if (rkind == 1)
-            W = W * rtm::gmax3(rtm::gmin3(rtm::pow3(area_sum, bt), rtm::splat3(1.0)), rtm::splat3(0.0));
-          else if (rkind == 2)
-            W = W * rtm::pow3(area_sum, bt);
-          const Resolved R = resolve_hit(S, rp, rd, bobj, bsub, nullptr, nullptr);
-          N = R.N;
-          m_kd = R.m.kd;
-          m_ks = R.m.ks;
-          m_sh = R.m.sh;
-          m_flags = R.m.flags;
-          st_t = bt;
-          sobj = bobj;
-          ssub = bsub;
-          if (STATS) C.shades++;
-          // Material::shade (material.cpp:34-69)
-          i_out = R.m.ke + R.m.ka * mk3(S.ambient[0], S.ambient[1], S.ambient[2]);
-          li = 0;
-          st = ST_LIGHT;
-          break;
-        }
-        case ST_LIGHT: {
-          if (li == S.n_lights) {
-            // colorC = shade(...); adaptive termination; recursion
-            const dvec3 col = i_out;
-            acc += W * col;
-            const int depth = rdepth - 1;
-            st = ST_POP;
-            if (aterm > 0.0 && rtm::dot(col, col) < aterm) break;
-            if ((m_flags & RTX_MF_RECUR) && depth > 0) {
-              const Resolved R = resolve_hit(S, rp, rd, sobj, ssub, nullptr, nullptr);
-              const bool leaving = rtm::dot(N, rd) >= 0;
-              const bool in_trans = (m_flags & RTX_MF_TRANS) != 0;
-              const bool next_trans = leaving ? true : in_trans;  // air is transmissive
-              const dvec3 normal = (leaving ? -1.0 : 1.0) * N;
-              const double c = -1 * rtm::dot(normal, rd);
-              const double eta =
-                  next_trans ? (leaving ? R.m.index : S.air_index) / (leaving ? S.air_index : R.m.index) : 0;
-              const double radicand = 1 - eta * eta * (1 - c * c);
-              const bool tir = next_trans && radicand < 0;
-              // push refraction first so that reflection is traced first
-              if (next_trans && !tir && top < pend_cap) {
-                const dvec3 tp = rtm::ray_at(rp, rd, st_t + RTX_RAY_EPS);
-                const dvec3 td = eta * rd + (eta * c - sqrt(radicand)) * normal;
-                push(top, tp, td, W, leaving ? mk3(1.0, 1.0, 1.0) : R.m.kt, depth, 2);
-                if (STATS) C.secondary++;
-              }
-              if (((m_flags & RTX_MF_REFL) || tir) && top < pend_cap) {
-                const dvec3 rdir = rd + 2 * c * normal;
-                const dvec3 rs = rtm::ray_at(rp, rd, st_t - RTX_RAY_EPS);
-                push(top, rs, rdir, W * R.m.kr, leaving ? R.m.kt : mk3(1.0, 1.0, 1.0), depth, 1);
-                if (STATS) C.secondary++;
-              }
-            }
-            break;
-          }
-          const RtxLight& L = S.lights[li];
-          const dvec3 X = rtm::ray_at(rp, rd, st_t);
-          const dvec3 l_i = light_dir(L, X);
-          const dvec3 l_r = (l_i - 2 * (rtm::dot(l_i, N)) * N);
-          double dt = rtm::dot(l_i, N);
-          if (m_flags & RTX_MF_TRANS) dt = fabs(dt);
-          const dvec3 d_comp = m_kd * rtm::gmax(0.0, dt);
-          const dvec3 s_comp = m_ks * rtm::pow3(rtm::splat3(rtm::gmax(0.0, rtm::dot(l_r, rd))), m_sh);
-          dscomp = d_comp + s_comp;
-          dattn = light_dist_atten(L, X);
-          // shadowAttenuation (light.cpp:16-20) / AreaLight (light.cpp:76-87)
-          if (L.type == RTX_LIGHT_DIRECTIONAL || L.type == RTX_LIGHT_POINT) {
-            sdir = light_dir(L, X - rd * RTX_EPS_BACKUP);
-            pick = -1;
-          } else {
-            const dvec3 ori = ld3(L.orient), lpos = ld3(L.pos);
-            if (L.type == RTX_LIGHT_SPOT &&
-                !((rtm::dot(light_dir(L, X), ori) <= 0) &&
-                  (rtm::dot(rtm::normalize(X - (lpos - L.offset * ori)), ori) > S.cos45))) {
-              i_out += dattn * mk3(0.0, 0.0, 0.0) * ld3(L.color) * dscomp;
-              li++;
-              break;
-            }
-            area_sum = mk3(1.0, 1.0, 1.0);
-            pick = 0;
-          }
-          st = ST_SRS;
-          break;
-        }
-        case ST_SRS: {
-          // start one srsAttenuation (light.cpp:21-53), or finish an area light
-          const RtxLight& L = S.lights[li];
-          const dvec3 pb = rtm::ray_at(rp, rd, st_t) - rd * RTX_EPS_BACKUP;
-          if (pick >= 0) {
-            bool started = false;
-            while (pick < S.ss_res) {
-              const dvec3 lp = ld3(S.picks + (size_t(li) * S.ss_res + pick) * 3);
-              pick++;
-              if (L.type == RTX_LIGHT_SPOT &&
-                  !((rtm::dot(light_dir(L, pb), ld3(L.orient)) <= 0) &&
-                    (rtm::dot(rtm::normalize(pb - lp), ld3(L.orient)) > S.cos45)))
-                continue;
-              sdir = rtm::normalize(lp - pb);
-              started = true;
-              break;
-            }
-            if (!started) {
-              dvec3 sa = area_sum;
-              sa *= (1.0 / (S.ss_res - 1));
-              i_out += dattn * sa * ld3(L.color) * dscomp;
-              li++;
-              st = ST_LIGHT;
-              break;
-            }
-          }
-          if (STATS) C.shadow++;
-          nrays++;
-          sattn = mk3(1.0, 1.0, 1.0);
-          wpos = pb;
-          last_t = 0.0;
-          qmode = Q_NEXT;
-          qtp = -RTX_INF;
-          qrp = -1;
-          qsq = -1;
-          st = ST_WALK;
-          break;
-        }
-        case ST_WALK: {
-          const RtxLight& L = S.lights[li];
-          bool done = false;
-          dvec3 result = sattn;
-          if (!bhave) {
-            done = true;
-          } else {
-            const double t = bt - last_t;
-            last_t = bt;
-            const dvec3 pb = rtm::ray_at(rp, rd, st_t) - rd * RTX_EPS_BACKUP;
-            const Resolved R = resolve_hit(S, pb, sdir, bobj, bsub, nullptr, nullptr);
-            const bool is_inside = rtm::dot(R.N, sdir) > 0;
-            wpos = rtm::ray_at(wpos, sdir, t);
-            bool limit = false;  // sattnLimitCheck with the relative t (U14)
-            if (L.type == RTX_LIGHT_POINT) {
-              limit = rtm::dot(ld3(L.pos) - rtm::ray_at(wpos, sdir, t), sdir) <= 0;
-            } else if (L.type != RTX_LIGHT_DIRECTIONAL) {
-              const dvec3 ori = ld3(L.orient), lpos = ld3(L.pos);
-              double ti = rtm::dot(ori, sdir);
-              ti = rtm::dot(lpos - wpos, ori) / ti;
-              dvec3 imp = rtm::ray_at(wpos, sdir, ti);
-              if (L.type != RTX_LIGHT_AREA_RECT && !(rtm::dot(imp - lpos, imp - lpos) < (L.radius * L.radius)))
-                imp = mk3(0.0, 0.0, 0.0);
-              limit = rtm::dot(imp - rtm::ray_at(wpos, sdir, t), sdir) <= 0;
-            }
-            if (limit) {
-              done = true;
-            } else {
-              const bool next_trans = is_inside ? true : ((R.m.flags & RTX_MF_TRANS) != 0);
-              if (!next_trans || (aterm > 0.0 && rtm::dot(sattn, sattn) < aterm * aterm)) {
-                result = mk3(0.0, 0.0, 0.0);
-                done = true;
-              } else {
-                const dvec3 kt = is_inside ? R.m.kt : mk3(1.0, 1.0, 1.0);
-                sattn *= rtm::pow3(kt, t);
-                qmode = Q_NEXT;
-                qtp = bt;
-                qrp = bobj;
-                qsq = bsub;
-              }
-            }
-          }
-          if (done) {
-            if (pick < 0) {
-              i_out += dattn * result * ld3(L.color) * dscomp;
-              li++;
-              st = ST_LIGHT;
-            } else {
-              area_sum += result;
-              st = ST_SRS;
-            }
-          }
-          break;
-        }
-        default:
-          st = ST_IDLE;
-          break;
-      }
-    }
+    advance_lane<STATS, ADAPTIVE>(L, S, F, C, sbuf, colbuf, hits, apix_out, an, pbuf, nlanes, glane, pend_cap);
 
     // ------------------------------------------------ exit / traversal
     const unsigned long long busy = __ballot(qmode != Q_NONE);
@@ -1076,6 +1098,230 @@ __global__ void __launch_bounds__(WG) render_kernel(DevScene S, const FrameParam
       int64_t x = v[k];
       for (int off = 32; off > 0; off >>= 1) x += __shfl_down(x, off);
       if (lane == 0) atomicAdd(&stats[k], static_cast<unsigned long long>(x));
+    }
+  }
+}
+
+// ============================================================ wavefront path
+// Path slots: NSLOT lanes' LaneState kept SoA in HBM.  Each iteration:
+//   advance_kernel  — one thread per slot: load state (+ last query result),
+//                     run the state machine to the next query, append the
+//                     query to the closest-hit or next-hit list (wave ballot
+//                     + popc + one atomic per wave, mbcnt for the offset:
+//                     compaction of the active-ray mask), store state;
+//   trace_kernel<Q> — one thread per compacted query: traverse, write result.
+// Samples are dealt to slots statically (sample slot + k * NSLOT).
+struct SlotArrays {
+  int* iv;      // LANE_INT_FIELDS, field-major [field][slot]
+  double* dv;   // LANE_DBL_FIELDS then LANE_VEC_FIELDS (x, y, z), field-major
+  double* res_t;
+  int* res_i;   // [0]: obj, [1]: sub, [2]: have  (field-major)
+};
+
+struct QList {
+  int* slot;    // [cap]
+  double* d;    // Px Py Pz Dx Dy Dz tp tlimit, field-major [8][cap]
+  int* iv;      // rp, sq  [2][cap]
+};
+
+#define N_INT_FIELDS 19
+#define N_DBL_FIELDS (7 + 13 * 3)
+
+__device__ __forceinline__ void load_lane(LaneState& L, const SlotArrays& A, int slot, int nslot) {
+  int fi = 0;
+#define LI(f) L.f = A.iv[static_cast<size_t>(fi++) * nslot + slot];
+  LANE_INT_FIELDS(LI)
+#undef LI
+  int fd = 0;
+#define LD(f) L.f = A.dv[static_cast<size_t>(fd++) * nslot + slot];
+  LANE_DBL_FIELDS(LD)
+#undef LD
+#define LV(f)                                               \
+  L.f.x = A.dv[static_cast<size_t>(fd++) * nslot + slot]; \
+  L.f.y = A.dv[static_cast<size_t>(fd++) * nslot + slot]; \
+  L.f.z = A.dv[static_cast<size_t>(fd++) * nslot + slot];
+  LANE_VEC_FIELDS(LV)
+#undef LV
+}
+
+__device__ __forceinline__ void store_lane(const LaneState& L, const SlotArrays& A, int slot, int nslot) {
+  int fi = 0;
+#define SI(f) A.iv[static_cast<size_t>(fi++) * nslot + slot] = L.f;
+  LANE_INT_FIELDS(SI)
+#undef SI
+  int fd = 0;
+#define SD(f) A.dv[static_cast<size_t>(fd++) * nslot + slot] = L.f;
+  LANE_DBL_FIELDS(SD)
+#undef SD
+#define SV(f)                                               \
+  A.dv[static_cast<size_t>(fd++) * nslot + slot] = L.f.x; \
+  A.dv[static_cast<size_t>(fd++) * nslot + slot] = L.f.y; \
+  A.dv[static_cast<size_t>(fd++) * nslot + slot] = L.f.z;
+  LANE_VEC_FIELDS(SV)
+#undef SV
+}
+
+__device__ __forceinline__ unsigned int lane_prefix(unsigned long long mask) {
+  return __builtin_amdgcn_mbcnt_hi(static_cast<unsigned int>(mask >> 32),
+                                   __builtin_amdgcn_mbcnt_lo(static_cast<unsigned int>(mask), 0u));
+}
+
+// Claim the next statically dealt sample for an idle slot (what the
+// scheduler of the megakernel does with its queue).
+__device__ __forceinline__ void claim_sample(LaneState& L, const FrameParams& F, RtxHitRecord* hits, int slot,
+                                             int nslot) {
+  const RtxRenderParams& P = F.P;
+  while (L.st == ST_IDLE) {
+    const int64_t sid = static_cast<int64_t>(slot) + static_cast<int64_t>(L.kdone) * nslot;
+    if (sid >= F.n_samples) return;
+    L.kdone++;
+    const int64_t item = sid / (F.ppw * F.spp);
+    const int sl = static_cast<int>(sid % (F.ppw * F.spp));
+    const int pix = sl / F.spp, smp = sl % F.spp;
+    int i, j;
+    int64_t oidx;
+    if (!item_pixel(F, item, pix, i, j, oidx)) continue;
+    int pi = i, pj = j;
+    double ssx = 1.0, ssy = 1.0;
+    if (P.aa_mode != RTX_AA_NONE) {  // tracePixel(i*s + si, j*s + sj)
+      pi = i * F.s + smp / F.s;
+      pj = j * F.s + smp % F.s;
+      ssx = F.s;
+      ssy = F.s;
+    }
+    L.sx = double(pi) / (double(P.width) * ssx);  // tracePixel (RayTracer.cpp:87-88)
+    L.sy = double(pj) / (double(P.height) * ssy);
+    L.sample_slot = static_cast<int>(oidx * F.spp + smp);
+    L.rec_on = hits != nullptr;
+    L.pass = 0;
+    L.camk = 0;
+    L.nrays = 0;
+    L.acc = mk3(0, 0, 0);
+    L.st = ST_CAM;
+  }
+}
+
+template <bool STATS>
+__global__ void __launch_bounds__(WG) advance_kernel(DevScene S, const FrameParams* __restrict__ Fp, SlotArrays A,
+                                                      int nslot, double* __restrict__ sbuf,
+                                                      RtxHitRecord* __restrict__ hits, double* __restrict__ pbuf,
+                                                      int pend_cap, QList q0, QList q1,
+                                                      unsigned int* __restrict__ counters,
+                                                      unsigned long long* __restrict__ stats) {
+  const FrameParams& F = *Fp;
+  const int slot = blockIdx.x * WG + threadIdx.x;
+  const bool valid = slot < nslot;
+  Counters C = {0, 0, 0, 0, 0, 0, 0};
+  LaneState L;
+  L.st = ST_IDLE;
+  L.qmode = Q_NONE;
+  L.kdone = 0;
+  bool loaded = false;
+  if (valid) {
+    L.st = A.iv[slot];                                       // field 0 = st
+    L.kdone = A.iv[static_cast<size_t>(18) * nslot + slot];  // field 18 = kdone
+    if (L.st != ST_IDLE || static_cast<int64_t>(slot) + static_cast<int64_t>(L.kdone) * nslot < F.n_samples) {
+      loaded = true;
+      load_lane(L, A, slot, nslot);
+      if (L.qmode != Q_NONE) {  // result of the previous iteration's query
+        L.bt = A.res_t[slot];
+        L.bobj = A.res_i[slot];
+        L.bsub = A.res_i[static_cast<size_t>(nslot) + slot];
+        L.bhave = A.res_i[static_cast<size_t>(2) * nslot + slot];
+      }
+      L.qmode = Q_NONE;
+      for (;;) {
+        claim_sample(L, F, hits, slot, nslot);
+        if (L.st == ST_IDLE) break;
+        advance_lane<STATS, false>(L, S, F, C, sbuf, nullptr, hits, 0, 0, pbuf, static_cast<size_t>(nslot),
+                                   static_cast<size_t>(slot), pend_cap);
+        if (L.qmode != Q_NONE) break;
+      }
+    }
+  }
+  // compaction: append queries to their list, one atomic per wave per list
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int m = Q_CLOSEST; m <= Q_NEXT; ++m) {
+    const unsigned long long mask = __ballot(valid && L.qmode == m);
+    if (mask == 0ull) continue;
+    unsigned int base = 0;
+    if (lane == 0) base = atomicAdd(&counters[m - 1], static_cast<unsigned int>(__popcll(mask)));
+    base = __shfl(base, 0);
+    if (valid && L.qmode == m) {
+      const QList& Q = m == Q_CLOSEST ? q0 : q1;
+      const size_t cap = static_cast<size_t>(nslot);
+      const unsigned int k = base + lane_prefix(mask);
+      dvec3 qP = L.rp, qD = L.rd;
+      double qlim = RTX_INF;
+      if (m == Q_NEXT) {
+        qP = rtm::ray_at(L.rp, L.rd, L.st_t) - L.rd * RTX_EPS_BACKUP;
+        qD = L.sdir;
+        const RtxLight& Lt = S.lights[L.li];
+        // any hit past a point light trips the limit check
+        if (Lt.type == RTX_LIGHT_POINT) qlim = rtm::distance(qP, ld3(Lt.pos)) * (1.0 + 1e-6) + S.margin;
+      }
+      Q.slot[k] = slot;
+      Q.d[0 * cap + k] = qP.x;
+      Q.d[1 * cap + k] = qP.y;
+      Q.d[2 * cap + k] = qP.z;
+      Q.d[3 * cap + k] = qD.x;
+      Q.d[4 * cap + k] = qD.y;
+      Q.d[5 * cap + k] = qD.z;
+      Q.d[6 * cap + k] = L.qtp;
+      Q.d[7 * cap + k] = qlim;
+      Q.iv[0 * cap + k] = L.qrp;
+      Q.iv[1 * cap + k] = L.qsq;
+    }
+  }
+  const unsigned long long alive = __ballot(valid && L.st != ST_IDLE);
+  if (lane == 0 && alive) atomicAdd(&counters[2], static_cast<unsigned int>(__popcll(alive)));
+  if (loaded) store_lane(L, A, slot, nslot);
+  if (STATS) {
+    int64_t v[7] = {C.camera, C.secondary, C.shadow, C.nodes, C.objects, C.tris, C.shades};
+#pragma unroll
+    for (int k = 0; k < 7; ++k) {
+      int64_t x = v[k];
+      for (int off = 32; off > 0; off >>= 1) x += __shfl_down(x, off);
+      if (lane == 0 && x) atomicAdd(&stats[k], static_cast<unsigned long long>(x));
+    }
+  }
+}
+
+template <bool STATS, int MODE>
+__global__ void __launch_bounds__(WG) trace_kernel(DevScene S, QList Q, const unsigned int* __restrict__ counters,
+                                                    SlotArrays A, int nslot, int stack_cap,
+                                                    unsigned long long* __restrict__ stats) {
+  extern __shared__ int lds_stack[];
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  int* stk = lds_stack + wave * stack_cap * 64;
+  const unsigned int n = counters[MODE - 1];
+  const size_t cap = static_cast<size_t>(nslot);
+  Counters C = {0, 0, 0, 0, 0, 0, 0};
+  for (unsigned int k = blockIdx.x * WG + threadIdx.x; k < ((n + 63u) & ~63u); k += gridDim.x * WG) {
+    if (k < n) {
+      const dvec3 P = mk3(Q.d[0 * cap + k], Q.d[1 * cap + k], Q.d[2 * cap + k]);
+      const dvec3 D = mk3(Q.d[3 * cap + k], Q.d[4 * cap + k], Q.d[5 * cap + k]);
+      const double tp = Q.d[6 * cap + k], tlim = Q.d[7 * cap + k];
+      const int rp = Q.iv[0 * cap + k], sq = Q.iv[1 * cap + k];
+      double bt;
+      int bobj, bsub;
+      const bool have = traverse<STATS>(S, MODE, P, D, tp, rp, sq, tlim, bt, bobj, bsub, stk, lane, C);
+      const int slot = Q.slot[k];
+      A.res_t[slot] = bt;
+      A.res_i[slot] = bobj;
+      A.res_i[static_cast<size_t>(nslot) + slot] = bsub;
+      A.res_i[static_cast<size_t>(2) * nslot + slot] = have ? 1 : 0;
+    }
+  }
+  if (STATS) {
+    int64_t v[3] = {C.nodes, C.objects, C.tris};
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      int64_t x = v[k];
+      for (int off = 32; off > 0; off >>= 1) x += __shfl_down(x, off);
+      if (lane == 0 && x) atomicAdd(&stats[3 + k], static_cast<unsigned long long>(x));
     }
   }
 }
@@ -1150,6 +1396,13 @@ struct SceneState {
   size_t sbuf_bytes = 0;
   double* d_pbuf = nullptr;     // per-lane pending-ray stacks (HBM)
   size_t pbuf_bytes = 0;
+  // wavefront path: slot state, query lists, counters
+  void* d_wf = nullptr;
+  size_t wf_bytes = 0;
+  unsigned int* d_counters = nullptr;
+  unsigned int* h_counters = nullptr;  // pinned
+  std::vector<hipEvent_t> ev_pool;
+  size_t ev_used = 0;
   std::vector<hipEvent_t> ev_start, ev_stop;
 };
 
@@ -1328,6 +1581,10 @@ rtx_status rtx_scene_destroy(void* scene) {
   if (st->d_picks) (void)hipFree(st->d_picks);
   if (st->d_sbuf) (void)hipFree(st->d_sbuf);
   if (st->d_pbuf) (void)hipFree(st->d_pbuf);
+  if (st->d_wf) (void)hipFree(st->d_wf);
+  if (st->d_counters) (void)hipFree(st->d_counters);
+  if (st->h_counters) (void)hipHostFree(st->h_counters);
+  for (auto e : st->ev_pool) (void)hipEventDestroy(e);
   for (auto e : st->ev_start) (void)hipEventDestroy(e);
   for (auto e : st->ev_stop) (void)hipEventDestroy(e);
   delete st;
@@ -1494,81 +1751,207 @@ rtx_status rtx_render(void* scene, const RtxRenderParams* params, uint8_t* rgb8,
   }
   HIP_TRY(hipMemsetAsync(st->d_work, 0, sizeof(unsigned long long), stream));
   if (stats) HIP_TRY(hipMemsetAsync(st->d_stats, 0, 8 * sizeof(unsigned long long), stream));
-
-  const int cslots = adaptive ? (F.spp > 64 ? F.spp : 64) : 0;
-  const int fslots = adaptive ? 16 * 8 : 0;
-  const size_t lds_per_wave =
-      size_t(cslots * 3 + fslots) * sizeof(double) + size_t(st->stack_cap) * 64 * sizeof(int);
-  const size_t lds = lds_per_wave * WAVES_PER_WG;
-  if (lds > 160 * 1024) {
-    g_err = "rtx_render: LDS budget exceeded (BVH too deep or too many AA samples)";
-    for (void* p : tmp) (void)hipFree(p);
-    return RTX_ERR_CAPACITY;
-  }
-  // persistent grid: as many resident workgroups as the occupancy allows
-  const void* kfn = stats ? (adaptive ? reinterpret_cast<const void*>(render_kernel<true, true>)
-                                      : reinterpret_cast<const void*>(render_kernel<true, false>))
-                          : (adaptive ? reinterpret_cast<const void*>(render_kernel<false, true>)
-                                      : reinterpret_cast<const void*>(render_kernel<false, false>));
-  int per_cu = 0;
-  HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kfn, WG, lds));
-  if (per_cu < 1) per_cu = 1;
-  int64_t grid = static_cast<int64_t>(st->n_cu) * per_cu;
-  const int64_t waves_needed = adaptive ? F.n_items : (F.n_samples + 63) / 64;
-  const int64_t grid_needed = (waves_needed + WAVES_PER_WG - 1) / WAVES_PER_WG;
-  if (grid > grid_needed) grid = grid_needed;
-  if (grid < 1) grid = 1;
-  {
-    // queue chunk: up to QCHUNK samples per atomic, but small frames must
-    // still spread over every wave
-    const int64_t waves = grid * WAVES_PER_WG;
-    int64_t c = F.n_samples / (waves * 4);
-    c = (c / 64) * 64;
-    if (c < 64) c = 64;
-    if (c > QCHUNK) c = QCHUNK;
-    F.qchunk = static_cast<int>(c);
-  }
-  HIP_TRY(hipMemcpyAsync(st->d_frame, &F, sizeof(FrameParams), hipMemcpyHostToDevice, stream));
   const int pend_cap = (params->depth > 0 ? params->depth : 0) + 2;
-  {
-    const size_t need = size_t(grid) * WG * pend_cap * 13 * sizeof(double);
-    if (need > st->pbuf_bytes) {
-      if (st->d_pbuf) (void)hipFree(st->d_pbuf);
-      st->d_pbuf = nullptr;
-      st->pbuf_bytes = 0;
-      HIP_TRY(hipMalloc(&st->d_pbuf, need));
-      st->pbuf_bytes = need;
+  auto get_event = [&](hipEvent_t* e) -> rtx_status {
+    if (!st->ev_pool.empty()) {
+      *e = st->ev_pool.back();
+      st->ev_pool.pop_back();
+      return RTX_OK;
+    }
+    HIP_TRY(hipEventCreate(e));
+    return RTX_OK;
+  };
+  auto ensure = [&](void** ptr, size_t* have, size_t need) -> rtx_status {
+    if (need > *have) {
+      if (*ptr) (void)hipFree(*ptr);
+      *ptr = nullptr;
+      *have = 0;
+      HIP_TRY(hipMalloc(ptr, need));
+      *have = need;
+    }
+    return RTX_OK;
+  };
+  // megakernel by default; RTX_WAVEFRONT=1 selects the wavefront path for
+  // non-adaptive frames (kernels)
+  const char* wf_env = getenv("RTX_WAVEFRONT");
+  const bool megakernel = adaptive || !(wf_env && atoi(wf_env) != 0);
+  double* sb = adaptive ? nullptr : st->d_sbuf;
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> frame_events;
+
+  if (megakernel) {
+    const int cslots = adaptive ? (F.spp > 64 ? F.spp : 64) : 0;
+    const int fslots = adaptive ? 16 * 8 : 0;
+    const size_t lds_per_wave =
+        size_t(cslots * 3 + fslots) * sizeof(double) + size_t(st->stack_cap) * 64 * sizeof(int);
+    const size_t lds = lds_per_wave * WAVES_PER_WG;
+    if (lds > 160 * 1024) {
+      g_err = "rtx_render: LDS budget exceeded (BVH too deep or too many AA samples)";
+      for (void* p : tmp) (void)hipFree(p);
+      return RTX_ERR_CAPACITY;
+    }
+    // persistent grid: as many resident workgroups as the occupancy allows
+    const void* kfn = stats ? (adaptive ? reinterpret_cast<const void*>(render_kernel<true, true>)
+                                        : reinterpret_cast<const void*>(render_kernel<true, false>))
+                            : (adaptive ? reinterpret_cast<const void*>(render_kernel<false, true>)
+                                        : reinterpret_cast<const void*>(render_kernel<false, false>));
+    int per_cu = 0;
+    HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kfn, WG, lds));
+    if (per_cu < 1) per_cu = 1;
+    int64_t grid = static_cast<int64_t>(st->n_cu) * per_cu;
+    const int64_t waves_needed = adaptive ? F.n_items : (F.n_samples + 63) / 64;
+    const int64_t grid_needed = (waves_needed + WAVES_PER_WG - 1) / WAVES_PER_WG;
+    if (grid > grid_needed) grid = grid_needed;
+    if (grid < 1) grid = 1;
+    {
+      // queue chunk: up to QCHUNK samples per atomic, but small frames must
+      // still spread over every wave
+      const int64_t waves = grid * WAVES_PER_WG;
+      int64_t c = F.n_samples / (waves * 4);
+      c = (c / 64) * 64;
+      if (c < 64) c = 64;
+      if (c > QCHUNK) c = QCHUNK;
+      F.qchunk = static_cast<int>(c);
+    }
+    HIP_TRY(hipMemcpyAsync(st->d_frame, &F, sizeof(FrameParams), hipMemcpyHostToDevice, stream));
+    if ((rc = ensure(reinterpret_cast<void**>(&st->d_pbuf), &st->pbuf_bytes,
+                     size_t(grid) * WG * pend_cap * 13 * sizeof(double))) != RTX_OK)
+      return rc;
+    hipEvent_t e0, e1;
+    if ((rc = get_event(&e0)) != RTX_OK || (rc = get_event(&e1)) != RTX_OK) return rc;
+    HIP_TRY(hipEventRecord(e0, stream));
+    if (stats) {
+      if (adaptive)
+        hipLaunchKernelGGL((render_kernel<true, true>), dim3(grid), dim3(WG), lds, stream, st->S_launch, st->d_frame,
+                           st->d_work, sb, d_hits, d_rgb8, d_rgbf, st->d_stats, st->stack_cap, st->d_pbuf, pend_cap);
+      else
+        hipLaunchKernelGGL((render_kernel<true, false>), dim3(grid), dim3(WG), lds, stream, st->S_launch,
+                           st->d_frame, st->d_work, sb, d_hits, d_rgb8, d_rgbf, st->d_stats, st->stack_cap,
+                           st->d_pbuf, pend_cap);
+    } else {
+      if (adaptive)
+        hipLaunchKernelGGL((render_kernel<false, true>), dim3(grid), dim3(WG), lds, stream, st->S_launch,
+                           st->d_frame, st->d_work, sb, d_hits, d_rgb8, d_rgbf, st->d_stats, st->stack_cap,
+                           st->d_pbuf, pend_cap);
+      else
+        hipLaunchKernelGGL((render_kernel<false, false>), dim3(grid), dim3(WG), lds, stream, st->S_launch,
+                           st->d_frame, st->d_work, sb, d_hits, d_rgb8, d_rgbf, st->d_stats, st->stack_cap,
+                           st->d_pbuf, pend_cap);
+    }
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipEventRecord(e1, stream));
+    frame_events.push_back({e0, e1});
+  } else {
+    // ---------------- wavefront path
+    int64_t nslot64 = static_cast<int64_t>(st->n_cu) * 2048;
+    const char* ns_env = getenv("RTX_SLOTS");
+    if (ns_env && atoll(ns_env) > 0) nslot64 = atoll(ns_env);
+    if (nslot64 > F.n_samples) nslot64 = F.n_samples;
+    nslot64 = ((nslot64 + WG - 1) / WG) * WG;
+    if (nslot64 < WG) nslot64 = WG;
+    const int nslot = static_cast<int>(nslot64);
+    const size_t ns = static_cast<size_t>(nslot);
+    const size_t bytes_iv = ns * N_INT_FIELDS * sizeof(int);
+    const size_t bytes_dv = ns * N_DBL_FIELDS * sizeof(double);
+    const size_t bytes_rt = ns * sizeof(double);
+    const size_t bytes_ri = ns * 3 * sizeof(int);
+    const size_t bytes_q = ns * (sizeof(int) + 8 * sizeof(double) + 2 * sizeof(int));
+    auto al = [](size_t x) { return (x + 255) & ~size_t(255); };
+    const size_t total = al(bytes_iv) + al(bytes_dv) + al(bytes_rt) + al(bytes_ri) + 2 * al(bytes_q);
+    if ((rc = ensure(&st->d_wf, &st->wf_bytes, total)) != RTX_OK) return rc;
+    if ((rc = ensure(reinterpret_cast<void**>(&st->d_pbuf), &st->pbuf_bytes,
+                     ns * pend_cap * 13 * sizeof(double))) != RTX_OK)
+      return rc;
+    if (!st->d_counters) HIP_TRY(hipMalloc(&st->d_counters, 4 * sizeof(unsigned int)));
+    if (!st->h_counters) HIP_TRY(hipHostMalloc(&st->h_counters, 4 * sizeof(unsigned int)));
+    char* base = static_cast<char*>(st->d_wf);
+    SlotArrays A;
+    A.iv = reinterpret_cast<int*>(base);
+    base += al(bytes_iv);
+    A.dv = reinterpret_cast<double*>(base);
+    base += al(bytes_dv);
+    A.res_t = reinterpret_cast<double*>(base);
+    base += al(bytes_rt);
+    A.res_i = reinterpret_cast<int*>(base);
+    base += al(bytes_ri);
+    QList ql[2];
+    for (int m = 0; m < 2; ++m) {
+      ql[m].slot = reinterpret_cast<int*>(base);
+      ql[m].d = reinterpret_cast<double*>(base + al(ns * sizeof(int)));
+      ql[m].iv = reinterpret_cast<int*>(base + al(ns * sizeof(int)) + al(ns * 8 * sizeof(double)));
+      base += al(bytes_q);
+    }
+    F.qchunk = 64;
+    HIP_TRY(hipMemcpyAsync(st->d_frame, &F, sizeof(FrameParams), hipMemcpyHostToDevice, stream));
+    HIP_TRY(hipMemsetAsync(A.iv, 0, bytes_iv, stream));  // every slot ST_IDLE, kdone = 0, no pending query
+    const size_t lds = size_t(st->stack_cap) * 64 * sizeof(int) * WAVES_PER_WG;
+    if (lds > 160 * 1024) {
+      g_err = "rtx_render: LDS budget exceeded (BVH too deep)";
+      for (void* p : tmp) (void)hipFree(p);
+      return RTX_ERR_CAPACITY;
+    }
+    const void* tfn = stats ? reinterpret_cast<const void*>(trace_kernel<true, Q_CLOSEST>)
+                            : reinterpret_cast<const void*>(trace_kernel<false, Q_CLOSEST>);
+    int per_cu = 0;
+    HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, tfn, WG, lds));
+    if (per_cu < 1) per_cu = 1;
+    int64_t tgrid = static_cast<int64_t>(st->n_cu) * per_cu;
+    const int64_t tneed = (nslot64 + WG - 1) / WG;
+    if (tgrid > tneed) tgrid = tneed;
+    const int agrid = nslot / WG;
+    const char* dbg_env = getenv("RTX_DEBUG");
+    const bool dbg = dbg_env && atoi(dbg_env) != 0;
+    const int check_every = dbg ? 1 : 8;
+    bool done = false;
+    for (int it = 0; !done; ++it) {
+      HIP_TRY(hipMemsetAsync(st->d_counters, 0, 3 * sizeof(unsigned int), stream));
+      if (stats)
+        hipLaunchKernelGGL((advance_kernel<true>), dim3(agrid), dim3(WG), 0, stream, S, st->d_frame, A, nslot, sb,
+                           d_hits, st->d_pbuf, pend_cap, ql[0], ql[1], st->d_counters, st->d_stats);
+      else
+        hipLaunchKernelGGL((advance_kernel<false>), dim3(agrid), dim3(WG), 0, stream, S, st->d_frame, A, nslot, sb,
+                           d_hits, st->d_pbuf, pend_cap, ql[0], ql[1], st->d_counters, st->d_stats);
+      HIP_TRY(hipGetLastError());
+      hipEvent_t e0, e1;
+      if ((rc = get_event(&e0)) != RTX_OK || (rc = get_event(&e1)) != RTX_OK) return rc;
+      HIP_TRY(hipEventRecord(e0, stream));
+      if (stats) {
+        hipLaunchKernelGGL((trace_kernel<true, Q_CLOSEST>), dim3(tgrid), dim3(WG), lds, stream, S, ql[0],
+                           st->d_counters, A, nslot, st->stack_cap, st->d_stats);
+        hipLaunchKernelGGL((trace_kernel<true, Q_NEXT>), dim3(tgrid), dim3(WG), lds, stream, S, ql[1],
+                           st->d_counters, A, nslot, st->stack_cap, st->d_stats);
+      } else {
+        hipLaunchKernelGGL((trace_kernel<false, Q_CLOSEST>), dim3(tgrid), dim3(WG), lds, stream, S, ql[0],
+                           st->d_counters, A, nslot, st->stack_cap, st->d_stats);
+        hipLaunchKernelGGL((trace_kernel<false, Q_NEXT>), dim3(tgrid), dim3(WG), lds, stream, S, ql[1],
+                           st->d_counters, A, nslot, st->stack_cap, st->d_stats);
+      }
+      HIP_TRY(hipGetLastError());
+      HIP_TRY(hipEventRecord(e1, stream));
+      frame_events.push_back({e0, e1});
+      if (it % check_every == check_every - 1) {
+        HIP_TRY(hipMemcpyAsync(st->h_counters, st->d_counters, 3 * sizeof(unsigned int), hipMemcpyDeviceToHost,
+                               stream));
+        HIP_TRY(hipStreamSynchronize(stream));
+        if (dbg)
+          fprintf(stderr, "rtx iter %d: closest %u next %u alive %u (nslot %d)\n", it, st->h_counters[0],
+                  st->h_counters[1], st->h_counters[2], nslot);
+        if (st->h_counters[2] == 0) done = true;  // no live slot after this advance
+      }
+      if (it > 1000000) {
+        g_err = "rtx_render: wavefront loop did not terminate";
+        return RTX_ERR_INVALID;
+      }
     }
   }
-  hipEvent_t e0 = nullptr, e1 = nullptr;
-  HIP_TRY(hipEventCreate(&e0));
-  HIP_TRY(hipEventCreate(&e1));
-  HIP_TRY(hipEventRecord(e0, stream));
-  double* sb = adaptive ? nullptr : st->d_sbuf;
-  if (stats) {
-    if (adaptive)
-      hipLaunchKernelGGL((render_kernel<true, true>), dim3(grid), dim3(WG), lds, stream, st->S_launch, st->d_frame,
-                         st->d_work, sb, d_hits, d_rgb8, d_rgbf, st->d_stats, st->stack_cap, st->d_pbuf, pend_cap);
-    else
-      hipLaunchKernelGGL((render_kernel<true, false>), dim3(grid), dim3(WG), lds, stream, st->S_launch, st->d_frame,
-                         st->d_work, sb, d_hits, d_rgb8, d_rgbf, st->d_stats, st->stack_cap, st->d_pbuf, pend_cap);
-  } else {
-    if (adaptive)
-      hipLaunchKernelGGL((render_kernel<false, true>), dim3(grid), dim3(WG), lds, stream, st->S_launch, st->d_frame,
-                         st->d_work, sb, d_hits, d_rgb8, d_rgbf, st->d_stats, st->stack_cap, st->d_pbuf, pend_cap);
-    else
-      hipLaunchKernelGGL((render_kernel<false, false>), dim3(grid), dim3(WG), lds, stream, st->S_launch,
-                         st->d_frame, st->d_work, sb, d_hits, d_rgb8, d_rgbf, st->d_stats, st->stack_cap, st->d_pbuf, pend_cap);
-  }
-  HIP_TRY(hipGetLastError());
-  HIP_TRY(hipEventRecord(e1, stream));
   if (!adaptive) {
     const int64_t rblocks = (npix + WG - 1) / WG;
     hipLaunchKernelGGL(reduce_kernel, dim3(rblocks), dim3(WG), 0, stream, st->d_frame, sb, d_rgb8, d_rgbf, npix);
     HIP_TRY(hipGetLastError());
   }
-  st->ev_start.push_back(e0);
-  st->ev_stop.push_back(e1);
+  for (auto& pr : frame_events) {
+    st->ev_start.push_back(pr.first);
+    st->ev_stop.push_back(pr.second);
+  }
   if (!device_ptrs) {
     if (rgb8) HIP_TRY(hipMemcpyAsync(rgb8, d_rgb8, npix * 3, hipMemcpyDeviceToHost, stream));
     if (rgb_f64) HIP_TRY(hipMemcpyAsync(rgb_f64, d_rgbf, npix * 3 * sizeof(double), hipMemcpyDeviceToHost, stream));
@@ -1589,9 +1972,13 @@ rtx_status rtx_render(void* scene, const RtxRenderParams* params, uint8_t* rgb8,
     stats->object_tests = c[4];
     stats->tri_tests = c[5];
     stats->shades = c[6];
-    float ms = 0.0f;
-    HIP_TRY(hipEventElapsedTime(&ms, e0, e1));
-    stats->kernel_ms = ms;
+    double tot = 0.0;
+    for (auto& pr : frame_events) {
+      float ms = 0.0f;
+      HIP_TRY(hipEventElapsedTime(&ms, pr.first, pr.second));
+      tot += ms;
+    }
+    stats->kernel_ms = tot;
   }
   return RTX_OK;
 }
@@ -1606,8 +1993,8 @@ rtx_status rtx_kernel_time(void* scene, double* total_ms, int* launches) {
     float ms = 0.0f;
     HIP_TRY(hipEventElapsedTime(&ms, st->ev_start[k], st->ev_stop[k]));
     tot += ms;
-    (void)hipEventDestroy(st->ev_start[k]);
-    (void)hipEventDestroy(st->ev_stop[k]);
+    st->ev_pool.push_back(st->ev_start[k]);
+    st->ev_pool.push_back(st->ev_stop[k]);
   }
   if (total_ms) *total_ms = tot;
   if (launches) *launches = static_cast<int>(st->ev_start.size());

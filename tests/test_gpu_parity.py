@@ -5,6 +5,8 @@ Bar (BASELINE.json north_star): pixel RGB within 1e-4 absolute; kd-node
 bit-exact; 8-bit output identical except where the oracle's 255*c sits within
 1e-9 of an integer (truncation boundary, only reachable through a last-ulp
 difference of device pow)."""
+import os
+
 import numpy as np
 import pytest
 
@@ -31,8 +33,28 @@ def _compare(gpu, ref, spp):
     assert np.array_equal(gh["t"][hit], rh["t"][hit]), "primary hit t not bit-exact"
 
 
+# render paths (DESIGN.md "Kernels"): the persistent megakernel (default), the
+# wavefront advance/trace pipeline, and the wavefront with a tiny slot pool so
+# every slot walks many samples (claim_sample's static deal)
+PATHS = {"mega": {}, "wavefront": {"RTX_WAVEFRONT": "1"}, "wavefront_256": {"RTX_WAVEFRONT": "1", "RTX_SLOTS": "256"}}
+
+
+@pytest.fixture(params=list(PATHS), ids=list(PATHS))
+def render_path(request):
+    saved = {k: os.environ.get(k) for k in ("RTX_WAVEFRONT", "RTX_SLOTS")}
+    for k in saved:
+        os.environ.pop(k, None)
+    os.environ.update(PATHS[request.param])
+    yield request.param
+    for k, v in saved.items():
+        if v is None:
+            os.environ.pop(k, None)
+        else:
+            os.environ[k] = v
+
+
 @pytest.mark.parametrize("name,scene,flags", CASES, ids=[c[0] for c in CASES])
-def test_parity(pkg, orc, name, scene, flags):
+def test_parity(pkg, orc, render_path, name, scene, flags):
     path = scene_path(scene)
     opts = pkg.RenderOptions.from_cli(flags.split())
     host = pkg.HostScene(path)
@@ -48,7 +70,7 @@ def test_parity(pkg, orc, name, scene, flags):
         assert gpu["stats"][k] == ref["stats"][k], (k, gpu["stats"][k], ref["stats"][k])
 
 
-def test_sharded_tiles_reassemble(pkg):
+def test_sharded_tiles_reassemble(pkg, render_path):
     """Tile sharding: packed shards reassemble to the full frame."""
     path = scene_path("hitchcock.ray")
     opts = pkg.RenderOptions.from_cli("-w 100 -r 2 -O r -A 2".split())
