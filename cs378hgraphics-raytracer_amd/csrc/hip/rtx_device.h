@@ -33,7 +33,31 @@ using rtm::mk3;
 #define RTX_INF 1.0e308
 #define RTX_MAX_LIGHTS 64
 
+// Device BVH layout (built from the RtxNode arrays by rtx_scene_create).
+// One record per INTERNAL node holding both children's boxes, so a visit is
+// one 128-byte fetch that tests both children and descends into the nearer
+// one first.  child[k] >= 0: index of the child's record; child[k] < 0: the
+// child is a leaf, ~child[k] = first_item << 2 | count (count 1..3,
+// kdTree.h:6).  Item ranks (DFS-leaf order) are unchanged, so the winner of
+// the lexicographic (t, rank) minimum does not depend on the visiting order.
+struct DevNode2 {
+  double box[12];      // lo0 xyz, hi0 xyz, lo1 xyz, hi1 xyz
+  int32_t child[2];
+  int32_t pad[6];
+};                     // 128 bytes
+
+// Root of a BVH (scene or one mesh): its own box + the reference to descend.
+struct DevRoot {
+  double lo[3], hi[3];
+  int32_t ref;         // >= 0: DevNode2 index; < 0: the root is a leaf (~code)
+  int32_t pad[3];
+};                     // 64 bytes
+
 struct DevScene {
+  const DevNode2* snode2;  // scene BVH, internal nodes
+  const DevNode2* mnode2;  // all mesh BVHs, internal nodes (global indices)
+  const DevRoot* mroots;   // per mesh (valid when meshes[m].node_count > 0)
+  DevRoot sroot;           // scene BVH root
   const RtxNode* snodes;
   const RtxObject* objs;
   const RtxMaterial* mats;
@@ -64,7 +88,7 @@ __host__ __device__ __forceinline__ dvec3 ld3(const double* p) { return mk3(p[0]
 // ------------------------------------------------------------------ slab
 // BoundingBox::intersect (bbox.cc:33-70), exact: same divisions, same
 // vd == 0 skip, same per-axis early outs.  Also returns tMin/tMax.
-__device__ __forceinline__ bool slab(const double* bmin, const double* bmax, const dvec3& o, const dvec3& d,
+RT_HD bool slab(const double* bmin, const double* bmax, const dvec3& o, const dvec3& d,
                                      double& tMinOut, double& tMaxOut) {
   double tMin = -1.0e308, tMax = 1.0e308;
 #pragma unroll
@@ -87,6 +111,55 @@ __device__ __forceinline__ bool slab(const double* bmin, const double* bmax, con
   tMinOut = tMin;
   tMaxOut = tMax;
   return true;
+}
+
+// Fast slab for traversal: multiplies by the ray's reciprocal direction
+// (3 divisions per ray instead of 6 per box) and only falls back to the exact
+// slab() when the rounded answer could differ from it.  (lo - o) is the same
+// in both; x * fl(1/d) differs from fl(x / d) by <= 3 ulp relative, so a
+// margin of 1e-15 relative on tMin/tMax separates certain hits and certain
+// misses from the rare ambiguous case.  Per-axis early outs of bbox.cc are
+// monotone (tMin only grows, tMax only shrinks), so deciding once at the end
+// is the same test.  `fast` is false when a direction component is so small
+// that 1/d overflows; then every box goes through slab().
+struct RayInv {
+  dvec3 inv;
+  bool fast;
+};
+
+RT_HD RayInv ray_inv(const dvec3& d) {
+  RayInv r;
+  r.fast = true;
+#pragma unroll
+  for (int a = 0; a < 3; ++a) {
+    const double v = rtm::get(d, a);
+    if (v != 0.0 && fabs(v) < 1e-290) r.fast = false;
+    rtm::set(r.inv, a, v == 0.0 ? 0.0 : 1.0 / v);
+  }
+  return r;
+}
+
+RT_HD bool box_test(const double* lo, const double* hi, const dvec3& o, const dvec3& d,
+                                         const RayInv& ri, double& a, double& b) {
+  if (!ri.fast) return slab(lo, hi, o, d, a, b);
+  double tmin = -1.0e308, tmax = 1.0e308;
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    if (rtm::get(d, k) == 0.0) continue;
+    const double iv = rtm::get(ri.inv, k), oa = rtm::get(o, k);
+    const double t1 = (lo[k] - oa) * iv;
+    const double t2 = (hi[k] - oa) * iv;
+    tmin = fmax(tmin, fmin(t1, t2));
+    tmax = fmin(tmax, fmax(t1, t2));
+  }
+  const double e1 = 1e-15 * fabs(tmin) + 1e-300, e2 = 1e-15 * fabs(tmax) + 1e-300;
+  if (tmin - e1 > tmax + e2 || tmax + e2 < RTX_RAY_EPS) return false;  // certain miss
+  if (tmin + e1 <= tmax - e2 && tmax - e2 >= RTX_RAY_EPS) {             // certain hit
+    a = tmin;
+    b = tmax;
+    return true;
+  }
+  return slab(lo, hi, o, d, a, b);
 }
 
 // ------------------------------------------------------------------ textures
@@ -188,13 +261,16 @@ __device__ dvec3 box_normal(const DevScene& S, const RtxMaterial& m, int bestInd
 // ------------------------------------------------------------------ primitives, closest hit
 // TrimeshFace::intersectLocal (trimesh.cpp:119-156) up to the barycentric
 // denominators; the barycentrics are computed for the winner only.
-__device__ __forceinline__ bool tri_hit(const RtxFace& F, const dvec3& p, const dvec3& d, double& tOut) {
+// tcap: callers pass a bound past which the hit cannot matter (see
+// traverse); rejecting there only skips work, never changes a result.
+RT_HD bool tri_hit(const RtxFace& F, const dvec3& p, const dvec3& d, double tcap,
+                                        double& tOut) {
   const dvec3 n = ld3(F.n);
   double t = rtm::dot(n, d);
   if (t < RTX_EPS32 && t > -RTX_EPS32) return false;
   const dvec3 v0 = ld3(F.v0), v1 = ld3(F.v1), v2 = ld3(F.v2);
   t = rtm::dot(v0 - p, n) / t;
-  if (t < RTX_EPS32) return false;
+  if (t < RTX_EPS32 || t > tcap) return false;
   const dvec3 P = rtm::ray_at(p, d, t);
   if (rtm::dot(rtm::cross(v1 - v0, P - v0), n) < RTX_EPS32) return false;
   if (rtm::dot(rtm::cross(v2 - v1, P - v1), n) < RTX_EPS32) return false;
@@ -205,7 +281,7 @@ __device__ __forceinline__ bool tri_hit(const RtxFace& F, const dvec3& p, const 
   return true;
 }
 
-__device__ __forceinline__ dvec3 tri_bary(const RtxFace& F, const dvec3& p, const dvec3& d, double t) {
+RT_HD dvec3 tri_bary(const RtxFace& F, const dvec3& p, const dvec3& d, double t) {
   const dvec3 n = ld3(F.n);
   const dvec3 v0 = ld3(F.v0), v1 = ld3(F.v1), v2 = ld3(F.v2);
   const dvec3 P = rtm::ray_at(p, d, t);
@@ -218,7 +294,7 @@ __device__ __forceinline__ dvec3 tri_bary(const RtxFace& F, const dvec3& p, cons
 }
 
 // Lexicographic key order used by both queries.
-__device__ __forceinline__ bool key_less(double ta, int ra, int sa, double tb, int rb, int sb) {
+RT_HD bool key_less(double ta, int ra, int sa, double tb, int rb, int sb) {
   return ta < tb || (ta == tb && (ra < rb || (ra == rb && sa < sb)));
 }
 

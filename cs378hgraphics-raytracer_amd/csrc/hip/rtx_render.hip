@@ -42,9 +42,6 @@ using rtm::mk3;
 #define MAX_DOF 64
 #define QCHUNK 256                 // samples per queue atomic
 
-#define Q_NONE 0
-#define Q_CLOSEST 1
-#define Q_NEXT 2
 
 // ============================================================ frame parameters
 struct FrameParams {
@@ -97,270 +94,7 @@ __device__ __forceinline__ double radinv2(int n) {  // hammersley x (util.cpp:3-
   return result;
 }
 
-// ============================================================ traversal
-// Unified query over the two-level BVH.
-//   Q_CLOSEST: Scene::intersect (scene.cpp:157-180): min over objects of
-//     (t_world, object rank) where each object's t is its own closest hit
-//     (Geometry::intersect + intersectLocal; a trimesh reduces its faces by
-//     (t_local, face rank) first, trimesh.cpp:79-95).
-//   Q_NEXT: the smallest (t_world, object rank, sub) list entry strictly
-//     after (tp, rp, sq) with t_world <= tlimit (Scene::intersectList +
-//     std::sort, light.cpp:25-26).
-// Nodes are skipped only when the exact slab test (bbox.cc:33-70) rejects
-// them or when their entry/exit distance proves that nothing inside can
-// change the answer (margins in DESIGN.md).
-template <bool STATS>
-__device__ __forceinline__ bool traverse(const DevScene& S, const int qmode, const dvec3& P, const dvec3& D,
-                                         const double tp, const int rp, const int sq, const double tlimit,
-                                         double& bt, int& bobj, int& bsub, int* __restrict__ stk, const int lane,
-                                         Counters& C) {
-  const bool closest = qmode == Q_CLOSEST;
-  bt = tlimit;
-  bobj = INT_MAX;
-  bsub = INT_MAX;
-  bool have = false;
-  if (S.n_snodes == 0) return false;
-  const double tlo = closest ? -RTX_INF : tp - S.margin;
-  int sp = 0, node = 0, mode = 0;  // mode: 0 scene node, 1 object, 2 mesh node
-  int oc = 0, oe = 0;
-  // mesh context
-  dvec3 lp = mk3(0, 0, 0), ld = mk3(0, 0, 0);
-  double len = 1.0, mbest = RTX_INF;
-  int moi = 0, mbase = 0, mnoff = 0, mfoff = 0, mface = -1;
-  bool mhave = false;
-  for (;;) {
-    if (mode == 0) {
-      const RtxNode nd = S.snodes[node];
-      if (STATS) C.nodes++;
-      double a, b;
-      bool ok = slab(nd.bmin, nd.bmax, P, D, a, b);
-      if (ok && (a > bt + S.margin || b < tlo)) ok = false;
-      if (ok) {
-        if (nd.count == 0) {
-          stk[sp * 64 + lane] = nd.right;
-          ++sp;
-          node = node + 1;
-        } else {
-          oc = nd.first;
-          oe = nd.first + nd.count;
-          mode = 1;
-        }
-        continue;
-      }
-      if (sp == 0) break;
-      --sp;
-      node = stk[sp * 64 + lane];
-      continue;
-    }
-    if (mode == 1) {
-      const int oi = oc++;
-      const RtxObject& o = S.objs[oi];
-      if (STATS) C.objects++;
-      double a, b;
-      // Geometry::intersect's world-box test (scene.cpp:15) + prune
-      if (slab(o.wmin, o.wmax, P, D, a, b) && !(a > bt + S.margin) && !(b < tlo)) {
-        const dvec3 pos = rtm::xform_point(o.inv, P);
-        dvec3 dir = rtm::xform_point(o.inv, P + D) - pos;
-        const double ln = rtm::length(dir);
-        dir = rtm::normalize(dir);
-        if (o.type == RTX_OBJ_TRIMESH) {
-          const RtxMesh me = S.meshes[o.mesh];
-          if (me.node_count > 0) {
-            lp = pos;
-            ld = dir;
-            len = ln;
-            moi = oi;
-            mbase = sp;
-            mnoff = me.node_off;
-            mfoff = me.face_off;
-            node = me.node_off;
-            mhave = false;
-            mbest = RTX_INF;
-            mface = -1;
-            mode = 2;
-            continue;
-          }
-        } else {
-          // the primitive's intersectLocalList entries, in list order.
-          // Q_CLOSEST keeps the (t, sub)-smallest entry == intersectLocal
-          // (DESIGN.md); Q_NEXT offers every entry to the key filter.
-          double lt = RTX_INF;
-          int ls = -1;
-          auto entry = [&](double t, int sb) {
-            if (closest) {
-              if (ls < 0 || t < lt || (t == lt && sb < ls)) {
-                lt = t;
-                ls = sb;
-              }
-            } else {
-              const double tw = t / ln;
-              if (key_less(tp, rp, sq, tw, oi, sb) && tw <= tlimit && (!have || key_less(tw, oi, sb, bt, bobj, bsub))) {
-                bt = tw;
-                bobj = oi;
-                bsub = sb;
-                have = true;
-              }
-            }
-          };
-          if (o.type == RTX_OBJ_SPHERE) {  // Sphere.cpp:42-72
-            const dvec3 d2 = rtm::normalize(dir);
-            const dvec3 v = -pos;
-            const double bb = rtm::dot(v, d2);
-            double disc = bb * bb - rtm::dot(v, v) + 1;
-            if (!(disc < 0.0)) {
-              disc = sqrt(disc);
-              const double t1 = bb - disc, t2 = bb + disc;
-              if (t1 > RTX_RAY_EPS) entry(t1, 0);
-              if (t2 > RTX_RAY_EPS) entry(t2, 1);
-            }
-          } else if (o.type == RTX_OBJ_BOX) {  // Box.cpp:65-97
-            for (int it = 0; it < 6; it++) {
-              const int mod0 = it % 3;
-              const double dm = rtm::get(dir, mod0);
-              if (dm == 0) continue;
-              const double t = ((it / 3) - 0.5 - rtm::get(pos, mod0)) / dm;
-              if (t < RTX_RAY_EPS) continue;
-              const int mod1 = (it + 1) % 3, mod2 = (it + 2) % 3;
-              const double x = rtm::get(pos, mod1) + t * rtm::get(dir, mod1);
-              const double y = rtm::get(pos, mod2) + t * rtm::get(dir, mod2);
-              if (x <= 0.5 && x >= -0.5 && y <= 0.5 && y >= -0.5) entry(t, it);
-            }
-          } else if (o.type == RTX_OBJ_CYLINDER) {  // Cylinder.cpp:155-263
-            const double pz = pos.z, dz = dir.z;
-            if (!(0.0 == dz)) {
-              double t1, t2;
-              if (dz > 0.0) {
-                t1 = (-pz) / dz;
-                t2 = (1.0 - pz) / dz;
-              } else {
-                t1 = (1.0 - pz) / dz;
-                t2 = (-pz) / dz;
-              }
-              if (t1 >= RTX_RAY_EPS) {
-                const dvec3 q = rtm::ray_at(pos, dir, t1);
-                if ((q.x * q.x + q.y * q.y) <= 1.0) entry(t1, 0);
-              }
-              if (t2 >= RTX_RAY_EPS) {
-                const dvec3 q = rtm::ray_at(pos, dir, t2);
-                if ((q.x * q.x + q.y * q.y) <= 1.0) entry(t2, 1);
-              }
-            }
-            const double x0 = pos.x, y0 = pos.y, x1 = dir.x, y1 = dir.y;
-            const double aa = x1 * x1 + y1 * y1;
-            const double bb = 2.0 * (x0 * x1 + y0 * y1);
-            const double cc = x0 * x0 + y0 * y0 - 1.0;
-            if (!(0.0 == aa)) {
-              double disc = bb * bb - 4.0 * aa * cc;
-              if (!(disc < 0.0)) {
-                disc = sqrt(disc);
-                const double t1 = (-bb - disc) / (2.0 * aa);
-                const double t2 = (-bb + disc) / (2.0 * aa);
-                if (t1 > RTX_RAY_EPS) {
-                  const double z = rtm::ray_at(pos, dir, t1).z;
-                  if (z >= 0.0 && z <= 1.0) entry(t1, 2);
-                }
-                if (t2 > RTX_RAY_EPS) {
-                  const double z = rtm::ray_at(pos, dir, t2).z;
-                  if (z >= 0.0 && z <= 1.0) entry(t2, 3);
-                }
-              }
-            }
-          } else if (o.type == RTX_OBJ_SQUARE) {  // Square.cpp:9-51
-            if (!(dir.z == 0.0)) {
-              const double t = -pos.z / dir.z;
-              if (!(t <= RTX_RAY_EPS)) {
-                const dvec3 Q = rtm::ray_at(pos, dir, t);
-                if (!(Q.x < -0.5 || Q.x > 0.5) && !(Q.y < -0.5 || Q.y > 0.5)) entry(t, 0);
-              }
-            }
-          }
-          if (closest && ls >= 0) {
-            const double tw = lt / ln;
-            if (!have || tw < bt || (tw == bt && oi < bobj)) {
-              bt = tw;
-              bobj = oi;
-              bsub = ls;
-              have = true;
-            }
-          }
-        }
-      }
-      if (oc == oe) {
-        if (sp == 0) break;
-        --sp;
-        node = stk[sp * 64 + lane];
-        mode = 0;
-      }
-      continue;
-    }
-    // mode == 2: mesh node (local frame of object moi)
-    {
-      const RtxNode m = S.mnodes[node];
-      if (STATS) C.nodes++;
-      double a, b;
-      bool ok = slab(m.bmin, m.bmax, lp, ld, a, b);
-      const double whi = (bt + S.margin) * len * (1.0 + 1e-12);
-      double hi = whi;
-      if (closest && mhave) hi = rtm::gmin(hi, mbest + S.lmargin);
-      const double lo = closest ? -RTX_INF : tlo * len * (1.0 - 1e-12) - S.lmargin;
-      if (ok && (a > hi || b < lo)) ok = false;
-      if (ok && m.count == 0) {
-        stk[sp * 64 + lane] = mnoff + m.right;
-        ++sp;
-        node = node + 1;
-        continue;
-      }
-      if (ok) {
-        for (int f = m.first; f < m.first + m.count; ++f) {
-          if (STATS) C.tris++;
-          double tf;
-          if (tri_hit(S.faces[mfoff + f], lp, ld, tf)) {
-            if (closest) {
-              if (!mhave || tf < mbest || (tf == mbest && f < mface)) {
-                mbest = tf;
-                mface = f;
-                mhave = true;
-              }
-            } else {
-              const double tw = tf / len;
-              if (key_less(tp, rp, sq, tw, moi, f) && tw <= tlimit &&
-                  (!have || key_less(tw, moi, f, bt, bobj, bsub))) {
-                bt = tw;
-                bobj = moi;
-                bsub = f;
-                have = true;
-              }
-            }
-          }
-        }
-      }
-      if (sp > mbase) {
-        --sp;
-        node = stk[sp * 64 + lane];
-        continue;
-      }
-      // mesh finished: Trimesh::intersectLocal's result enters Scene::intersect
-      if (closest && mhave) {
-        const double tw = mbest / len;
-        if (!have || tw < bt || (tw == bt && moi < bobj)) {
-          bt = tw;
-          bobj = moi;
-          bsub = mface;
-          have = true;
-        }
-      }
-      if (oc < oe) {
-        mode = 1;
-      } else {
-        if (sp == 0) break;
-        --sp;
-        node = stk[sp * 64 + lane];
-        mode = 0;
-      }
-    }
-  }
-  return have;
-}
+#include "rtx_traverse.h"
 
 // Recompute the winning entry's local quantities (deterministic: same
 // operations as the traversal) and resolve the isect the reference returns:
@@ -389,7 +123,7 @@ __device__ Resolved resolve_hit(const DevScene& S, const dvec3& P, const dvec3& 
     const RtxFace F = S.faces[me.face_off + sub];
     const RtxFaceIds fi = S.fids[me.face_off + sub];
     double tl = 0.0;
-    tri_hit(F, pos, dir, tl);
+    tri_hit(F, pos, dir, RTX_INF, tl);
     const dvec3 bary = tri_bary(F, pos, dir, tl);
     if (me.has_normals) {  // trimesh.cpp:166-172
       const dvec3 n0 = ld3(S.vnormals + size_t(me.vert_off + fi.vi[0]) * 3);
@@ -1420,29 +1154,6 @@ rtx_status upload(SceneState& st, const T* src, size_t n, const T** dst) {
   return RTX_OK;
 }
 
-double scene_extent(const RtxSceneDesc* d) {
-  double e = 1.0;
-  for (int i = 0; i < d->n_objects; ++i)
-    for (int k = 0; k < 3; ++k) {
-      e = std::fmax(e, std::fabs(d->objects[i].wmin[k]));
-      e = std::fmax(e, std::fabs(d->objects[i].wmax[k]));
-    }
-  for (int k = 0; k < 3; ++k) e = std::fmax(e, std::fabs(d->camera.eye[k]));
-  for (int i = 0; i < d->n_lights; ++i)
-    for (int k = 0; k < 3; ++k) e = std::fmax(e, std::fabs(d->lights[i].pos[k]));
-  return e;
-}
-
-double mesh_extent(const RtxSceneDesc* d) {
-  double e = 1.0;
-  for (int i = 0; i < d->n_mesh_nodes; ++i)
-    for (int k = 0; k < 3; ++k) {
-      e = std::fmax(e, std::fabs(d->mesh_nodes[i].bmin[k]));
-      e = std::fmax(e, std::fabs(d->mesh_nodes[i].bmax[k]));
-    }
-  return e;
-}
-
 // Area-light sample positions (AreaLightRect::pick / AreaLightCirc::pick,
 // light.cpp:106-131): host glibc cos/sin, exactly as the CPU restatement.
 std::vector<double> make_picks(const std::vector<RtxLight>& lights, int res) {
@@ -1548,6 +1259,29 @@ rtx_status rtx_scene_create(int device, const RtxSceneDesc* d, void** out) {
   UP(d->textures, d->n_textures, S.texs);
   UP(d->texels, d->n_texels, S.texels);
 #undef UP
+  {
+    std::vector<DevNode2> sn2, mn2;
+    std::vector<DevRoot> mroots(size_t(d->n_meshes));
+    bool ok = true;
+    std::memset(&S.sroot, 0, sizeof(S.sroot));
+    if (d->n_scene_nodes > 0) ok = build_node2(d->scene_nodes, d->n_scene_nodes, sn2, S.sroot);
+    for (int m = 0; ok && m < d->n_meshes; ++m) {
+      const RtxMesh& me = d->meshes[m];
+      std::memset(&mroots[size_t(m)], 0, sizeof(DevRoot));
+      if (me.node_count > 0) ok = build_node2(d->mesh_nodes + me.node_off, me.node_count, mn2, mroots[size_t(m)]);
+    }
+    if (!ok) {
+      g_err = "rtx_scene_create: malformed BVH (leaf with more than 3 items or bad child link)";
+      rtx_scene_destroy(st);
+      return RTX_ERR_INVALID;
+    }
+#define UP(src, n, dst) \
+  if ((rc = upload(*st, src, size_t(n), &dst)) != RTX_OK) { rtx_scene_destroy(st); return rc; }
+    UP(sn2.data(), sn2.size(), S.snode2);
+    UP(mn2.data(), mn2.size(), S.mnode2);
+    UP(mroots.data(), mroots.size(), S.mroots);
+#undef UP
+  }
   S.n_snodes = d->n_scene_nodes;
   S.n_objs = d->n_objects;
   S.n_lights = d->n_lights;

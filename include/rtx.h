@@ -69,7 +69,7 @@ typedef struct RtxObject {
   int32_t mesh;             /* index into meshes (trimesh) or -1              */
   int32_t orig_id;          /* index in Scene::objects (parse order)          */
   int32_t leaf;             /* scene-BVH leaf node holding this object        */
-  int32_t pad[3];
+  int32_t pad[5];           /* to 256 bytes: two whole 128-byte lines         */
 } RtxObject;                /* 256 bytes */
 
 /* Material parameter: constant vec3 or texture (MaterialParameter,

@@ -1305,4 +1305,41 @@ int oracle_probe(const char* ray_path, const double p[3], const double d[3], dou
   }
 }
 
+/* Batched queries for the traversal unit test (tests/test_traverse_host.py).
+ * mode 0: Scene::intersect (scene.cpp:157-180) -> 1 entry per ray;
+ * mode 1: Scene::intersectList + std::sort on t, the list srsAttenuation
+ *         walks (light.cpp:25-26) -> up to kmax entries per ray. */
+int oracle_query_batch(const char* ray_path, int32_t n, const double* P, const double* D, int32_t mode,
+                       int32_t kmax, double* t, int32_t* object, int32_t* face, int32_t* nhits) {
+  try {
+    std::unique_ptr<orc::Scene> S = orc::build_scene(ray_path);
+    orc::tl_scene = S.get();
+    for (int32_t k = 0; k < n; ++k) {
+      orc::Ray r(mk3(P[3 * k], P[3 * k + 1], P[3 * k + 2]), mk3(D[3 * k], D[3 * k + 1], D[3 * k + 2]));
+      if (mode == 0) {
+        orc::Isect i;
+        const bool hit = S->intersect(r, i);
+        t[k] = i.t;
+        object[k] = hit ? i.obj->orig_id : -1;
+        face[k] = hit ? i.face : -1;
+        nhits[k] = hit ? 1 : 0;
+      } else {
+        std::vector<orc::Isect> iv = S->intersectList(r);
+        std::sort(iv.begin(), iv.end(), [](const orc::Isect& a, const orc::Isect& b) { return a.t < b.t; });
+        nhits[k] = static_cast<int32_t>(iv.size());
+        for (int32_t j = 0; j < kmax; ++j) {
+          const bool ok = j < static_cast<int32_t>(iv.size());
+          t[size_t(k) * kmax + j] = ok ? iv[size_t(j)].t : 0.0;
+          object[size_t(k) * kmax + j] = ok ? iv[size_t(j)].obj->orig_id : -1;
+          face[size_t(k) * kmax + j] = ok ? iv[size_t(j)].face : -1;
+        }
+      }
+    }
+    return 0;
+  } catch (const std::exception& e) {
+    orc::g_err = e.what();
+    return -1;
+  }
+}
+
 }  // extern "C"

@@ -44,6 +44,11 @@ int oracle_bvh_hash(const char* ray_path, uint64_t* scene_hash, uint64_t* mesh_h
 int oracle_probe(const char* ray_path, const double p[3], const double d[3], double* t, double n[3],
                  int32_t* object, int32_t* face);
 
+/* Batched closest-hit (mode 0) or sorted all-hits (mode 1, kmax per ray)
+ * queries for the traversal unit test. */
+int oracle_query_batch(const char* ray_path, int32_t n, const double* P, const double* D, int32_t mode,
+                       int32_t kmax, double* t, int32_t* object, int32_t* face, int32_t* nhits);
+
 #ifdef __cplusplus
 }
 #endif

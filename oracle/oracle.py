@@ -45,8 +45,31 @@ def lib(pkg):
         L.oracle_probe.argtypes = [C.c_char_p, C.POINTER(C.c_double), C.POINTER(C.c_double),
                                    C.POINTER(C.c_double), C.POINTER(C.c_double), C.POINTER(C.c_int32),
                                    C.POINTER(C.c_int32)]
+        L.oracle_query_batch.argtypes = [C.c_char_p, C.c_int32, C.c_void_p, C.c_void_p, C.c_int32, C.c_int32,
+                                         C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]
         _lib = L
     return _lib
+
+
+def query_batch(pkg, path: str, P, D, mode: int, kmax: int = 1):
+    """Scene::intersect (mode 0) or sorted intersectList (mode 1) for rays
+    (P[k], D[k]).  Returns (t, object, face, nhits) arrays."""
+    import numpy as np
+
+    L = lib(pkg)
+    P = np.ascontiguousarray(P, np.float64)
+    D = np.ascontiguousarray(D, np.float64)
+    n = P.shape[0]
+    k = 1 if mode == 0 else kmax
+    t = np.zeros((n, k), np.float64)
+    o = np.zeros((n, k), np.int32)
+    f = np.zeros((n, k), np.int32)
+    nh = np.zeros(n, np.int32)
+    rc = L.oracle_query_batch(path.encode(), n, P.ctypes.data, D.ctypes.data, mode, k, t.ctypes.data, o.ctypes.data,
+                              f.ctypes.data, nh.ctypes.data)
+    if rc != 0:
+        raise RuntimeError(L.oracle_last_error().decode())
+    return t, o, f, nh
 
 
 def render(pkg, path: str, opts, rect=None, threads: int = 0, want_hits: bool = True):

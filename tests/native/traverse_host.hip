@@ -1,0 +1,109 @@
+// traverse_host.hip — TEST HARNESS: the device traversal (rtx_traverse.h,
+// the code every render kernel runs) compiled for the HOST so the unit test
+// tests/test_traverse_host.py can compare it query by query with the CPU
+// restatement's Scene::intersect / sorted intersectList on thousands of rays
+// without a GPU.  Built with --offload-host-only; never shipped, never used
+// by the product.
+#include <cstdint>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../cs378hgraphics-raytracer_amd/csrc/hip/rtx_traverse.h"
+
+using namespace rtxd;
+
+namespace {
+std::string g_err;
+
+struct HostScene {
+  DevScene S;
+  std::vector<DevNode2> sn2, mn2;
+  std::vector<DevRoot> mroots;
+  int stack_cap = 0;
+};
+
+bool make_scene(const RtxSceneDesc* d, HostScene& H) {
+  std::memset(&H.S, 0, sizeof(H.S));
+  DevScene& S = H.S;
+  if (d->n_scene_nodes > 0 && !build_node2(d->scene_nodes, d->n_scene_nodes, H.sn2, S.sroot)) return false;
+  H.mroots.resize(size_t(d->n_meshes));
+  for (int m = 0; m < d->n_meshes; ++m) {
+    const RtxMesh& me = d->meshes[m];
+    std::memset(&H.mroots[size_t(m)], 0, sizeof(DevRoot));
+    if (me.node_count > 0 && !build_node2(d->mesh_nodes + me.node_off, me.node_count, H.mn2, H.mroots[size_t(m)]))
+      return false;
+  }
+  S.snode2 = H.sn2.data();
+  S.mnode2 = H.mn2.data();
+  S.mroots = H.mroots.data();
+  S.snodes = d->scene_nodes;
+  S.objs = d->objects;
+  S.mats = d->materials;
+  S.meshes = d->meshes;
+  S.mnodes = d->mesh_nodes;
+  S.faces = d->faces;
+  S.fids = d->face_ids;
+  S.n_snodes = d->n_scene_nodes;
+  S.n_objs = d->n_objects;
+  S.margin = 1e-9 * scene_extent(d);
+  S.lmargin = 1e-9 * mesh_extent(d);
+  H.stack_cap = d->scene_depth + d->mesh_depth + 4;
+  return true;
+}
+}  // namespace
+
+extern "C" {
+
+const char* trav_host_last_error(void) { return g_err.c_str(); }
+
+// qmode 1: closest hit per ray -> t/object/face (orig ids), 1 entry.
+// qmode 2: the shadow walk's successive next-hit queries, up to kmax entries
+//          per ray, each query bounded by tlimit[k] (1e308 = unbounded).
+// counters[3] += node box tests, object tests, triangle tests.
+int trav_host_run(const RtxSceneDesc* d, int32_t qmode, int32_t n, const double* P, const double* D,
+                  const double* tlimit, int32_t kmax, double* t, int32_t* object, int32_t* face, int32_t* nhits,
+                  int64_t* counters) {
+  HostScene H;
+  if (!make_scene(d, H)) {
+    g_err = "malformed BVH";
+    return -1;
+  }
+  std::vector<int> stk(size_t(H.stack_cap + 4) * 64, 0);
+  Counters C = {0, 0, 0, 0, 0, 0, 0};
+  for (int32_t k = 0; k < n; ++k) {
+    const dvec3 p = mk3(P[3 * k], P[3 * k + 1], P[3 * k + 2]);
+    const dvec3 dd = mk3(D[3 * k], D[3 * k + 1], D[3 * k + 2]);
+    double tp = -RTX_INF;
+    int rp = -1, sq = -1, cnt = 0;
+    const int kk = qmode == Q_CLOSEST ? 1 : kmax;
+    for (int j = 0; j < kk; ++j) {
+      t[size_t(k) * kk + j] = 0.0;
+      object[size_t(k) * kk + j] = -1;
+      face[size_t(k) * kk + j] = -1;
+    }
+    for (int j = 0; j < kk; ++j) {
+      double bt;
+      int bobj, bsub;
+      const bool have = traverse<true>(H.S, qmode, p, dd, tp, rp, sq, qmode == Q_CLOSEST ? RTX_INF : tlimit[k], bt,
+                                       bobj, bsub, stk.data(), 0, C);
+      if (!have) break;
+      const RtxObject& o = d->objects[bobj];
+      t[size_t(k) * kk + j] = bt;
+      object[size_t(k) * kk + j] = o.orig_id;
+      face[size_t(k) * kk + j] =
+          o.type == RTX_OBJ_TRIMESH ? d->face_ids[d->meshes[o.mesh].face_off + bsub].orig_id : -1;
+      ++cnt;
+      tp = bt;
+      rp = bobj;
+      sq = bsub;
+    }
+    nhits[k] = cnt;
+  }
+  counters[0] += C.nodes;
+  counters[1] += C.objects;
+  counters[2] += C.tris;
+  return 0;
+}
+
+}  // extern "C"

@@ -1,0 +1,125 @@
+"""The device traversal (csrc/hip/rtx_traverse.h — what every render kernel
+runs) compiled for the host and compared query by query with the CPU
+restatement: closest hit (Scene::intersect, scene.cpp:157-180) and the shadow
+walk's successive next-hit queries against intersectList + std::sort
+(light.cpp:25-26).  Object / face ids and t must be bit-exact.
+
+Rays: camera rays through random pixels, rays from random interior points in
+random directions, and axis-aligned rays (exercise the d[a] == 0 slab skip,
+bbox.cc:48-49).  No GPU needed; the harness is test-only
+(tests/native/traverse_host.hip)."""
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+from conftest import ROOT, scene_path
+
+NATIVE = os.path.join(ROOT, "tests", "native", "traverse_host.hip")
+LIB = os.path.join(ROOT, "tests", "_build", "libtraverse_host.so")
+SRC = os.path.join(ROOT, "cs378hgraphics-raytracer_amd", "csrc")
+HDRS = [os.path.join(SRC, "hip", "rtx_traverse.h"), os.path.join(SRC, "hip", "rtx_device.h"),
+        os.path.join(SRC, "common", "rt_math.h"), os.path.join(ROOT, "include", "rtx.h")]
+
+
+def _harness(pkg):
+    deps = [NATIVE] + HDRS
+    if not os.path.exists(LIB) or os.path.getmtime(LIB) < max(os.path.getmtime(d) for d in deps):
+        os.makedirs(os.path.dirname(LIB), exist_ok=True)
+        subprocess.run(["/opt/rocm/bin/hipcc", "-O2", "-std=c++17", "-fPIC", "--offload-host-only",
+                        "-ffp-contract=off", "-fno-fast-math", "-I" + os.path.join(ROOT, "include"), "-shared",
+                        "-o", LIB, NATIVE], check=True)
+    L = C.CDLL(LIB)
+    L.trav_host_run.argtypes = [C.POINTER(pkg.RtxSceneDesc), C.c_int32, C.c_int32, C.c_void_p, C.c_void_p,
+                                C.c_void_p, C.c_int32, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]
+    L.trav_host_last_error.restype = C.c_char_p
+    return L
+
+
+def _run(L, pkg, host, qmode, P, D, tlim, kmax):
+    n = P.shape[0]
+    k = 1 if qmode == 1 else kmax
+    t = np.zeros((n, k), np.float64)
+    o = np.zeros((n, k), np.int32)
+    f = np.zeros((n, k), np.int32)
+    nh = np.zeros(n, np.int32)
+    cnt = np.zeros(3, np.int64)
+    P = np.ascontiguousarray(P)
+    D = np.ascontiguousarray(D)
+    tl = np.ascontiguousarray(tlim, np.float64)
+    rc = L.trav_host_run(C.byref(host.desc), qmode, n, P.ctypes.data, D.ctypes.data, tl.ctypes.data, k,
+                         t.ctypes.data, o.ctypes.data, f.ctypes.data, nh.ctypes.data, cnt.ctypes.data)
+    assert rc == 0, L.trav_host_last_error()
+    return t, o, f, nh, cnt
+
+
+def _rays(host, n, seed):
+    rng = np.random.default_rng(seed)
+    cam = host.desc.camera
+    eye, look, u, v = (np.array(x[:]) for x in (cam.eye, cam.look, cam.u, cam.v))
+    no = host.desc.n_objects  # RtxObject: 256 B (32 doubles), world box = first 6
+    rec = np.frombuffer((C.c_double * (32 * no)).from_address(host.desc.objects), np.float64).reshape(no, 32)
+    lo = rec[:, 0:3].min(axis=0)
+    hi = rec[:, 3:6].max(axis=0)
+    k = n // 3
+    # camera rays (Camera::rayThrough, camera.cpp:21-31)
+    xy = rng.random((k, 2))
+    d = look[None] + (xy[:, :1] - 0.5) * u[None] + (xy[:, 1:] - 0.5) * v[None]
+    d /= np.linalg.norm(d, axis=1, keepdims=True)
+    P = [np.repeat(eye[None], k, 0)]
+    D = [d]
+    # random interior origins, random directions
+    p = lo + (hi - lo) * rng.random((k, 3))
+    d = rng.normal(size=(k, 3))
+    d /= np.linalg.norm(d, axis=1, keepdims=True)
+    P.append(p)
+    D.append(d)
+    # axis-aligned directions
+    m = n - 2 * k
+    p = lo + (hi - lo) * rng.random((m, 3))
+    d = np.zeros((m, 3))
+    ax = rng.integers(0, 3, m)
+    d[np.arange(m), ax] = rng.choice([-1.0, 1.0], m)
+    P.append(p)
+    D.append(d)
+    return np.concatenate(P), np.concatenate(D)
+
+
+SCENES = [("hitchcock.ray", 3000), ("spheres_overlap.ray", 1500), ("box_cyl_opaque_shadow_spotlight.ray", 1500),
+          ("distance.ray", 1500), ("trimesh2_square.ray", 1500), ("trimesh2.ray", 900)]
+
+
+@pytest.mark.parametrize("scene,n", SCENES, ids=[s[0] for s in SCENES])
+def test_closest_hit_matches_restatement(pkg, orc, scene, n):
+    L = _harness(pkg)
+    path = scene_path(scene)
+    host = pkg.HostScene(path)
+    P, D = _rays(host, n, 7)
+    t, o, f, nh, cnt = _run(L, pkg, host, 1, P, D, np.full(n, 1e308), 1)
+    rt, ro, rf, rnh = orc.query_batch(pkg, path, P, D, 0)
+    hit = rnh > 0
+    assert np.array_equal(nh > 0, hit)
+    assert np.array_equal(o[:, 0], ro[:, 0])
+    assert np.array_equal(f[:, 0], rf[:, 0])
+    assert np.array_equal(t[hit, 0], rt[hit, 0]), "closest t not bit-exact"
+    assert hit.mean() > 0.05  # the ray set actually hits things
+
+
+@pytest.mark.parametrize("scene,n", SCENES[:4] + [("trimesh2_square.ray", 600)],
+                         ids=[s[0] for s in SCENES[:4]] + ["trimesh2_square.ray"])
+def test_next_hit_walk_matches_sorted_list(pkg, orc, scene, n):
+    L = _harness(pkg)
+    path = scene_path(scene)
+    host = pkg.HostScene(path)
+    P, D = _rays(host, n, 11)
+    kmax = 16
+    t, o, f, nh, _ = _run(L, pkg, host, 2, P, D, np.full(n, 1e308), kmax)
+    rt, ro, rf, rnh = orc.query_batch(pkg, path, P, D, 1, kmax)
+    ok = rnh <= kmax  # longer lists: std::sort leaves insertion-sort territory
+    assert np.array_equal(nh[ok], rnh[ok])
+    assert np.array_equal(o[ok], ro[ok])
+    assert np.array_equal(f[ok], rf[ok])
+    assert np.array_equal(t[ok], rt[ok])
+    assert (rnh[ok] > 1).mean() > 0.05
