@@ -11,8 +11,8 @@ over xGMI (dist.gather) — total work is fixed, so scaling is strong.
 value = rays of the whole frame (camera + reflection/refraction + shadow
 queries) / frame wall time, taken as the max over ranks between
 barrier+synchronize brackets.  roofline.achieved = algorithmic bytes of one
-render-kernel launch / its HIP-event duration (rtx_kernel_time on the render
-stream).  cpu_baseline = the CPU restatement (oracle/, "port") timed on this
+frame / the frame's GPU time (HIP events on the render stream bracketing all
+of the frame's kernels, rtx_kernel_time).  cpu_baseline = the CPU restatement (oracle/, "port") timed on this
 host's cores over row bands of the same frame.
 """
 import argparse
@@ -173,12 +173,15 @@ def main():
     value = frame_rays * args.steps / elapsed / 1e6
 
     if rank == 0:
-        # one launch of the render megakernel renders the whole frame; the
-        # wavefront path (RTX_WAVEFRONT=1) splits a frame into many launches,
-        # so the figure is priced per frame: algorithmic bytes of one frame /
-        # the HIP-event kernel time of one frame (both identical for the
-        # megakernel, where launches == frames)
+        # the default wavefront path renders a frame as ~80 iterations of
+        # advance_kernel + trace_kernel<closest> + trace_kernel<next> on 3
+        # streams; rtx_kernel_time returns one HIP-event pair per frame
+        # spanning all of them (recorded on the render stream before the
+        # fork and after the join), so the roofline is priced per frame:
+        # algorithmic bytes of one frame / GPU time of one frame.  With
+        # RTX_MEGAKERNEL=1 the frame is one render_kernel launch.
         launches_per_frame = nlaunch / max(1, args.steps)
+        mega = os.environ.get("RTX_MEGAKERNEL", "0") not in ("", "0")
         avg_kernel_ms = kms / max(1, args.steps)
         algo_bytes = (B_RAY * st["rays"] + B_NODE * st["node_visits"] + B_OBJ * st["object_tests"] +
                       B_TRI * st["tri_tests"] + B_SHADE * st["shades"])
@@ -205,8 +208,8 @@ def main():
                        "parallelism": f"tile-shard x{world} + RCCL gather" if world > 1 else "single GPU"},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                         "kernel": ("render_kernel<false,false>" if launches_per_frame <= 1.0 else
-                                    "advance_kernel+trace_kernel (wavefront)"),
+                         "kernel": ("render_kernel<false,false> (megakernel, 1 launch per frame)" if mega else
+                                    "frame span: advance_kernel + trace_kernel<false,1|2> iterations on 3 streams"),
                          "avg_kernel_ms": round(avg_kernel_ms, 3), "launches_per_frame": launches_per_frame,
                          "algorithmic_bytes_per_launch": algo_bytes},
             "cpu_baseline": cpu,

@@ -128,7 +128,9 @@ def hip_lib():
     """librtx_hip.so (gfx950 kernels).  Raises if it is not built."""
     global _hip
     if _hip is None:
-        path = os.path.join(LIB_DIR, "librtx_hip.so")
+        # RTX_HIP_LIB: an alternative in-tree build of the same library
+        # (tuning experiments, tools/build_variants.sh)
+        path = os.environ.get("RTX_HIP_LIB") or os.path.join(LIB_DIR, "librtx_hip.so")
         if not os.path.exists(path):
             raise RtxError(f"{path} not built (run __graft_entry__.build()); there is no CPU fallback")
         lib = C.CDLL(path)

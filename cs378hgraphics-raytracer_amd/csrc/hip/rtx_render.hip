@@ -41,6 +41,16 @@ using rtm::mk3;
 #define MAX_PENDING (MAX_DEPTH + 2)
 #define MAX_DOF 64
 #define QCHUNK 256                 // samples per queue atomic
+// occupancy targets (waves per SIMD) of the wavefront kernels, measured on
+// the headline frame: traversal at 3 waves (<= 168 VGPRs, no spills) beats 4
+// (128 VGPRs + scratch spills) and 2; the state-machine kernel is left
+// unconstrained
+#ifndef RTX_TRACE_WAVES
+#define RTX_TRACE_WAVES 3
+#endif
+#ifndef RTX_ADV_WAVES
+#define RTX_ADV_WAVES 1
+#endif
 
 
 // ============================================================ frame parameters
@@ -205,20 +215,93 @@ struct Pending {
 };
 
 // Per-lane state of one sample's path (everything the state machine keeps
-// between traversal queries).  Registers in the adaptive megakernel, SoA in
-// HBM (SlotArrays) in the wavefront path.
-struct LaneState {
-  int st, sample_slot, rec_on, pass, camk, nrays, top, rdepth, rkind, first_query, sobj, ssub, m_flags, li, pick,
-      qmode, qrp, qsq, bobj, bsub, bhave, kdone;
-  double sx, sy, st_t, m_sh, dattn, last_t, qtp, bt;
-  dvec3 acc, rp, rd, W, N, i_out, dscomp, m_kd, m_ks, area_sum, sdir, wpos, sattn;
-};
-
+// between traversal queries, plus the last query's result).  It lives in HBM
+// (L2 / Infinity-Cache resident), one array per field indexed by lane, so a
+// wave's access to a field is one contiguous 64-lane line set, and no kernel
+// has to hold the whole state in VGPRs: the state machine touches only the
+// fields of its current step, and the traversal's registers are not shared
+// with it.  LaneRef binds a lane's fields by reference, so the state machine
+// reads like plain per-lane code.
 #define LANE_INT_FIELDS(X) X(st) X(sample_slot) X(rec_on) X(pass) X(camk) X(nrays) X(top) X(rdepth) X(rkind) \
-  X(first_query) X(sobj) X(ssub) X(m_flags) X(li) X(pick) X(qmode) X(qrp) X(qsq) X(kdone)
-#define LANE_DBL_FIELDS(X) X(sx) X(sy) X(st_t) X(m_sh) X(dattn) X(last_t) X(qtp)
+  X(first_query) X(sobj) X(ssub) X(m_flags) X(li) X(pick) X(qmode) X(qrp) X(qsq) X(kdone) X(bobj) X(bsub) X(bhave)
+#define LANE_DBL_FIELDS(X) X(sx) X(sy) X(st_t) X(m_sh) X(dattn) X(last_t) X(qtp) X(bt)
 #define LANE_VEC_FIELDS(X) X(acc) X(rp) X(rd) X(W) X(N) X(i_out) X(dscomp) X(m_kd) X(m_ks) X(area_sum) X(sdir) \
   X(wpos) X(sattn)
+
+enum {
+#define E_(f) LI_##f,
+  LANE_INT_FIELDS(E_)
+#undef E_
+  LI_COUNT
+};
+enum {
+#define E_(f) LD_##f,
+  LANE_DBL_FIELDS(E_)
+#undef E_
+  LD_COUNT
+};
+enum {
+#define E_(f) LV_##f,
+  LANE_VEC_FIELDS(E_)
+#undef E_
+  LV_COUNT
+};
+
+struct LaneMem {
+  int* i;     // [LI_COUNT][n]
+  double* d;  // [LD_COUNT][n]
+  dvec3* v;   // [LV_COUNT][n]
+  size_t n;   // lanes
+};
+
+__host__ __device__ inline size_t lane_mem_bytes(size_t n) {
+  return n * (LI_COUNT * sizeof(int) + LD_COUNT * sizeof(double) + LV_COUNT * sizeof(dvec3)) + 512;
+}
+
+// carve a LaneMem out of one allocation (256-byte aligned pieces)
+inline LaneMem lane_mem_at(void* base, size_t n) {
+  auto al = [](size_t x) { return (x + 255) & ~size_t(255); };
+  char* p = static_cast<char*>(base);
+  LaneMem m;
+  m.n = n;
+  m.d = reinterpret_cast<double*>(p);
+  p += al(n * LD_COUNT * sizeof(double));
+  m.v = reinterpret_cast<dvec3*>(p);
+  p += al(n * LV_COUNT * sizeof(dvec3));
+  m.i = reinterpret_cast<int*>(p);
+  return m;
+}
+
+struct LaneRef {
+#define M_I(f) int& f;
+#define M_D(f) double& f;
+#define M_V(f) dvec3& f;
+  LANE_INT_FIELDS(M_I)
+  LANE_DBL_FIELDS(M_D)
+  LANE_VEC_FIELDS(M_V)
+#undef M_I
+#undef M_D
+#undef M_V
+  int dummy_;
+  __device__ __forceinline__ LaneRef(const LaneMem& m, size_t g)
+      :
+#define I_I(f) f(m.i[size_t(LI_##f) * m.n + g]),
+#define I_D(f) f(m.d[size_t(LD_##f) * m.n + g]),
+#define I_V(f) f(m.v[size_t(LV_##f) * m.n + g]),
+        LANE_INT_FIELDS(I_I) LANE_DBL_FIELDS(I_D) LANE_VEC_FIELDS(I_V)
+#undef I_I
+#undef I_D
+#undef I_V
+        dummy_(0) {
+  }
+};
+
+// zero one lane's state (kernel start)
+__device__ __forceinline__ void lane_clear(const LaneMem& m, size_t g) {
+  for (int k = 0; k < LI_COUNT; ++k) m.i[size_t(k) * m.n + g] = 0;
+  for (int k = 0; k < LD_COUNT; ++k) m.d[size_t(k) * m.n + g] = 0.0;
+  for (int k = 0; k < LV_COUNT; ++k) m.v[size_t(k) * m.n + g] = mk3(0.0, 0.0, 0.0);
+}
 
 // Run one lane's state machine (trace / traceRay / shade / srsAttenuation,
 // RayTracer.cpp:35-174, material.cpp:34-69, light.cpp:16-53) until it needs
@@ -226,7 +309,7 @@ struct LaneState {
 // The pending-ray stack lives in HBM: entry e, field f at
 // pbuf[(e * 13 + f) * nlanes + glane].
 template <bool STATS, bool ADAPTIVE>
-__device__ __forceinline__ void advance_lane(LaneState& L, const DevScene& S, const FrameParams& F, Counters& C,
+__device__ __forceinline__ void advance_lane(LaneRef& L, const DevScene& S, const FrameParams& F, Counters& C,
                                              double* __restrict__ sbuf, double* __restrict__ colbuf,
                                              RtxHitRecord* __restrict__ hits, int64_t apix_out, int an,
                                              double* __restrict__ pbuf, size_t nlanes, size_t glane, int pend_cap) {
@@ -234,7 +317,6 @@ __device__ __forceinline__ void advance_lane(LaneState& L, const DevScene& S, co
   LANE_INT_FIELDS(REF)
   LANE_DBL_FIELDS(REF)
   LANE_VEC_FIELDS(REF)
-  REF(bt) REF(bobj) REF(bsub) REF(bhave)
 #undef REF
   const RtxRenderParams& P = F.P;
   const double aterm = P.aterm_thresh;
@@ -554,7 +636,7 @@ __global__ void __launch_bounds__(WG) render_kernel(DevScene S, const FrameParam
                                                      double* __restrict__ sbuf, RtxHitRecord* __restrict__ hits,
                                                      uint8_t* __restrict__ rgb8, double* __restrict__ rgbf,
                                                      unsigned long long* __restrict__ stats, int stack_cap,
-                                                     double* __restrict__ pbuf, int pend_cap) {
+                                                     double* __restrict__ pbuf, int pend_cap, LaneMem lm) {
   extern __shared__ double smem[];
   const FrameParams& F = *Fp;
   const int lane = threadIdx.x & 63;
@@ -574,14 +656,13 @@ __global__ void __launch_bounds__(WG) render_kernel(DevScene S, const FrameParam
   const double aterm = P.aterm_thresh;
   const int ncam = P.dof ? P.dof_div + 1 : 1;
 
-  // ---- lane state
-  LaneState L;
-  memset(&L, 0, sizeof(L));
+  // ---- lane state (HBM, see LaneRef)
+  lane_clear(lm, glane);
+  LaneRef L(lm, glane);
 #define REF(f) auto& f = L.f;
   LANE_INT_FIELDS(REF)
   LANE_DBL_FIELDS(REF)
   LANE_VEC_FIELDS(REF)
-  REF(bt) REF(bobj) REF(bsub) REF(bhave)
 #undef REF
   st = ST_IDLE;
   sample_slot = -1;
@@ -837,63 +918,21 @@ __global__ void __launch_bounds__(WG) render_kernel(DevScene S, const FrameParam
 }
 
 // ============================================================ wavefront path
-// Path slots: NSLOT lanes' LaneState kept SoA in HBM.  Each iteration:
-//   advance_kernel  — one thread per slot: load state (+ last query result),
-//                     run the state machine to the next query, append the
-//                     query to the closest-hit or next-hit list (wave ballot
-//                     + popc + one atomic per wave, mbcnt for the offset:
-//                     compaction of the active-ray mask), store state;
-//   trace_kernel<Q> — one thread per compacted query: traverse, write result.
+// Path slots: NSLOT lanes whose LaneRef state lives in HBM.  Each iteration:
+//   advance_kernel  — one thread per slot: take the last query's result, run
+//                     the state machine to the next ray query, append it to
+//                     the closest-hit or next-hit list (wave ballot + popc +
+//                     one atomic per wave, mbcnt for the offset: compaction
+//                     of the active-ray mask);
+//   trace_kernel<Q> — one thread per compacted query: traverse, write the
+//                     result into the slot's state.
 // Samples are dealt to slots statically (sample slot + k * NSLOT).
-struct SlotArrays {
-  int* iv;      // LANE_INT_FIELDS, field-major [field][slot]
-  double* dv;   // LANE_DBL_FIELDS then LANE_VEC_FIELDS (x, y, z), field-major
-  double* res_t;
-  int* res_i;   // [0]: obj, [1]: sub, [2]: have  (field-major)
-};
-
 struct QList {
   int* slot;    // [cap]
   double* d;    // Px Py Pz Dx Dy Dz tp tlimit, field-major [8][cap]
   int* iv;      // rp, sq  [2][cap]
+  size_t cap;
 };
-
-#define N_INT_FIELDS 19
-#define N_DBL_FIELDS (7 + 13 * 3)
-
-__device__ __forceinline__ void load_lane(LaneState& L, const SlotArrays& A, int slot, int nslot) {
-  int fi = 0;
-#define LI(f) L.f = A.iv[static_cast<size_t>(fi++) * nslot + slot];
-  LANE_INT_FIELDS(LI)
-#undef LI
-  int fd = 0;
-#define LD(f) L.f = A.dv[static_cast<size_t>(fd++) * nslot + slot];
-  LANE_DBL_FIELDS(LD)
-#undef LD
-#define LV(f)                                               \
-  L.f.x = A.dv[static_cast<size_t>(fd++) * nslot + slot]; \
-  L.f.y = A.dv[static_cast<size_t>(fd++) * nslot + slot]; \
-  L.f.z = A.dv[static_cast<size_t>(fd++) * nslot + slot];
-  LANE_VEC_FIELDS(LV)
-#undef LV
-}
-
-__device__ __forceinline__ void store_lane(const LaneState& L, const SlotArrays& A, int slot, int nslot) {
-  int fi = 0;
-#define SI(f) A.iv[static_cast<size_t>(fi++) * nslot + slot] = L.f;
-  LANE_INT_FIELDS(SI)
-#undef SI
-  int fd = 0;
-#define SD(f) A.dv[static_cast<size_t>(fd++) * nslot + slot] = L.f;
-  LANE_DBL_FIELDS(SD)
-#undef SD
-#define SV(f)                                               \
-  A.dv[static_cast<size_t>(fd++) * nslot + slot] = L.f.x; \
-  A.dv[static_cast<size_t>(fd++) * nslot + slot] = L.f.y; \
-  A.dv[static_cast<size_t>(fd++) * nslot + slot] = L.f.z;
-  LANE_VEC_FIELDS(SV)
-#undef SV
-}
 
 __device__ __forceinline__ unsigned int lane_prefix(unsigned long long mask) {
   return __builtin_amdgcn_mbcnt_hi(static_cast<unsigned int>(mask >> 32),
@@ -902,7 +941,7 @@ __device__ __forceinline__ unsigned int lane_prefix(unsigned long long mask) {
 
 // Claim the next statically dealt sample for an idle slot (what the
 // scheduler of the megakernel does with its queue).
-__device__ __forceinline__ void claim_sample(LaneState& L, const FrameParams& F, RtxHitRecord* hits, int slot,
+__device__ __forceinline__ void claim_sample(LaneRef& L, const FrameParams& F, RtxHitRecord* hits, int slot,
                                              int nslot) {
   const RtxRenderParams& P = F.P;
   while (L.st == ST_IDLE) {
@@ -936,55 +975,41 @@ __device__ __forceinline__ void claim_sample(LaneState& L, const FrameParams& F,
 }
 
 template <bool STATS>
-__global__ void __launch_bounds__(WG) advance_kernel(DevScene S, const FrameParams* __restrict__ Fp, SlotArrays A,
-                                                      int nslot, double* __restrict__ sbuf,
-                                                      RtxHitRecord* __restrict__ hits, double* __restrict__ pbuf,
-                                                      int pend_cap, QList q0, QList q1,
+__global__ void __launch_bounds__(WG, RTX_ADV_WAVES) advance_kernel(DevScene S, const FrameParams* __restrict__ Fp, LaneMem lm,
+                                                      double* __restrict__ sbuf, RtxHitRecord* __restrict__ hits,
+                                                      double* __restrict__ pbuf, int pend_cap, QList q0, QList q1,
                                                       unsigned int* __restrict__ counters,
-                                                      unsigned long long* __restrict__ stats) {
+                                                      unsigned long long* __restrict__ stats, int slot_off) {
   const FrameParams& F = *Fp;
-  const int slot = blockIdx.x * WG + threadIdx.x;
-  const bool valid = slot < nslot;
+  const int nslot = static_cast<int>(lm.n);
+  const int slot = slot_off + blockIdx.x * WG + threadIdx.x;  // the grid covers this group's slots exactly
   Counters C = {0, 0, 0, 0, 0, 0, 0};
-  LaneState L;
-  L.st = ST_IDLE;
-  L.qmode = Q_NONE;
-  L.kdone = 0;
-  bool loaded = false;
-  if (valid) {
-    L.st = A.iv[slot];                                       // field 0 = st
-    L.kdone = A.iv[static_cast<size_t>(18) * nslot + slot];  // field 18 = kdone
-    if (L.st != ST_IDLE || static_cast<int64_t>(slot) + static_cast<int64_t>(L.kdone) * nslot < F.n_samples) {
-      loaded = true;
-      load_lane(L, A, slot, nslot);
-      if (L.qmode != Q_NONE) {  // result of the previous iteration's query
-        L.bt = A.res_t[slot];
-        L.bobj = A.res_i[slot];
-        L.bsub = A.res_i[static_cast<size_t>(nslot) + slot];
-        L.bhave = A.res_i[static_cast<size_t>(2) * nslot + slot];
-      }
-      L.qmode = Q_NONE;
-      for (;;) {
-        claim_sample(L, F, hits, slot, nslot);
-        if (L.st == ST_IDLE) break;
-        advance_lane<STATS, false>(L, S, F, C, sbuf, nullptr, hits, 0, 0, pbuf, static_cast<size_t>(nslot),
-                                   static_cast<size_t>(slot), pend_cap);
-        if (L.qmode != Q_NONE) break;
-      }
+  LaneRef L(lm, static_cast<size_t>(slot));
+  int qm = Q_NONE;
+  if (L.st != ST_IDLE || static_cast<int64_t>(slot) + static_cast<int64_t>(L.kdone) * nslot < F.n_samples) {
+    // the previous iteration's query result is already in L.bt/bobj/bsub/bhave
+    L.qmode = Q_NONE;
+    for (;;) {
+      claim_sample(L, F, hits, slot, nslot);
+      if (L.st == ST_IDLE) break;
+      advance_lane<STATS, false>(L, S, F, C, sbuf, nullptr, hits, 0, 0, pbuf, lm.n, static_cast<size_t>(slot),
+                                 pend_cap);
+      if (L.qmode != Q_NONE) break;
     }
+    qm = L.qmode;
   }
   // compaction: append queries to their list, one atomic per wave per list
   const int lane = threadIdx.x & 63;
 #pragma unroll
   for (int m = Q_CLOSEST; m <= Q_NEXT; ++m) {
-    const unsigned long long mask = __ballot(valid && L.qmode == m);
+    const unsigned long long mask = __ballot(qm == m);
     if (mask == 0ull) continue;
     unsigned int base = 0;
     if (lane == 0) base = atomicAdd(&counters[m - 1], static_cast<unsigned int>(__popcll(mask)));
     base = __shfl(base, 0);
-    if (valid && L.qmode == m) {
+    if (qm == m) {
       const QList& Q = m == Q_CLOSEST ? q0 : q1;
-      const size_t cap = static_cast<size_t>(nslot);
+      const size_t cap = Q.cap;
       const unsigned int k = base + lane_prefix(mask);
       dvec3 qP = L.rp, qD = L.rd;
       double qlim = RTX_INF;
@@ -1008,9 +1033,8 @@ __global__ void __launch_bounds__(WG) advance_kernel(DevScene S, const FramePara
       Q.iv[1 * cap + k] = L.qsq;
     }
   }
-  const unsigned long long alive = __ballot(valid && L.st != ST_IDLE);
+  const unsigned long long alive = __ballot(L.st != ST_IDLE);
   if (lane == 0 && alive) atomicAdd(&counters[2], static_cast<unsigned int>(__popcll(alive)));
-  if (loaded) store_lane(L, A, slot, nslot);
   if (STATS) {
     int64_t v[7] = {C.camera, C.secondary, C.shadow, C.nodes, C.objects, C.tris, C.shades};
 #pragma unroll
@@ -1023,15 +1047,14 @@ __global__ void __launch_bounds__(WG) advance_kernel(DevScene S, const FramePara
 }
 
 template <bool STATS, int MODE>
-__global__ void __launch_bounds__(WG) trace_kernel(DevScene S, QList Q, const unsigned int* __restrict__ counters,
-                                                    SlotArrays A, int nslot, int stack_cap,
-                                                    unsigned long long* __restrict__ stats) {
+__global__ void __launch_bounds__(WG, RTX_TRACE_WAVES) trace_kernel(DevScene S, QList Q, const unsigned int* __restrict__ counters,
+                                                    LaneMem lm, int stack_cap, unsigned long long* __restrict__ stats) {
   extern __shared__ int lds_stack[];
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   int* stk = lds_stack + wave * stack_cap * 64;
   const unsigned int n = counters[MODE - 1];
-  const size_t cap = static_cast<size_t>(nslot);
+  const size_t cap = Q.cap;
   Counters C = {0, 0, 0, 0, 0, 0, 0};
   for (unsigned int k = blockIdx.x * WG + threadIdx.x; k < ((n + 63u) & ~63u); k += gridDim.x * WG) {
     if (k < n) {
@@ -1042,11 +1065,11 @@ __global__ void __launch_bounds__(WG) trace_kernel(DevScene S, QList Q, const un
       double bt;
       int bobj, bsub;
       const bool have = traverse<STATS>(S, MODE, P, D, tp, rp, sq, tlim, bt, bobj, bsub, stk, lane, C);
-      const int slot = Q.slot[k];
-      A.res_t[slot] = bt;
-      A.res_i[slot] = bobj;
-      A.res_i[static_cast<size_t>(nslot) + slot] = bsub;
-      A.res_i[static_cast<size_t>(2) * nslot + slot] = have ? 1 : 0;
+      const size_t slot = static_cast<size_t>(Q.slot[k]);
+      lm.d[size_t(LD_bt) * lm.n + slot] = bt;
+      lm.i[size_t(LI_bobj) * lm.n + slot] = bobj;
+      lm.i[size_t(LI_bsub) * lm.n + slot] = bsub;
+      lm.i[size_t(LI_bhave) * lm.n + slot] = have ? 1 : 0;
     }
   }
   if (STATS) {
@@ -1133,6 +1156,11 @@ struct SceneState {
   // wavefront path: slot state, query lists, counters
   void* d_wf = nullptr;
   size_t wf_bytes = 0;
+  void* d_lane = nullptr;       // LaneRef state of every lane / slot (HBM)
+  size_t lane_bytes = 0;
+  std::vector<hipStream_t> wf_streams;  // wavefront slot groups
+  std::vector<hipEvent_t> wf_join, wf_check;
+  hipEvent_t wf_fork = nullptr;
   unsigned int* d_counters = nullptr;
   unsigned int* h_counters = nullptr;  // pinned
   std::vector<hipEvent_t> ev_pool;
@@ -1316,6 +1344,11 @@ rtx_status rtx_scene_destroy(void* scene) {
   if (st->d_sbuf) (void)hipFree(st->d_sbuf);
   if (st->d_pbuf) (void)hipFree(st->d_pbuf);
   if (st->d_wf) (void)hipFree(st->d_wf);
+  if (st->d_lane) (void)hipFree(st->d_lane);
+  for (auto e : st->wf_join) (void)hipEventDestroy(e);
+  for (auto e : st->wf_check) (void)hipEventDestroy(e);
+  if (st->wf_fork) (void)hipEventDestroy(st->wf_fork);
+  for (auto q : st->wf_streams) (void)hipStreamDestroy(q);
   if (st->d_counters) (void)hipFree(st->d_counters);
   if (st->h_counters) (void)hipHostFree(st->h_counters);
   for (auto e : st->ev_pool) (void)hipEventDestroy(e);
@@ -1505,10 +1538,10 @@ rtx_status rtx_render(void* scene, const RtxRenderParams* params, uint8_t* rgb8,
     }
     return RTX_OK;
   };
-  // megakernel by default; RTX_WAVEFRONT=1 selects the wavefront path for
-  // non-adaptive frames (kernels)
-  const char* wf_env = getenv("RTX_WAVEFRONT");
-  const bool megakernel = adaptive || !(wf_env && atoi(wf_env) != 0);
+  // wavefront path by default; adaptive AA (per-pixel sample frames) and
+  // RTX_MEGAKERNEL=1 use the persistent megakernel (kernels)
+  const char* mk_env = getenv("RTX_MEGAKERNEL");
+  const bool megakernel = adaptive || (mk_env && atoi(mk_env) != 0);
   double* sb = adaptive ? nullptr : st->d_sbuf;
   std::vector<std::pair<hipEvent_t, hipEvent_t>> frame_events;
 
@@ -1550,73 +1583,91 @@ rtx_status rtx_render(void* scene, const RtxRenderParams* params, uint8_t* rgb8,
     if ((rc = ensure(reinterpret_cast<void**>(&st->d_pbuf), &st->pbuf_bytes,
                      size_t(grid) * WG * pend_cap * 13 * sizeof(double))) != RTX_OK)
       return rc;
+    if ((rc = ensure(&st->d_lane, &st->lane_bytes, lane_mem_bytes(size_t(grid) * WG))) != RTX_OK) return rc;
+    const LaneMem lm = lane_mem_at(st->d_lane, size_t(grid) * WG);
     hipEvent_t e0, e1;
     if ((rc = get_event(&e0)) != RTX_OK || (rc = get_event(&e1)) != RTX_OK) return rc;
     HIP_TRY(hipEventRecord(e0, stream));
     if (stats) {
       if (adaptive)
         hipLaunchKernelGGL((render_kernel<true, true>), dim3(grid), dim3(WG), lds, stream, st->S_launch, st->d_frame,
-                           st->d_work, sb, d_hits, d_rgb8, d_rgbf, st->d_stats, st->stack_cap, st->d_pbuf, pend_cap);
+                           st->d_work, sb, d_hits, d_rgb8, d_rgbf, st->d_stats, st->stack_cap, st->d_pbuf, pend_cap, lm);
       else
         hipLaunchKernelGGL((render_kernel<true, false>), dim3(grid), dim3(WG), lds, stream, st->S_launch,
                            st->d_frame, st->d_work, sb, d_hits, d_rgb8, d_rgbf, st->d_stats, st->stack_cap,
-                           st->d_pbuf, pend_cap);
+                           st->d_pbuf, pend_cap, lm);
     } else {
       if (adaptive)
         hipLaunchKernelGGL((render_kernel<false, true>), dim3(grid), dim3(WG), lds, stream, st->S_launch,
                            st->d_frame, st->d_work, sb, d_hits, d_rgb8, d_rgbf, st->d_stats, st->stack_cap,
-                           st->d_pbuf, pend_cap);
+                           st->d_pbuf, pend_cap, lm);
       else
         hipLaunchKernelGGL((render_kernel<false, false>), dim3(grid), dim3(WG), lds, stream, st->S_launch,
                            st->d_frame, st->d_work, sb, d_hits, d_rgb8, d_rgbf, st->d_stats, st->stack_cap,
-                           st->d_pbuf, pend_cap);
+                           st->d_pbuf, pend_cap, lm);
     }
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipEventRecord(e1, stream));
     frame_events.push_back({e0, e1});
   } else {
     // ---------------- wavefront path
-    int64_t nslot64 = static_cast<int64_t>(st->n_cu) * 2048;
+    // NSLOT path slots split into G groups, each iterating advance -> trace
+    // (closest) -> trace (next) on its own stream, so one group's launch
+    // tails overlap the other groups' work.
+    int64_t nslot64 = static_cast<int64_t>(st->n_cu) * 49152;  // 12.6 M on 256 CUs (tools/gpu_exp*.sh sweeps)
     const char* ns_env = getenv("RTX_SLOTS");
     if (ns_env && atoll(ns_env) > 0) nslot64 = atoll(ns_env);
+    int G = 3;
+    const char* g_env = getenv("RTX_GROUPS");
+    if (g_env && atoi(g_env) > 0) G = atoi(g_env);
+    if (G > 16) G = 16;
     if (nslot64 > F.n_samples) nslot64 = F.n_samples;
-    nslot64 = ((nslot64 + WG - 1) / WG) * WG;
-    if (nslot64 < WG) nslot64 = WG;
+    const int64_t per = (nslot64 + G * WG - 1) / (G * WG);  // workgroups per group
+    const int64_t gslots = per * WG;
+    nslot64 = gslots * G;
+    const size_t ns = static_cast<size_t>(nslot64);
     const int nslot = static_cast<int>(nslot64);
-    const size_t ns = static_cast<size_t>(nslot);
-    const size_t bytes_iv = ns * N_INT_FIELDS * sizeof(int);
-    const size_t bytes_dv = ns * N_DBL_FIELDS * sizeof(double);
-    const size_t bytes_rt = ns * sizeof(double);
-    const size_t bytes_ri = ns * 3 * sizeof(int);
-    const size_t bytes_q = ns * (sizeof(int) + 8 * sizeof(double) + 2 * sizeof(int));
+    const size_t gs = static_cast<size_t>(gslots);
+    const size_t bytes_q = gs * (sizeof(int) + 8 * sizeof(double) + 2 * sizeof(int)) + 1024;
     auto al = [](size_t x) { return (x + 255) & ~size_t(255); };
-    const size_t total = al(bytes_iv) + al(bytes_dv) + al(bytes_rt) + al(bytes_ri) + 2 * al(bytes_q);
-    if ((rc = ensure(&st->d_wf, &st->wf_bytes, total)) != RTX_OK) return rc;
+    if ((rc = ensure(&st->d_wf, &st->wf_bytes, size_t(G) * 2 * al(bytes_q))) != RTX_OK) return rc;
+    if ((rc = ensure(&st->d_lane, &st->lane_bytes, lane_mem_bytes(ns))) != RTX_OK) return rc;
+    const LaneMem A = lane_mem_at(st->d_lane, ns);
     if ((rc = ensure(reinterpret_cast<void**>(&st->d_pbuf), &st->pbuf_bytes,
                      ns * pend_cap * 13 * sizeof(double))) != RTX_OK)
       return rc;
-    if (!st->d_counters) HIP_TRY(hipMalloc(&st->d_counters, 4 * sizeof(unsigned int)));
-    if (!st->h_counters) HIP_TRY(hipHostMalloc(&st->h_counters, 4 * sizeof(unsigned int)));
-    char* base = static_cast<char*>(st->d_wf);
-    SlotArrays A;
-    A.iv = reinterpret_cast<int*>(base);
-    base += al(bytes_iv);
-    A.dv = reinterpret_cast<double*>(base);
-    base += al(bytes_dv);
-    A.res_t = reinterpret_cast<double*>(base);
-    base += al(bytes_rt);
-    A.res_i = reinterpret_cast<int*>(base);
-    base += al(bytes_ri);
-    QList ql[2];
-    for (int m = 0; m < 2; ++m) {
-      ql[m].slot = reinterpret_cast<int*>(base);
-      ql[m].d = reinterpret_cast<double*>(base + al(ns * sizeof(int)));
-      ql[m].iv = reinterpret_cast<int*>(base + al(ns * sizeof(int)) + al(ns * 8 * sizeof(double)));
-      base += al(bytes_q);
+    if (!st->d_counters) HIP_TRY(hipMalloc(&st->d_counters, 16 * 4 * sizeof(unsigned int)));
+    if (!st->h_counters) HIP_TRY(hipHostMalloc(&st->h_counters, 16 * 4 * sizeof(unsigned int)));
+    // group 0 runs on the caller's stream, groups 1.. on their own streams
+    // (GPU_MAX_HW_QUEUES is 4 by default: more streams than queues would
+    // serialize groups behind each other)
+    while (static_cast<int>(st->wf_streams.size()) < G) {
+      hipStream_t s2;
+      HIP_TRY(hipStreamCreateWithFlags(&s2, hipStreamNonBlocking));
+      st->wf_streams.push_back(s2);
+      hipEvent_t ev;
+      HIP_TRY(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+      st->wf_join.push_back(ev);
+      HIP_TRY(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+      st->wf_check.push_back(ev);
+    }
+    if (!st->wf_fork) HIP_TRY(hipEventCreateWithFlags(&st->wf_fork, hipEventDisableTiming));
+    std::vector<QList> ql(size_t(G) * 2);
+    {
+      char* base = static_cast<char*>(st->d_wf);
+      for (size_t m = 0; m < ql.size(); ++m) {
+        ql[m].slot = reinterpret_cast<int*>(base);
+        ql[m].d = reinterpret_cast<double*>(base + al(gs * sizeof(int)));
+        ql[m].iv = reinterpret_cast<int*>(base + al(gs * sizeof(int)) + al(gs * 8 * sizeof(double)));
+        ql[m].cap = gs;
+        base += al(bytes_q);
+      }
     }
     F.qchunk = 64;
     HIP_TRY(hipMemcpyAsync(st->d_frame, &F, sizeof(FrameParams), hipMemcpyHostToDevice, stream));
-    HIP_TRY(hipMemsetAsync(A.iv, 0, bytes_iv, stream));  // every slot ST_IDLE, kdone = 0, no pending query
+    // every slot ST_IDLE, kdone = 0, no pending query
+    HIP_TRY(hipMemsetAsync(A.i, 0, ns * LI_COUNT * sizeof(int), stream));
+    HIP_TRY(hipMemsetAsync(st->d_counters, 0, 16 * 4 * sizeof(unsigned int), stream));
     const size_t lds = size_t(st->stack_cap) * 64 * sizeof(int) * WAVES_PER_WG;
     if (lds > 160 * 1024) {
       g_err = "rtx_render: LDS budget exceeded (BVH too deep)";
@@ -1629,53 +1680,73 @@ rtx_status rtx_render(void* scene, const RtxRenderParams* params, uint8_t* rgb8,
     HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, tfn, WG, lds));
     if (per_cu < 1) per_cu = 1;
     int64_t tgrid = static_cast<int64_t>(st->n_cu) * per_cu;
-    const int64_t tneed = (nslot64 + WG - 1) / WG;
-    if (tgrid > tneed) tgrid = tneed;
-    const int agrid = nslot / WG;
+    if (tgrid > per) tgrid = per;
     const char* dbg_env = getenv("RTX_DEBUG");
     const bool dbg = dbg_env && atoi(dbg_env) != 0;
-    const int check_every = dbg ? 1 : 8;
-    bool done = false;
-    for (int it = 0; !done; ++it) {
-      HIP_TRY(hipMemsetAsync(st->d_counters, 0, 3 * sizeof(unsigned int), stream));
-      if (stats)
-        hipLaunchKernelGGL((advance_kernel<true>), dim3(agrid), dim3(WG), 0, stream, S, st->d_frame, A, nslot, sb,
-                           d_hits, st->d_pbuf, pend_cap, ql[0], ql[1], st->d_counters, st->d_stats);
-      else
-        hipLaunchKernelGGL((advance_kernel<false>), dim3(agrid), dim3(WG), 0, stream, S, st->d_frame, A, nslot, sb,
-                           d_hits, st->d_pbuf, pend_cap, ql[0], ql[1], st->d_counters, st->d_stats);
-      HIP_TRY(hipGetLastError());
-      hipEvent_t e0, e1;
-      if ((rc = get_event(&e0)) != RTX_OK || (rc = get_event(&e1)) != RTX_OK) return rc;
-      HIP_TRY(hipEventRecord(e0, stream));
-      if (stats) {
-        hipLaunchKernelGGL((trace_kernel<true, Q_CLOSEST>), dim3(tgrid), dim3(WG), lds, stream, S, ql[0],
-                           st->d_counters, A, nslot, st->stack_cap, st->d_stats);
-        hipLaunchKernelGGL((trace_kernel<true, Q_NEXT>), dim3(tgrid), dim3(WG), lds, stream, S, ql[1],
-                           st->d_counters, A, nslot, st->stack_cap, st->d_stats);
-      } else {
-        hipLaunchKernelGGL((trace_kernel<false, Q_CLOSEST>), dim3(tgrid), dim3(WG), lds, stream, S, ql[0],
-                           st->d_counters, A, nslot, st->stack_cap, st->d_stats);
-        hipLaunchKernelGGL((trace_kernel<false, Q_NEXT>), dim3(tgrid), dim3(WG), lds, stream, S, ql[1],
-                           st->d_counters, A, nslot, st->stack_cap, st->d_stats);
-      }
-      HIP_TRY(hipGetLastError());
-      HIP_TRY(hipEventRecord(e1, stream));
-      frame_events.push_back({e0, e1});
-      if (it % check_every == check_every - 1) {
-        HIP_TRY(hipMemcpyAsync(st->h_counters, st->d_counters, 3 * sizeof(unsigned int), hipMemcpyDeviceToHost,
-                               stream));
-        HIP_TRY(hipStreamSynchronize(stream));
-        if (dbg)
-          fprintf(stderr, "rtx iter %d: closest %u next %u alive %u (nslot %d)\n", it, st->h_counters[0],
-                  st->h_counters[1], st->h_counters[2], nslot);
-        if (st->h_counters[2] == 0) done = true;  // no live slot after this advance
+    const int check_every = 4;
+    hipEvent_t e0, e1;
+    if ((rc = get_event(&e0)) != RTX_OK || (rc = get_event(&e1)) != RTX_OK) return rc;
+    HIP_TRY(hipEventRecord(e0, stream));
+    HIP_TRY(hipEventRecord(st->wf_fork, stream));
+    for (int g = 1; g < G; ++g) HIP_TRY(hipStreamWaitEvent(st->wf_streams[size_t(g)], st->wf_fork, 0));
+    std::vector<int> done(size_t(G), 0), pending_check(size_t(G), -1);
+    int ndone = 0;
+    for (int it = 0; ndone < G; ++it) {
+      for (int g = 0; g < G; ++g) {
+        if (done[size_t(g)]) continue;
+        hipStream_t sg = g == 0 ? stream : st->wf_streams[size_t(g)];
+        unsigned int* cnt = st->d_counters + 4 * g;
+        const QList& q0 = ql[size_t(g) * 2];
+        const QList& q1 = ql[size_t(g) * 2 + 1];
+        HIP_TRY(hipMemsetAsync(cnt, 0, 3 * sizeof(unsigned int), sg));
+        if (stats)
+          hipLaunchKernelGGL((advance_kernel<true>), dim3(per), dim3(WG), 0, sg, S, st->d_frame, A, sb, d_hits,
+                             st->d_pbuf, pend_cap, q0, q1, cnt, st->d_stats, static_cast<int>(g * gslots));
+        else
+          hipLaunchKernelGGL((advance_kernel<false>), dim3(per), dim3(WG), 0, sg, S, st->d_frame, A, sb, d_hits,
+                             st->d_pbuf, pend_cap, q0, q1, cnt, st->d_stats, static_cast<int>(g * gslots));
+        if (stats) {
+          hipLaunchKernelGGL((trace_kernel<true, Q_CLOSEST>), dim3(tgrid), dim3(WG), lds, sg, S, q0, cnt, A,
+                             st->stack_cap, st->d_stats);
+          hipLaunchKernelGGL((trace_kernel<true, Q_NEXT>), dim3(tgrid), dim3(WG), lds, sg, S, q1, cnt, A,
+                             st->stack_cap, st->d_stats);
+        } else {
+          hipLaunchKernelGGL((trace_kernel<false, Q_CLOSEST>), dim3(tgrid), dim3(WG), lds, sg, S, q0, cnt, A,
+                             st->stack_cap, st->d_stats);
+          hipLaunchKernelGGL((trace_kernel<false, Q_NEXT>), dim3(tgrid), dim3(WG), lds, sg, S, q1, cnt, A,
+                             st->stack_cap, st->d_stats);
+        }
+        HIP_TRY(hipGetLastError());
+        if (it % check_every == check_every - 1) {
+          // pipelined liveness check: read back the counters of the check
+          // enqueued one round earlier (the GPU keeps ~check_every
+          // iterations of this group queued meanwhile)
+          if (pending_check[size_t(g)] >= 0) {
+            HIP_TRY(hipEventSynchronize(st->wf_check[size_t(g)]));
+            const unsigned int alive = st->h_counters[4 * g + 2];
+            if (dbg)
+              fprintf(stderr, "rtx group %d iter %d: alive %u (closest %u next %u)\n", g, pending_check[size_t(g)],
+                      alive, st->h_counters[4 * g + 0], st->h_counters[4 * g + 1]);
+            if (alive == 0) {
+              done[size_t(g)] = 1;
+              ++ndone;
+              HIP_TRY(hipEventRecord(st->wf_join[size_t(g)], sg));
+              continue;
+            }
+          }
+          HIP_TRY(hipMemcpyAsync(st->h_counters + 4 * g, cnt, 3 * sizeof(unsigned int), hipMemcpyDeviceToHost, sg));
+          HIP_TRY(hipEventRecord(st->wf_check[size_t(g)], sg));
+          pending_check[size_t(g)] = it;
+        }
       }
       if (it > 1000000) {
         g_err = "rtx_render: wavefront loop did not terminate";
         return RTX_ERR_INVALID;
       }
     }
+    for (int g = 1; g < G; ++g) HIP_TRY(hipStreamWaitEvent(stream, st->wf_join[size_t(g)], 0));
+    HIP_TRY(hipEventRecord(e1, stream));
+    frame_events.push_back({e0, e1});
   }
   if (!adaptive) {
     const int64_t rblocks = (npix + WG - 1) / WG;

@@ -33,15 +33,17 @@ def _compare(gpu, ref, spp):
     assert np.array_equal(gh["t"][hit], rh["t"][hit]), "primary hit t not bit-exact"
 
 
-# render paths (DESIGN.md "Kernels"): the persistent megakernel (default), the
-# wavefront advance/trace pipeline, and the wavefront with a tiny slot pool so
-# every slot walks many samples (claim_sample's static deal)
-PATHS = {"mega": {}, "wavefront": {"RTX_WAVEFRONT": "1"}, "wavefront_256": {"RTX_WAVEFRONT": "1", "RTX_SLOTS": "256"}}
+# render paths (DESIGN.md "Kernels"): the wavefront advance/trace pipeline
+# (default, 3 slot groups on 3 streams), the persistent megakernel, one slot
+# group, and a tiny slot pool so every slot walks many samples
+# (claim_sample's static deal)
+PATHS = {"wavefront": {}, "mega": {"RTX_MEGAKERNEL": "1"}, "wavefront_1g": {"RTX_GROUPS": "1"},
+         "wavefront_256": {"RTX_SLOTS": "256"}}
 
 
 @pytest.fixture(params=list(PATHS), ids=list(PATHS))
 def render_path(request):
-    saved = {k: os.environ.get(k) for k in ("RTX_WAVEFRONT", "RTX_SLOTS")}
+    saved = {k: os.environ.get(k) for k in ("RTX_MEGAKERNEL", "RTX_SLOTS", "RTX_GROUPS")}
     for k in saved:
         os.environ.pop(k, None)
     os.environ.update(PATHS[request.param])
