@@ -78,8 +78,19 @@ RT_HD dvec3 gclamp3(const dvec3& v, double lo, double hi) {
 RT_HD dvec3 gmin3(const dvec3& a, const dvec3& b) { return mk3(gmin(a.x, b.x), gmin(a.y, b.y), gmin(a.z, b.z)); }
 RT_HD dvec3 gmax3(const dvec3& a, const dvec3& b) { return mk3(gmax(a.x, b.x), gmax(a.y, b.y), gmax(a.z, b.z)); }
 
+// Scalar pow.  On the device it is an out-of-line call: the FP64 pow of the
+// device math library is long, and three inlined copies interleaved by the
+// scheduler dominated the register peak of the shading kernel.
+#if defined(__HIP_DEVICE_COMPILE__)
+__device__ __attribute__((noinline)) inline double rpow(double b, double e) { return ::pow(b, e); }
+#elif defined(__HIPCC__)
+__host__ inline double rpow(double b, double e) { return ::pow(b, e); }
+#else
+inline double rpow(double b, double e) { return pow(b, e); }
+#endif
+
 // glm::pow(dvec3, dvec3(s)) — componentwise std::pow.
-RT_HD dvec3 pow3(const dvec3& b, double e) { return mk3(pow(b.x, e), pow(b.y, e), pow(b.z, e)); }
+RT_HD dvec3 pow3(const dvec3& b, double e) { return mk3(rpow(b.x, e), rpow(b.y, e), rpow(b.z, e)); }
 
 // ray::at (scene/ray.h:40): p + (t * d)
 RT_HD dvec3 ray_at(const dvec3& p, const dvec3& d, double t) { return p + (t * d); }

@@ -172,7 +172,10 @@ __device__ __forceinline__ dvec3 tex_pixel(const DevScene& S, const RtxTexture& 
   return mk3(0.0, 0.0, 0.0);
 }
 
-__device__ dvec3 tex_lookup(const DevScene& S, int tex, const dvec2& uv) {
+// noinline: one out-of-line copy instead of one inlined copy per material
+// parameter (textures are rare; the register peak of the shading kernel
+// must not carry eight bilinear lookups)
+__device__ __noinline__ dvec3 tex_lookup(const DevScene& S, int tex, const dvec2& uv) {
   const RtxTexture t = S.texs[tex];
   double x = uv.x, y = uv.y;
   if (0.0 <= x && x <= 1.0 && 0.0 <= y && y <= 1.0) {

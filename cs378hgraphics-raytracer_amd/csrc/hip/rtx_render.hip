@@ -108,15 +108,22 @@ __device__ __forceinline__ double radinv2(int n) {  // hammersley x (util.cpp:3-
 
 // Recompute the winning entry's local quantities (deterministic: same
 // operations as the traversal) and resolve the isect the reference returns:
-// world normal (scene.cpp:31-33), uv and material.
-struct Resolved {
+// world normal (scene.cpp:31-33), uv, and where its material comes from.
+// Material parameters are then evaluated one at a time where the state
+// machine needs them (hit_param & co.), not all ten up front: the shading
+// kernel's register peak is set by how much of a material is live at once.
+struct HitRef {
   dvec3 N;
-  EvalMat m;
+  dvec2 uv;
+  dvec3 bary;
+  int mat;          // material index (objects without per-vertex materials)
+  int vm_off;       // >= 0: per-vertex materials of the mesh (vi valid)
+  int vi0, vi1, vi2;
 };
 
-__device__ Resolved resolve_hit(const DevScene& S, const dvec3& P, const dvec3& D, int oi, int sub,
-                                int* rec_face, int* rec_mleaf) {
-  Resolved r;
+__device__ HitRef resolve_hit(const DevScene& S, const dvec3& P, const dvec3& D, int oi, int sub,
+                              int* rec_face, int* rec_mleaf) {
+  HitRef r;
   const RtxObject& o = S.objs[oi];
   const RtxMaterial& mat = S.mats[o.material];
   const dvec3 pos = rtm::xform_point(o.inv, P);
@@ -144,7 +151,11 @@ __device__ Resolved resolve_hit(const DevScene& S, const dvec3& P, const dvec3& 
     } else {
       nl = ld3(F.n);
     }
-    r.m = me.has_vmats ? eval_vertex_material(S, me, fi, bary) : eval_material(S, mat, uv);
+    r.bary = bary;
+    r.vm_off = me.has_vmats ? me.vert_off : -1;
+    r.vi0 = fi.vi[0];
+    r.vi1 = fi.vi[1];
+    r.vi2 = fi.vi[2];
     if (rec_face) {
       *rec_face = fi.orig_id;
       *rec_mleaf = fi.leaf;
@@ -188,10 +199,42 @@ __device__ Resolved resolve_hit(const DevScene& S, const dvec3& P, const dvec3& 
       nl = dir.z > 0.0 ? mk3(0.0, 0.0, -1.0) : mk3(0.0, 0.0, 1.0);
       uv = rtm::mk2(Q.x + 0.5, Q.y + 0.5);
     }
-    r.m = eval_material(S, mat, uv);
+    r.bary = mk3(0.0, 0.0, 0.0);
+    r.vm_off = -1;
+    r.vi0 = r.vi1 = r.vi2 = 0;
   }
+  r.mat = o.material;
+  r.uv = uv;
   r.N = rtm::normalize(rtm::mat3_mul(o.normi, nl));
   return r;
+}
+
+// One material parameter at a hit: MaterialParameter::value
+// (material.cpp:140-146), or the per-vertex interpolation
+// Material() += b_k * M_k (trimesh.cpp:157-163, index starts at 1).
+__device__ __forceinline__ dvec3 hit_param(const DevScene& S, const HitRef& h, int k) {
+  if (h.vm_off >= 0) {
+    const int f = k <= RTX_P_KT ? 3 * k : (k == RTX_P_SHININESS ? 18 : (k == RTX_P_INDEX ? 21 : 24));
+    dvec3 e = k == RTX_P_INDEX ? mk3(1.0, 1.0, 1.0) : mk3(0.0, 0.0, 0.0);
+    e += ld3(reinterpret_cast<const double*>(&S.vmats[h.vm_off + h.vi0]) + f) * h.bary.x;
+    e += ld3(reinterpret_cast<const double*>(&S.vmats[h.vm_off + h.vi1]) + f) * h.bary.y;
+    e += ld3(reinterpret_cast<const double*>(&S.vmats[h.vm_off + h.vi2]) + f) * h.bary.z;
+    return e;
+  }
+  return pval(S, S.mats[h.mat].p[k], h.uv);
+}
+// shininess (material.h:204-209: a texture map is scaled by 128)
+__device__ __forceinline__ double hit_shininess(const DevScene& S, const HitRef& h) {
+  if (h.vm_off >= 0) return intensity(hit_param(S, h, RTX_P_SHININESS));
+  const RtxParam& shp = S.mats[h.mat].p[RTX_P_SHININESS];
+  return shp.tex >= 0 ? 128.0 * intensity(pval(S, shp, h.uv)) : intensity(ld3(shp.v));
+}
+__device__ __forceinline__ double hit_index(const DevScene& S, const HitRef& h) {
+  return intensity(hit_param(S, h, RTX_P_INDEX));
+}
+// per-vertex materials never get setBools (decision U2: flags 0)
+__device__ __forceinline__ int hit_flags(const DevScene& S, const HitRef& h) {
+  return h.vm_off >= 0 ? 0 : S.mats[h.mat].flags;
 }
 
 // ============================================================ lights
@@ -332,6 +375,10 @@ __device__ __forceinline__ void advance_lane(LaneRef& L, const DevScene& S, cons
   };
   qmode = Q_NONE;
   while (st != ST_IDLE && qmode == Q_NONE) {
+    // compiler barrier: the lane state is memory (LaneRef); without this,
+    // LLVM promotes every field to a loop-carried register and the kernel
+    // needs ~290 VGPRs.  Each step re-reads the few fields it uses.
+    asm volatile("" ::: "memory");
     switch (st) {
       case ST_CAM: {
         // next camera ray of trace(x, y) (RayTracer.cpp:35-79)
@@ -450,18 +497,18 @@ __device__ __forceinline__ void advance_lane(LaneRef& L, const DevScene& S, cons
           W = W * rtm::gmax3(rtm::gmin3(rtm::pow3(area_sum, bt), rtm::splat3(1.0)), rtm::splat3(0.0));
         else if (rkind == 2)
           W = W * rtm::pow3(area_sum, bt);
-        const Resolved R = resolve_hit(S, rp, rd, bobj, bsub, nullptr, nullptr);
+        const HitRef R = resolve_hit(S, rp, rd, bobj, bsub, nullptr, nullptr);
         N = R.N;
-        m_kd = R.m.kd;
-        m_ks = R.m.ks;
-        m_sh = R.m.sh;
-        m_flags = R.m.flags;
+        m_kd = hit_param(S, R, RTX_P_KD);
+        m_ks = hit_param(S, R, RTX_P_KS);
+        m_sh = hit_shininess(S, R);
+        m_flags = hit_flags(S, R);
         st_t = bt;
         sobj = bobj;
         ssub = bsub;
         if (STATS) C.shades++;
         // Material::shade (material.cpp:34-69)
-        i_out = R.m.ke + R.m.ka * mk3(S.ambient[0], S.ambient[1], S.ambient[2]);
+        i_out = hit_param(S, R, RTX_P_KE) + hit_param(S, R, RTX_P_KA) * mk3(S.ambient[0], S.ambient[1], S.ambient[2]);
         li = 0;
         st = ST_LIGHT;
         break;
@@ -475,27 +522,28 @@ __device__ __forceinline__ void advance_lane(LaneRef& L, const DevScene& S, cons
           st = ST_POP;
           if (aterm > 0.0 && rtm::dot(col, col) < aterm) break;
           if ((m_flags & RTX_MF_RECUR) && depth > 0) {
-            const Resolved R = resolve_hit(S, rp, rd, sobj, ssub, nullptr, nullptr);
+            const HitRef R = resolve_hit(S, rp, rd, sobj, ssub, nullptr, nullptr);
             const bool leaving = rtm::dot(N, rd) >= 0;
             const bool in_trans = (m_flags & RTX_MF_TRANS) != 0;
             const bool next_trans = leaving ? true : in_trans;  // air is transmissive
             const dvec3 normal = (leaving ? -1.0 : 1.0) * N;
             const double c = -1 * rtm::dot(normal, rd);
             const double eta =
-                next_trans ? (leaving ? R.m.index : S.air_index) / (leaving ? S.air_index : R.m.index) : 0;
+                next_trans ? (leaving ? hit_index(S, R) : S.air_index) / (leaving ? S.air_index : hit_index(S, R)) : 0;
             const double radicand = 1 - eta * eta * (1 - c * c);
             const bool tir = next_trans && radicand < 0;
             // push refraction first so that reflection is traced first
             if (next_trans && !tir && top < pend_cap) {
               const dvec3 tp = rtm::ray_at(rp, rd, st_t + RTX_RAY_EPS);
               const dvec3 td = eta * rd + (eta * c - sqrt(radicand)) * normal;
-              push(top, tp, td, W, leaving ? mk3(1.0, 1.0, 1.0) : R.m.kt, depth, 2);
+              push(top, tp, td, W, leaving ? mk3(1.0, 1.0, 1.0) : hit_param(S, R, RTX_P_KT), depth, 2);
               if (STATS) C.secondary++;
             }
             if (((m_flags & RTX_MF_REFL) || tir) && top < pend_cap) {
               const dvec3 rdir = rd + 2 * c * normal;
               const dvec3 rs = rtm::ray_at(rp, rd, st_t - RTX_RAY_EPS);
-              push(top, rs, rdir, W * R.m.kr, leaving ? R.m.kt : mk3(1.0, 1.0, 1.0), depth, 1);
+              push(top, rs, rdir, W * hit_param(S, R, RTX_P_KR), leaving ? hit_param(S, R, RTX_P_KT) : mk3(1.0, 1.0, 1.0),
+                   depth, 1);
               if (STATS) C.secondary++;
             }
           }
@@ -508,7 +556,8 @@ __device__ __forceinline__ void advance_lane(LaneRef& L, const DevScene& S, cons
         double dt = rtm::dot(l_i, N);
         if (m_flags & RTX_MF_TRANS) dt = fabs(dt);
         const dvec3 d_comp = m_kd * rtm::gmax(0.0, dt);
-        const dvec3 s_comp = m_ks * rtm::pow3(rtm::splat3(rtm::gmax(0.0, rtm::dot(l_r, rd))), m_sh);
+        // glm::pow(dvec3(x), dvec3(sh)): three identical std::pow calls, one here
+        const dvec3 s_comp = m_ks * rtm::splat3(rtm::rpow(rtm::gmax(0.0, rtm::dot(l_r, rd)), m_sh));
         dscomp = d_comp + s_comp;
         dattn = light_dist_atten(L, X);
         // shadowAttenuation (light.cpp:16-20) / AreaLight (light.cpp:76-87)
@@ -578,7 +627,7 @@ __device__ __forceinline__ void advance_lane(LaneRef& L, const DevScene& S, cons
           const double t = bt - last_t;
           last_t = bt;
           const dvec3 pb = rtm::ray_at(rp, rd, st_t) - rd * RTX_EPS_BACKUP;
-          const Resolved R = resolve_hit(S, pb, sdir, bobj, bsub, nullptr, nullptr);
+          const HitRef R = resolve_hit(S, pb, sdir, bobj, bsub, nullptr, nullptr);
           const bool is_inside = rtm::dot(R.N, sdir) > 0;
           wpos = rtm::ray_at(wpos, sdir, t);
           bool limit = false;  // sattnLimitCheck with the relative t (U14)
@@ -596,12 +645,12 @@ __device__ __forceinline__ void advance_lane(LaneRef& L, const DevScene& S, cons
           if (limit) {
             done = true;
           } else {
-            const bool next_trans = is_inside ? true : ((R.m.flags & RTX_MF_TRANS) != 0);
+            const bool next_trans = is_inside ? true : ((hit_flags(S, R) & RTX_MF_TRANS) != 0);
             if (!next_trans || (aterm > 0.0 && rtm::dot(sattn, sattn) < aterm * aterm)) {
               result = mk3(0.0, 0.0, 0.0);
               done = true;
             } else {
-              const dvec3 kt = is_inside ? R.m.kt : mk3(1.0, 1.0, 1.0);
+              const dvec3 kt = is_inside ? hit_param(S, R, RTX_P_KT) : mk3(1.0, 1.0, 1.0);
               sattn *= rtm::pow3(kt, t);
               qmode = Q_NEXT;
               qtp = bt;
