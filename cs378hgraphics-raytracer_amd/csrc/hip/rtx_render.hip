@@ -26,6 +26,7 @@
 #include <cstdio>
 #include <cstring>
 #include <string>
+#include <type_traits>
 #include <vector>
 
 #include "rtx_device.h"
@@ -70,6 +71,12 @@ struct FrameParams {
   int64_t n_items;           // work items (pixel blocks)
   int64_t n_samples;         // n_items * ppw * spp  (sample ids)
   int qchunk;                // samples per queue atomic (multiple of 64)
+  // wavefront path: slots are numbered (group, band, local); band b owns
+  // samples [b * wf_band_n, (b+1) * wf_band_n) (see slot_sample)
+  int wf_gb;                 // slots per (group, band), a multiple of WG
+  int wf_nb;                 // bands
+  int wf_band_slots;         // slots per band over all groups
+  int64_t wf_band_n;         // samples per band
 };
 
 // Work item -> pixel; out_index is the output slot (packed tile order or
@@ -247,6 +254,26 @@ __device__ __forceinline__ double light_dist_atten(const RtxLight& L, const dvec
   if (L.type == RTX_LIGHT_DIRECTIONAL) return 1.0;  // light.cpp:56
   const double d = rtm::distance(ld3(L.pos), P);    // light.cpp:61-64 (float terms promoted)
   return rtm::gclamp(1.0 / (L.atten[0] + L.atten[1] * d + L.atten[2] * d * d), 0.0, 1.0);
+}
+
+// Bounds of a shadow walk's next-hit query (DESIGN.md "Shadow walk"):
+//   tlim: hits past it cannot change the walk's result.  For a point light
+//     the U14 limit check trips past the light, and for the walk's FIRST hit
+//     already past half the light distance (the double advance puts its
+//     check point at twice the hit distance, light.cpp:38,66).
+//   tblk: below it the point-light limit check cannot trip, so a blocker
+//     there ends the walk with 0 (directional lights never trip it).
+__device__ __forceinline__ void shadow_bounds(const DevScene& S, const RtxLight& L, const dvec3& qP, bool first,
+                                              double& tlim, double& tblk) {
+  tlim = RTX_INF;
+  tblk = -RTX_INF;
+  if (L.type == RTX_LIGHT_POINT) {
+    const double dl = rtm::distance(qP, ld3(L.pos));
+    tlim = (first ? 0.5 * dl : dl) * (1.0 + 1e-6) + S.margin;
+    tblk = 0.5 * dl * (1.0 - 1e-6) - S.margin;
+  } else if (L.type == RTX_LIGHT_DIRECTIONAL) {
+    tblk = RTX_INF;
+  }
 }
 
 // ============================================================ lane state machine
@@ -623,6 +650,9 @@ __device__ __forceinline__ void advance_lane(LaneRef& L, const DevScene& S, cons
         dvec3 result = sattn;
         if (!bhave) {
           done = true;
+        } else if (bhave == 2) {  // a blocker below tblock (trace_kernel's shadow early-out)
+          result = mk3(0.0, 0.0, 0.0);
+          done = true;
         } else {
           const double t = bt - last_t;
           last_t = bt;
@@ -948,9 +978,8 @@ __global__ void __launch_bounds__(WG) render_kernel(DevScene S, const FrameParam
       if (qmode == Q_NEXT) {
         qP = rtm::ray_at(rp, rd, st_t) - rd * RTX_EPS_BACKUP;
         qD = sdir;
-        const RtxLight& L = S.lights[li];
-        // any hit past a point light trips the limit check
-        if (L.type == RTX_LIGHT_POINT) qlim = rtm::distance(qP, ld3(L.pos)) * (1.0 + 1e-6) + S.margin;
+        double qblk;
+        shadow_bounds(S, S.lights[li], qP, qrp < 0, qlim, qblk);
       }
       bhave = traverse<STATS>(S, qmode, qP, qD, qtp, qrp, qsq, qlim, bt, bobj, bsub, stk, lane, C);
     }
@@ -970,32 +999,65 @@ __global__ void __launch_bounds__(WG) render_kernel(DevScene S, const FrameParam
 // Path slots: NSLOT lanes whose LaneRef state lives in HBM.  Each iteration:
 //   advance_kernel  — one thread per slot: take the last query's result, run
 //                     the state machine to the next ray query, append it to
-//                     the closest-hit or next-hit list (wave ballot + popc +
-//                     one atomic per wave, mbcnt for the offset: compaction
-//                     of the active-ray mask);
-//   trace_kernel<Q> — one thread per compacted query: traverse, write the
-//                     result into the slot's state.
-// Samples are dealt to slots statically (sample slot + k * NSLOT).
+//                     its band's closest-hit or next-hit list (wave ballot +
+//                     popc + one atomic per wave, mbcnt for the offset:
+//                     compaction of the active-ray mask);
+//   trace_kernel<Q> — persistent traversal of the compacted lists; a lane
+//                     whose query ended takes the next one at once, results
+//                     go into the slots' state.
+// XCD affinity: the frame's samples are cut into wf_nb contiguous bands
+// (horizontal strips of the image, or runs of tiles), each with its own
+// slots and its own query sub-lists.  A trace wave drains the band numbered
+// like its XCD (HW_REG_XCC_ID) first and only then helps the others, so an
+// XCD's 4 MB L2 holds the nodes and faces one strip touches instead of the
+// whole scene's.
 struct QList {
   int* slot;    // [cap]
-  double* d;    // Px Py Pz Dx Dy Dz tp tlimit, field-major [8][cap]
+  double* d;    // Px Py Pz Dx Dy Dz tp tlimit tblock, field-major [QL_D][cap]
   int* iv;      // rp, sq  [2][cap]
-  size_t cap;
+  size_t cap;   // band b's sub-list is [b * wf_gb, (b+1) * wf_gb)
 };
+#define QL_D 9
+#define MAX_BANDS 8
+// per-group counters (unsigned ints): [m * MAX_BANDS + b] queries of mode
+// m (0 closest, 1 next) in band b; [CNT_ALIVE] live slots;
+// [CNT_CLAIM + m * MAX_BANDS + b] the trace kernel's claim cursors
+#define CNT_ALIVE 16
+#define CNT_CLAIM 32
+#define CNT_PER_GROUP 64
 
 __device__ __forceinline__ unsigned int lane_prefix(unsigned long long mask) {
   return __builtin_amdgcn_mbcnt_hi(static_cast<unsigned int>(mask >> 32),
                                    __builtin_amdgcn_mbcnt_lo(static_cast<unsigned int>(mask), 0u));
 }
 
+// XCD (XCC) of the executing wave, 0..7 — for L2 affinity only, never for
+// correctness (placement is not part of the HIP contract).
+__device__ __forceinline__ int xcc_id() {
+  unsigned int v;
+  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(v));
+  return static_cast<int>(v & 7u);
+}
+
+// Sample id of a slot's kdone-th claim.  Slots are numbered (group, band,
+// local); band b deals its samples round-robin over its wf_band_slots slots.
+__device__ __forceinline__ int64_t slot_sample(const FrameParams& F, int slot, int kdone, int64_t& band_end) {
+  const int gslots = F.wf_gb * F.wf_nb;
+  const int g = slot / gslots, r = slot - g * gslots;
+  const int b = r / F.wf_gb, ls = r - b * F.wf_gb;
+  const int64_t start = static_cast<int64_t>(b) * F.wf_band_n;
+  band_end = start + F.wf_band_n < F.n_samples ? start + F.wf_band_n : F.n_samples;
+  return start + static_cast<int64_t>(g) * F.wf_gb + ls + static_cast<int64_t>(kdone) * F.wf_band_slots;
+}
+
 // Claim the next statically dealt sample for an idle slot (what the
 // scheduler of the megakernel does with its queue).
-__device__ __forceinline__ void claim_sample(LaneRef& L, const FrameParams& F, RtxHitRecord* hits, int slot,
-                                             int nslot) {
+__device__ __forceinline__ void claim_sample(LaneRef& L, const FrameParams& F, RtxHitRecord* hits, int slot) {
   const RtxRenderParams& P = F.P;
   while (L.st == ST_IDLE) {
-    const int64_t sid = static_cast<int64_t>(slot) + static_cast<int64_t>(L.kdone) * nslot;
-    if (sid >= F.n_samples) return;
+    int64_t band_end;
+    const int64_t sid = slot_sample(F, slot, L.kdone, band_end);
+    if (sid >= band_end) return;
     L.kdone++;
     const int64_t item = sid / (F.ppw * F.spp);
     const int sl = static_cast<int>(sid % (F.ppw * F.spp));
@@ -1030,16 +1092,18 @@ __global__ void __launch_bounds__(WG, RTX_ADV_WAVES) advance_kernel(DevScene S, 
                                                       unsigned int* __restrict__ counters,
                                                       unsigned long long* __restrict__ stats, int slot_off) {
   const FrameParams& F = *Fp;
-  const int nslot = static_cast<int>(lm.n);
-  const int slot = slot_off + blockIdx.x * WG + threadIdx.x;  // the grid covers this group's slots exactly
+  const int local = blockIdx.x * WG + threadIdx.x;  // the grid covers this group's slots exactly
+  const int slot = slot_off + local;
+  const int band = local / F.wf_gb;                 // wf_gb is a multiple of WG: one band per workgroup
   Counters C = {0, 0, 0, 0, 0, 0, 0};
   LaneRef L(lm, static_cast<size_t>(slot));
   int qm = Q_NONE;
-  if (L.st != ST_IDLE || static_cast<int64_t>(slot) + static_cast<int64_t>(L.kdone) * nslot < F.n_samples) {
+  int64_t band_end;
+  if (L.st != ST_IDLE || slot_sample(F, slot, L.kdone, band_end) < band_end) {
     // the previous iteration's query result is already in L.bt/bobj/bsub/bhave
     L.qmode = Q_NONE;
     for (;;) {
-      claim_sample(L, F, hits, slot, nslot);
+      claim_sample(L, F, hits, slot);
       if (L.st == ST_IDLE) break;
       advance_lane<STATS, false>(L, S, F, C, sbuf, nullptr, hits, 0, 0, pbuf, lm.n, static_cast<size_t>(slot),
                                  pend_cap);
@@ -1054,21 +1118,21 @@ __global__ void __launch_bounds__(WG, RTX_ADV_WAVES) advance_kernel(DevScene S, 
     const unsigned long long mask = __ballot(qm == m);
     if (mask == 0ull) continue;
     unsigned int base = 0;
-    if (lane == 0) base = atomicAdd(&counters[m - 1], static_cast<unsigned int>(__popcll(mask)));
+    if (lane == 0)
+      base = atomicAdd(&counters[(m - 1) * MAX_BANDS + band], static_cast<unsigned int>(__popcll(mask)));
     base = __shfl(base, 0);
     if (qm == m) {
       const QList& Q = m == Q_CLOSEST ? q0 : q1;
       const size_t cap = Q.cap;
-      const unsigned int k = base + lane_prefix(mask);
+      const size_t k = static_cast<size_t>(band) * F.wf_gb + base + lane_prefix(mask);
       dvec3 qP = L.rp, qD = L.rd;
-      double qlim = RTX_INF;
+      double qlim = RTX_INF, qblk = -RTX_INF;
       if (m == Q_NEXT) {
         qP = rtm::ray_at(L.rp, L.rd, L.st_t) - L.rd * RTX_EPS_BACKUP;
         qD = L.sdir;
-        const RtxLight& Lt = S.lights[L.li];
-        // any hit past a point light trips the limit check
-        if (Lt.type == RTX_LIGHT_POINT) qlim = rtm::distance(qP, ld3(Lt.pos)) * (1.0 + 1e-6) + S.margin;
+        shadow_bounds(S, S.lights[L.li], qP, L.qrp < 0, qlim, qblk);
       }
+      Q.d[8 * cap + k] = qblk;
       Q.slot[k] = slot;
       Q.d[0 * cap + k] = qP.x;
       Q.d[1 * cap + k] = qP.y;
@@ -1083,7 +1147,7 @@ __global__ void __launch_bounds__(WG, RTX_ADV_WAVES) advance_kernel(DevScene S, 
     }
   }
   const unsigned long long alive = __ballot(L.st != ST_IDLE);
-  if (lane == 0 && alive) atomicAdd(&counters[2], static_cast<unsigned int>(__popcll(alive)));
+  if (lane == 0 && alive) atomicAdd(&counters[CNT_ALIVE], static_cast<unsigned int>(__popcll(alive)));
   if (STATS) {
     int64_t v[7] = {C.camera, C.secondary, C.shadow, C.nodes, C.objects, C.tris, C.shades};
 #pragma unroll
@@ -1095,31 +1159,123 @@ __global__ void __launch_bounds__(WG, RTX_ADV_WAVES) advance_kernel(DevScene S, 
   }
 }
 
+// Blocker of the shadow early-out (rtx_traverse.h): hit (oi, sb) of the
+// lane's query is entered from outside (N.dir <= 0) an opaque material —
+// the walk's own resolve_hit normal and flags (ST_WALK).  Out of line: run
+// about once per shadow query, and resolve_hit's registers must not raise
+// the traversal loop's peak.  Opt-in (-DRTX_EARLYOUT): it saves 5% of the
+// traversal work on the headline frame but the call (scratch frame, saved
+// registers) cost more than that (205 vs 185 ms/frame).
+__device__ __noinline__ bool shadow_blocks(const DevScene* __restrict__ Sg, const dvec3 P, const dvec3 D, int oi,
+                                           int sb) {
+  const DevScene& S = *Sg;
+  const RtxObject& o = S.objs[oi];
+  const bool vmats = o.type == RTX_OBJ_TRIMESH && S.meshes[o.mesh].has_vmats;  // flags 0 (decision U2)
+  if (!vmats && (S.mats[o.material].flags & RTX_MF_TRANS)) return false;
+  const HitRef R = resolve_hit(S, P, D, oi, sb, nullptr, nullptr);
+  return !(rtm::dot(R.N, D) > 0);
+}
+
+struct ShadowBlocker {
+  const DevScene* Sg;
+  __device__ explicit ShadowBlocker(const DevScene* s) : Sg(s) {}
+  __device__ bool operator()(const Trav& T, int oi, int sb) const { return shadow_blocks(Sg, T.P, T.D, oi, sb); }
+};
+
+// Refill a wave's idle lanes once fewer than RTX_REFILL are still
+// traversing.  Measured on the headline frame (ms/frame): 1 -> 182, 16 -> 197,
+// 40 -> 205, 56 -> 220: mixing a new query into a wave whose other lanes are
+// deep in the tree costs more (divergent nodes and modes) than the idle lanes
+// waste, so by default a wave claims its next 64 queries only when all of its
+// lanes are done (the claims still balance waves against each other).
+#ifndef RTX_REFILL
+#define RTX_REFILL 1
+#endif
+
+// Persistent traversal of one group's compacted query lists.  A wave claims
+// 64 queries at a time (one atomic) from its XCD's band, then from the other
+// bands; inside the wave, lanes whose query ended take the next ones of the
+// claim (ballot + mbcnt) while the others keep stepping, so a wave's time
+// follows its total work rather than its slowest ray.
 template <bool STATS, int MODE>
-__global__ void __launch_bounds__(WG, RTX_TRACE_WAVES) trace_kernel(DevScene S, QList Q, const unsigned int* __restrict__ counters,
-                                                    LaneMem lm, int stack_cap, unsigned long long* __restrict__ stats) {
+__global__ void __launch_bounds__(WG, RTX_TRACE_WAVES)
+    trace_kernel(DevScene S, const DevScene* __restrict__ Sg, QList Q, unsigned int* __restrict__ counters, int gb,
+                 int nbands, LaneMem lm, int stack_cap, unsigned long long* __restrict__ stats) {
   extern __shared__ int lds_stack[];
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   int* stk = lds_stack + wave * stack_cap * 64;
-  const unsigned int n = counters[MODE - 1];
   const size_t cap = Q.cap;
+  const unsigned int* n_band = counters + (MODE - 1) * MAX_BANDS;
+  unsigned int* claim = counters + CNT_CLAIM + (MODE - 1) * MAX_BANDS;
+  const int b0 = xcc_id() % nbands;
+#ifdef RTX_EARLYOUT
+  using Blk = typename std::conditional<MODE == Q_NEXT, ShadowBlocker, NoBlocker>::type;
+#else
+  using Blk = NoBlocker;
+#endif
+  const Blk blk(Sg);
   Counters C = {0, 0, 0, 0, 0, 0, 0};
-  for (unsigned int k = blockIdx.x * WG + threadIdx.x; k < ((n + 63u) & ~63u); k += gridDim.x * WG) {
-    if (k < n) {
-      const dvec3 P = mk3(Q.d[0 * cap + k], Q.d[1 * cap + k], Q.d[2 * cap + k]);
-      const dvec3 D = mk3(Q.d[3 * cap + k], Q.d[4 * cap + k], Q.d[5 * cap + k]);
-      const double tp = Q.d[6 * cap + k], tlim = Q.d[7 * cap + k];
-      const int rp = Q.iv[0 * cap + k], sq = Q.iv[1 * cap + k];
-      double bt;
-      int bobj, bsub;
-      const bool have = traverse<STATS>(S, MODE, P, D, tp, rp, sq, tlim, bt, bobj, bsub, stk, lane, C);
-      const size_t slot = static_cast<size_t>(Q.slot[k]);
-      lm.d[size_t(LD_bt) * lm.n + slot] = bt;
-      lm.i[size_t(LI_bobj) * lm.n + slot] = bobj;
-      lm.i[size_t(LI_bsub) * lm.n + slot] = bsub;
-      lm.i[size_t(LI_bhave) * lm.n + slot] = have ? 1 : 0;
+  Trav T;
+  bool active = false;
+  size_t kq = 0;
+  // wave-uniform claim state: [qnext, qend) of band qb's sub-list
+  unsigned int qnext = 0, qend = 0;
+  int qb = 0, bi = 0;
+  bool exhausted = false;
+  auto finish = [&]() {
+    const size_t slot = static_cast<size_t>(Q.slot[kq]);
+    lm.d[size_t(LD_bt) * lm.n + slot] = T.bt;
+    lm.i[size_t(LI_bobj) * lm.n + slot] = T.bobj;
+    lm.i[size_t(LI_bsub) * lm.n + slot] = T.bsub;
+    lm.i[size_t(LI_bhave) * lm.n + slot] = T.blocked ? 2 : (T.have ? 1 : 0);
+  };
+  for (;;) {
+    unsigned long long idle = __ballot(!active);
+    while (idle != 0ull && !exhausted) {
+      if (qnext >= qend) {
+        for (;;) {  // claim: this XCD's band first, then help the others
+          if (bi >= nbands) {
+            exhausted = true;
+            break;
+          }
+          qb = (b0 + bi) % nbands;
+          const unsigned int nq = n_band[qb];
+          unsigned int base = nq;
+          if (lane == 0 && nq > 0) base = atomicAdd(&claim[qb], 64u);
+          base = __shfl(base, 0);
+          if (base < nq) {
+            qnext = base;
+            qend = base + 64u < nq ? base + 64u : nq;
+            break;
+          }
+          ++bi;
+        }
+        if (exhausted) break;
+      }
+      const unsigned int rank = lane_prefix(idle);
+      const unsigned int avail = qend - qnext;
+      const unsigned int nidle = __popcll(idle);
+      const unsigned int take = avail < nidle ? avail : nidle;
+      if (!active && rank < take) {
+        kq = static_cast<size_t>(qb) * gb + qnext + rank;
+        const dvec3 P = mk3(Q.d[0 * cap + kq], Q.d[1 * cap + kq], Q.d[2 * cap + kq]);
+        const dvec3 D = mk3(Q.d[3 * cap + kq], Q.d[4 * cap + kq], Q.d[5 * cap + kq]);
+        active = trav_init<STATS>(T, S, MODE, P, D, Q.d[6 * cap + kq], Q.iv[0 * cap + kq], Q.iv[1 * cap + kq],
+                                  Q.d[7 * cap + kq], MODE == Q_NEXT ? Q.d[8 * cap + kq] : -RTX_INF, C);
+        if (!active) finish();
+      }
+      qnext += take;
+      idle = __ballot(!active);
     }
+    if (__ballot(active) == 0ull) break;  // nothing claimed and nothing left
+    const int thresh = exhausted ? 1 : RTX_REFILL;
+    do {
+      if (active && trav_step<STATS>(T, S, stk, lane, blk, C)) {
+        finish();
+        active = false;
+      }
+    } while (static_cast<int>(__popcll(__ballot(active))) >= thresh);
   }
   if (STATS) {
     int64_t v[3] = {C.nodes, C.objects, C.tris};
@@ -1212,6 +1368,7 @@ struct SceneState {
   hipEvent_t wf_fork = nullptr;
   unsigned int* d_counters = nullptr;
   unsigned int* h_counters = nullptr;  // pinned
+  DevScene* d_scene = nullptr;         // device copy of S_launch (shadow early-out)
   std::vector<hipEvent_t> ev_pool;
   size_t ev_used = 0;
   std::vector<hipEvent_t> ev_start, ev_stop;
@@ -1400,6 +1557,7 @@ rtx_status rtx_scene_destroy(void* scene) {
   for (auto q : st->wf_streams) (void)hipStreamDestroy(q);
   if (st->d_counters) (void)hipFree(st->d_counters);
   if (st->h_counters) (void)hipHostFree(st->h_counters);
+  if (st->d_scene) (void)hipFree(st->d_scene);
   for (auto e : st->ev_pool) (void)hipEventDestroy(e);
   for (auto e : st->ev_start) (void)hipEventDestroy(e);
   for (auto e : st->ev_stop) (void)hipEventDestroy(e);
@@ -1670,14 +1828,26 @@ rtx_status rtx_render(void* scene, const RtxRenderParams* params, uint8_t* rgb8,
     const char* g_env = getenv("RTX_GROUPS");
     if (g_env && atoi(g_env) > 0) G = atoi(g_env);
     if (G > 16) G = 16;
+    // XCD-affine bands: off by default (1).  With 8 bands the headline frame
+    // took 218 ms instead of 182: each band's slots walk only that strip's
+    // samples, so the costliest strip sets the iteration count.
+    int NB = 1;
+    const char* b_env = getenv("RTX_BANDS");
+    if (b_env && atoi(b_env) > 0) NB = atoi(b_env);
+    if (NB > MAX_BANDS) NB = MAX_BANDS;
     if (nslot64 > F.n_samples) nslot64 = F.n_samples;
-    const int64_t per = (nslot64 + G * WG - 1) / (G * WG);  // workgroups per group
-    const int64_t gslots = per * WG;
+    const int64_t unit = static_cast<int64_t>(G) * NB * WG;
+    const int64_t gb = (nslot64 + unit - 1) / unit * WG;  // slots per (group, band)
+    const int64_t gslots = gb * NB;
+    const int64_t per = gslots / WG;                      // workgroups per group
     nslot64 = gslots * G;
+    F.wf_gb = static_cast<int>(gb);
+    F.wf_nb = NB;
+    F.wf_band_slots = static_cast<int>(gb * G);
+    F.wf_band_n = (F.n_samples + NB - 1) / NB;
     const size_t ns = static_cast<size_t>(nslot64);
-    const int nslot = static_cast<int>(nslot64);
     const size_t gs = static_cast<size_t>(gslots);
-    const size_t bytes_q = gs * (sizeof(int) + 8 * sizeof(double) + 2 * sizeof(int)) + 1024;
+    const size_t bytes_q = gs * (sizeof(int) + QL_D * sizeof(double) + 2 * sizeof(int)) + 1024;
     auto al = [](size_t x) { return (x + 255) & ~size_t(255); };
     if ((rc = ensure(&st->d_wf, &st->wf_bytes, size_t(G) * 2 * al(bytes_q))) != RTX_OK) return rc;
     if ((rc = ensure(&st->d_lane, &st->lane_bytes, lane_mem_bytes(ns))) != RTX_OK) return rc;
@@ -1685,8 +1855,10 @@ rtx_status rtx_render(void* scene, const RtxRenderParams* params, uint8_t* rgb8,
     if ((rc = ensure(reinterpret_cast<void**>(&st->d_pbuf), &st->pbuf_bytes,
                      ns * pend_cap * 13 * sizeof(double))) != RTX_OK)
       return rc;
-    if (!st->d_counters) HIP_TRY(hipMalloc(&st->d_counters, 16 * 4 * sizeof(unsigned int)));
-    if (!st->h_counters) HIP_TRY(hipHostMalloc(&st->h_counters, 16 * 4 * sizeof(unsigned int)));
+    if (!st->d_counters) HIP_TRY(hipMalloc(&st->d_counters, 16 * CNT_PER_GROUP * sizeof(unsigned int)));
+    if (!st->h_counters) HIP_TRY(hipHostMalloc(&st->h_counters, 16 * CNT_PER_GROUP * sizeof(unsigned int)));
+    if (!st->d_scene) HIP_TRY(hipMalloc(&st->d_scene, sizeof(DevScene)));
+    HIP_TRY(hipMemcpyAsync(st->d_scene, &st->S_launch, sizeof(DevScene), hipMemcpyHostToDevice, stream));
     // group 0 runs on the caller's stream, groups 1.. on their own streams
     // (GPU_MAX_HW_QUEUES is 4 by default: more streams than queues would
     // serialize groups behind each other)
@@ -1707,7 +1879,7 @@ rtx_status rtx_render(void* scene, const RtxRenderParams* params, uint8_t* rgb8,
       for (size_t m = 0; m < ql.size(); ++m) {
         ql[m].slot = reinterpret_cast<int*>(base);
         ql[m].d = reinterpret_cast<double*>(base + al(gs * sizeof(int)));
-        ql[m].iv = reinterpret_cast<int*>(base + al(gs * sizeof(int)) + al(gs * 8 * sizeof(double)));
+        ql[m].iv = reinterpret_cast<int*>(base + al(gs * sizeof(int)) + al(gs * QL_D * sizeof(double)));
         ql[m].cap = gs;
         base += al(bytes_q);
       }
@@ -1716,7 +1888,7 @@ rtx_status rtx_render(void* scene, const RtxRenderParams* params, uint8_t* rgb8,
     HIP_TRY(hipMemcpyAsync(st->d_frame, &F, sizeof(FrameParams), hipMemcpyHostToDevice, stream));
     // every slot ST_IDLE, kdone = 0, no pending query
     HIP_TRY(hipMemsetAsync(A.i, 0, ns * LI_COUNT * sizeof(int), stream));
-    HIP_TRY(hipMemsetAsync(st->d_counters, 0, 16 * 4 * sizeof(unsigned int), stream));
+    HIP_TRY(hipMemsetAsync(st->d_counters, 0, 16 * CNT_PER_GROUP * sizeof(unsigned int), stream));
     const size_t lds = size_t(st->stack_cap) * 64 * sizeof(int) * WAVES_PER_WG;
     if (lds > 160 * 1024) {
       g_err = "rtx_render: LDS budget exceeded (BVH too deep)";
@@ -1744,10 +1916,11 @@ rtx_status rtx_render(void* scene, const RtxRenderParams* params, uint8_t* rgb8,
       for (int g = 0; g < G; ++g) {
         if (done[size_t(g)]) continue;
         hipStream_t sg = g == 0 ? stream : st->wf_streams[size_t(g)];
-        unsigned int* cnt = st->d_counters + 4 * g;
+        unsigned int* cnt = st->d_counters + CNT_PER_GROUP * g;
         const QList& q0 = ql[size_t(g) * 2];
         const QList& q1 = ql[size_t(g) * 2 + 1];
-        HIP_TRY(hipMemsetAsync(cnt, 0, 3 * sizeof(unsigned int), sg));
+        const int gbi = static_cast<int>(gb);
+        HIP_TRY(hipMemsetAsync(cnt, 0, CNT_PER_GROUP * sizeof(unsigned int), sg));
         if (stats)
           hipLaunchKernelGGL((advance_kernel<true>), dim3(per), dim3(WG), 0, sg, S, st->d_frame, A, sb, d_hits,
                              st->d_pbuf, pend_cap, q0, q1, cnt, st->d_stats, static_cast<int>(g * gslots));
@@ -1755,15 +1928,15 @@ rtx_status rtx_render(void* scene, const RtxRenderParams* params, uint8_t* rgb8,
           hipLaunchKernelGGL((advance_kernel<false>), dim3(per), dim3(WG), 0, sg, S, st->d_frame, A, sb, d_hits,
                              st->d_pbuf, pend_cap, q0, q1, cnt, st->d_stats, static_cast<int>(g * gslots));
         if (stats) {
-          hipLaunchKernelGGL((trace_kernel<true, Q_CLOSEST>), dim3(tgrid), dim3(WG), lds, sg, S, q0, cnt, A,
-                             st->stack_cap, st->d_stats);
-          hipLaunchKernelGGL((trace_kernel<true, Q_NEXT>), dim3(tgrid), dim3(WG), lds, sg, S, q1, cnt, A,
-                             st->stack_cap, st->d_stats);
+          hipLaunchKernelGGL((trace_kernel<true, Q_CLOSEST>), dim3(tgrid), dim3(WG), lds, sg, S, st->d_scene, q0,
+                             cnt, gbi, NB, A, st->stack_cap, st->d_stats);
+          hipLaunchKernelGGL((trace_kernel<true, Q_NEXT>), dim3(tgrid), dim3(WG), lds, sg, S, st->d_scene, q1, cnt,
+                             gbi, NB, A, st->stack_cap, st->d_stats);
         } else {
-          hipLaunchKernelGGL((trace_kernel<false, Q_CLOSEST>), dim3(tgrid), dim3(WG), lds, sg, S, q0, cnt, A,
-                             st->stack_cap, st->d_stats);
-          hipLaunchKernelGGL((trace_kernel<false, Q_NEXT>), dim3(tgrid), dim3(WG), lds, sg, S, q1, cnt, A,
-                             st->stack_cap, st->d_stats);
+          hipLaunchKernelGGL((trace_kernel<false, Q_CLOSEST>), dim3(tgrid), dim3(WG), lds, sg, S, st->d_scene, q0,
+                             cnt, gbi, NB, A, st->stack_cap, st->d_stats);
+          hipLaunchKernelGGL((trace_kernel<false, Q_NEXT>), dim3(tgrid), dim3(WG), lds, sg, S, st->d_scene, q1, cnt,
+                             gbi, NB, A, st->stack_cap, st->d_stats);
         }
         HIP_TRY(hipGetLastError());
         if (it % check_every == check_every - 1) {
@@ -1772,10 +1945,17 @@ rtx_status rtx_render(void* scene, const RtxRenderParams* params, uint8_t* rgb8,
           // iterations of this group queued meanwhile)
           if (pending_check[size_t(g)] >= 0) {
             HIP_TRY(hipEventSynchronize(st->wf_check[size_t(g)]));
-            const unsigned int alive = st->h_counters[4 * g + 2];
-            if (dbg)
+            const unsigned int* hc = st->h_counters + CNT_PER_GROUP * g;
+            const unsigned int alive = hc[CNT_ALIVE];
+            if (dbg) {
+              unsigned int nc = 0, nn = 0;
+              for (int b = 0; b < NB; ++b) {
+                nc += hc[b];
+                nn += hc[MAX_BANDS + b];
+              }
               fprintf(stderr, "rtx group %d iter %d: alive %u (closest %u next %u)\n", g, pending_check[size_t(g)],
-                      alive, st->h_counters[4 * g + 0], st->h_counters[4 * g + 1]);
+                      alive, nc, nn);
+            }
             if (alive == 0) {
               done[size_t(g)] = 1;
               ++ndone;
@@ -1783,7 +1963,8 @@ rtx_status rtx_render(void* scene, const RtxRenderParams* params, uint8_t* rgb8,
               continue;
             }
           }
-          HIP_TRY(hipMemcpyAsync(st->h_counters + 4 * g, cnt, 3 * sizeof(unsigned int), hipMemcpyDeviceToHost, sg));
+          HIP_TRY(hipMemcpyAsync(st->h_counters + CNT_PER_GROUP * g, cnt, CNT_PER_GROUP * sizeof(unsigned int),
+                                 hipMemcpyDeviceToHost, sg));
           HIP_TRY(hipEventRecord(st->wf_check[size_t(g)], sg));
           pending_check[size_t(g)] = it;
         }
