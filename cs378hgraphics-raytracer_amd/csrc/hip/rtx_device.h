@@ -33,29 +33,37 @@ using rtm::mk3;
 #define RTX_INF 1.0e308
 #define RTX_MAX_LIGHTS 64
 
-// Device BVH layout (built from the RtxNode arrays by rtx_scene_create).
-// One record per INTERNAL node holding both children's boxes, so a visit is
-// one 128-byte fetch that tests both children and descends into the nearer
-// one first.  child[k] >= 0: index of the child's record; child[k] < 0: the
-// child is a leaf, ~child[k] = first_item << 2 | count (count 1..3,
-// kdTree.h:6).  Item ranks (DFS-leaf order) are unchanged, so the winner of
-// the lexicographic (t, rank) minimum does not depend on the visiting order.
-struct DevNode2 {
-  double box[12];      // lo0 xyz, hi0 xyz, lo1 xyz, hi1 xyz
-  int32_t child[2];
-  int32_t pad[6];
-};                     // 128 bytes
+// Device BVH layout (built from the RtxNode arrays by rtx_scene_create): the
+// reference's binary KdTree collapsed to 4-wide records.  A record stands
+// for one internal node and holds the boxes of its children, where an
+// internal child is replaced by ITS two children (so 2..4 entries): one
+// 256-byte fetch tests up to four boxes and the walk needs half as many
+// dependent fetches as on the binary tree.  Skipping the intermediate box is
+// exact: node boxes are merges of their children's (kdTree.h:30-39), and the
+// slab test (bbox.cc:33-70) is monotone under box containment in floating
+// point too (per axis, (lo - o) / d rounds monotonically), so a child box is
+// only ever hit when its parent's is.  child[k] >= 0: index of the child's
+// record; child[k] < 0: the child is a leaf, ~child[k] = first_item << 2 |
+// count (count 1..3, kdTree.h:6).  Item ranks (DFS-leaf order) are
+// unchanged, so the winner of the lexicographic (t, rank) minimum does not
+// depend on the visiting order.
+struct DevNode4 {
+  double box[4][6];    // per entry: lo xyz, hi xyz
+  int32_t child[4];
+  int32_t count;       // entries, 2..4
+  int32_t pad[11];
+};                     // 256 bytes
 
 // Root of a BVH (scene or one mesh): its own box + the reference to descend.
 struct DevRoot {
   double lo[3], hi[3];
-  int32_t ref;         // >= 0: DevNode2 index; < 0: the root is a leaf (~code)
+  int32_t ref;         // >= 0: DevNode4 index; < 0: the root is a leaf (~code)
   int32_t pad[3];
 };                     // 64 bytes
 
 struct DevScene {
-  const DevNode2* snode2;  // scene BVH, internal nodes
-  const DevNode2* mnode2;  // all mesh BVHs, internal nodes (global indices)
+  const DevNode4* snode4;  // scene BVH records
+  const DevNode4* mnode4;  // all mesh BVHs' records (global indices)
   const DevRoot* mroots;   // per mesh (valid when meshes[m].node_count > 0)
   DevRoot sroot;           // scene BVH root
   const RtxNode* snodes;

@@ -1494,25 +1494,30 @@ rtx_status rtx_scene_create(int device, const RtxSceneDesc* d, void** out) {
   UP(d->texels, d->n_texels, S.texels);
 #undef UP
   {
-    std::vector<DevNode2> sn2, mn2;
+    std::vector<DevNode4> sn4, mn4;
     std::vector<DevRoot> mroots(size_t(d->n_meshes));
     bool ok = true;
+    int sneed = 0, mneed = 0;
     std::memset(&S.sroot, 0, sizeof(S.sroot));
-    if (d->n_scene_nodes > 0) ok = build_node2(d->scene_nodes, d->n_scene_nodes, sn2, S.sroot);
+    if (d->n_scene_nodes > 0) ok = build_node4(d->scene_nodes, d->n_scene_nodes, sn4, S.sroot, sneed);
     for (int m = 0; ok && m < d->n_meshes; ++m) {
       const RtxMesh& me = d->meshes[m];
       std::memset(&mroots[size_t(m)], 0, sizeof(DevRoot));
-      if (me.node_count > 0) ok = build_node2(d->mesh_nodes + me.node_off, me.node_count, mn2, mroots[size_t(m)]);
+      int need = 0;
+      if (me.node_count > 0) ok = build_node4(d->mesh_nodes + me.node_off, me.node_count, mn4, mroots[size_t(m)], need);
+      mneed = need > mneed ? need : mneed;
     }
     if (!ok) {
       g_err = "rtx_scene_create: malformed BVH (leaf with more than 3 items or bad child link)";
       rtx_scene_destroy(st);
       return RTX_ERR_INVALID;
     }
+    // per-lane LDS stack: scene-level entries stay below a mesh walk's
+    st->stack_cap = sneed + mneed + 2;
 #define UP(src, n, dst) \
   if ((rc = upload(*st, src, size_t(n), &dst)) != RTX_OK) { rtx_scene_destroy(st); return rc; }
-    UP(sn2.data(), sn2.size(), S.snode2);
-    UP(mn2.data(), mn2.size(), S.mnode2);
+    UP(sn4.data(), sn4.size(), S.snode4);
+    UP(mn4.data(), mn4.size(), S.mnode4);
     UP(mroots.data(), mroots.size(), S.mroots);
 #undef UP
   }
@@ -1526,7 +1531,6 @@ rtx_status rtx_scene_create(int device, const RtxSceneDesc* d, void** out) {
   S.air_index = (0.299 * 1.0) + (0.587 * 1.0) + (0.114 * 1.0);
   st->cam = d->camera;
   st->lights.assign(d->lights, d->lights + d->n_lights);
-  st->stack_cap = d->scene_depth + d->mesh_depth + 4;
   if (hipMalloc(&st->d_frame, sizeof(FrameParams)) != hipSuccess ||
       hipMalloc(&st->d_work, sizeof(unsigned long long)) != hipSuccess ||
       hipMalloc(&st->d_stats, 8 * sizeof(unsigned long long)) != hipSuccess) {

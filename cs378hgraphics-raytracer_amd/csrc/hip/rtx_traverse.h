@@ -6,6 +6,7 @@
 
 #include <climits>
 #include <cstring>
+#include <functional>
 #include <vector>
 
 #include "rtx_device.h"
@@ -29,7 +30,7 @@ namespace rtxd {
 // change the answer (margins in DESIGN.md).
 //
 // The loop is cut into units: trav_init, then trav_step until it returns
-// true.  One step is one paired-child BVH record, one object of a leaf, or
+// true.  One step is one 4-wide BVH record, one object of a leaf, or
 // one mesh leaf's faces.  The query's whole state lives in a Trav, so the
 // persistent trace kernel can hand a lane a new query as soon as its own one
 // ends while the other lanes of the wave keep stepping; traverse() runs one
@@ -52,7 +53,7 @@ struct Trav {
   double bt;
   int bobj, bsub;
   bool have, blocked;
-  // walk: ref >= 0 internal DevNode2, ref < 0 leaf ~(first << 2 | count);
+  // walk: ref >= 0 DevNode4 record, ref < 0 leaf ~(first << 2 | count);
   // mode 0 scene BVH, 1 objects [oc, oe) of a scene leaf, 2 mesh BVH
   int sp, ref, mode, oc, oe;
   // mesh context (local frame of object moi)
@@ -69,6 +70,54 @@ struct NoBlocker {
   RT_HD explicit NoBlocker(const void*) {}
   RT_HD bool operator()(const Trav&, int, int) const { return false; }
 };
+
+// Visit one 4-wide record: test its entries' boxes (exact slab verdicts,
+// pruned to [lo, hi]), continue with the nearest entry hit and push the
+// other hits farthest first, so the walk stays near-first.  False if no
+// entry was hit (the caller pops).
+template <bool STATS>
+RT_HD bool visit4(const DevNode4& nd, const dvec3& o, const dvec3& d, const RayInv& ri, const double hi,
+                  const double lo, int* __restrict__ stk, const int lane, int& sp, int& ref, Counters& C) {
+  const double NOHIT = __builtin_inf();
+  double a0 = NOHIT, a1 = NOHIT, a2 = NOHIT, a3 = NOHIT;
+  int r0 = 0, r1 = 0, r2 = 0, r3 = 0;
+  const int cnt = nd.count;
+  auto test = [&](int k, double& ak, int& rk) {
+    if (k < cnt) {
+      if (STATS) C.nodes++;
+      double ta, tb;
+      if (box_test(nd.box[k], nd.box[k] + 3, o, d, ri, ta, tb) && !(ta > hi) && !(tb < lo)) {
+        ak = ta;
+        rk = nd.child[k];
+      }
+    }
+  };
+  test(0, a0, r0);
+  test(1, a1, r1);
+  test(2, a2, r2);
+  test(3, a3, r3);
+  // sorting network on (entry distance, ref)
+  auto cs = [](double& x, int& rx, double& y, int& ry) {
+    const bool s = y < x;
+    const double lo_ = s ? y : x, hi_ = s ? x : y;
+    const int rlo = s ? ry : rx, rhi = s ? rx : ry;
+    x = lo_;
+    y = hi_;
+    rx = rlo;
+    ry = rhi;
+  };
+  cs(a0, r0, a1, r1);
+  cs(a2, r2, a3, r3);
+  cs(a0, r0, a2, r2);
+  cs(a1, r1, a3, r3);
+  cs(a1, r1, a2, r2);
+  if (!(a0 < NOHIT)) return false;
+  if (a3 < NOHIT) stk[(sp++) * 64 + lane] = r3;
+  if (a2 < NOHIT) stk[(sp++) * 64 + lane] = r2;
+  if (a1 < NOHIT) stk[(sp++) * 64 + lane] = r1;
+  ref = r0;
+  return true;
+}
 
 // Start a query; false if it is already complete (empty scene or the root
 // box is missed: KdTree::intersectList starts with the root's bbox test).
@@ -128,25 +177,7 @@ RT_HD bool trav_step(Trav& T, const DevScene& S, int* __restrict__ stk, const in
   int& ref = T.ref;
   if (T.mode == 0) {
     if (ref >= 0) {
-      const DevNode2& nd = S.snode2[ref];
-      if (STATS) C.nodes += 2;
-      double a0, b0, a1, b1;
-      const bool h0 =
-          box_test(nd.box + 0, nd.box + 3, T.P, T.D, T.ri, a0, b0) && !(a0 > bt + S.margin) && !(b0 < tlo);
-      const bool h1 =
-          box_test(nd.box + 6, nd.box + 9, T.P, T.D, T.ri, a1, b1) && !(a1 > bt + S.margin) && !(b1 < tlo);
-      const int c0 = nd.child[0], c1 = nd.child[1];
-      if (h0 && h1) {  // nearer child first; the other waits on the stack
-        const bool swap = a1 < a0;
-        stk[sp * 64 + lane] = swap ? c0 : c1;
-        ++sp;
-        ref = swap ? c1 : c0;
-        return false;
-      }
-      if (h0 || h1) {
-        ref = h0 ? c0 : c1;
-        return false;
-      }
+      if (visit4<STATS>(S.snode4[ref], T.P, T.D, T.ri, bt + S.margin, tlo, stk, lane, sp, ref, C)) return false;
       if (sp == 0) return true;
       --sp;
       ref = stk[sp * 64 + lane];
@@ -322,23 +353,7 @@ RT_HD bool trav_step(Trav& T, const DevScene& S, int* __restrict__ stk, const in
   if (closest && T.mhave) hi = rtm::gmin(hi, T.mbest + S.lmargin);
   const double lo = closest ? -RTX_INF : tlo * len * (1.0 - 1e-12) - S.lmargin;
   if (ref >= 0) {
-    const DevNode2& nd = S.mnode2[ref];
-    if (STATS) C.nodes += 2;
-    double a0, b0, a1, b1;
-    const bool h0 = box_test(nd.box + 0, nd.box + 3, T.lp, T.ld, T.lri, a0, b0) && !(a0 > hi) && !(b0 < lo);
-    const bool h1 = box_test(nd.box + 6, nd.box + 9, T.lp, T.ld, T.lri, a1, b1) && !(a1 > hi) && !(b1 < lo);
-    const int c0 = nd.child[0], c1 = nd.child[1];
-    if (h0 && h1) {
-      const bool swap = a1 < a0;
-      stk[sp * 64 + lane] = swap ? c0 : c1;
-      ++sp;
-      ref = swap ? c1 : c0;
-      return false;
-    }
-    if (h0 || h1) {
-      ref = h0 ? c0 : c1;
-      return false;
-    }
+    if (visit4<STATS>(S.mnode4[ref], T.lp, T.ld, T.lri, hi, lo, stk, lane, sp, ref, C)) return false;
   } else {
     const int code = ~ref;
     const int f0 = code >> 2, f1 = f0 + (code & 3);
@@ -422,44 +437,59 @@ RT_HD bool traverse(const DevScene& S, const int qmode, const dvec3& P, const dv
 }
 
 
-// Paired-child device layout (DevNode2) of one DFS-pre-order RtxNode tree
-// nodes[0..n): child0 = i + 1, child1 = right (tree-relative), leaf items
-// [first, first + count).  Internal node i becomes record base + k.
-inline bool build_node2(const RtxNode* nodes, int n, std::vector<DevNode2>& out, DevRoot& root) {
-  std::vector<int> idx(size_t(n), -1);
-  const int base = static_cast<int>(out.size());
-  int k = 0;
-  for (int i = 0; i < n; ++i)
-    if (nodes[i].count == 0) idx[size_t(i)] = base + k++;
-  auto ref = [&](int c) -> int {
-    const RtxNode& nd = nodes[c];
-    if (nd.count == 0) return idx[size_t(c)];
-    return ~((nd.first << 2) | nd.count);
-  };
+// 4-wide records (DevNode4) of one DFS-pre-order RtxNode tree nodes[0..n)
+// (child0 = i + 1, child1 = right, tree-relative; leaf items [first,
+// first + count)), emitted in DFS pre-order after the records already in
+// `out`.  stack_need: the most stack entries a walk of this tree can hold
+// (the sum of entries - 1 over the records of a root-to-leaf path).
+inline bool build_node4(const RtxNode* nodes, int n, std::vector<DevNode4>& out, DevRoot& root, int& stack_need) {
   for (int i = 0; i < n; ++i) {
     const RtxNode& nd = nodes[i];
     if (nd.count < 0 || nd.count > 3) return false;
-    if (nd.count != 0) continue;
-    const int c0 = i + 1, c1 = nd.right;
-    if (c0 >= n || c1 <= i || c1 >= n) return false;
-    DevNode2 r;
-    std::memset(&r, 0, sizeof(r));
-    for (int a = 0; a < 3; ++a) {
-      r.box[0 + a] = nodes[c0].bmin[a];
-      r.box[3 + a] = nodes[c0].bmax[a];
-      r.box[6 + a] = nodes[c1].bmin[a];
-      r.box[9 + a] = nodes[c1].bmax[a];
-    }
-    r.child[0] = ref(c0);
-    r.child[1] = ref(c1);
-    out.push_back(r);
+    if (nd.count == 0 && (i + 1 >= n || nd.right <= i || nd.right >= n)) return false;
   }
+  auto leaf_code = [&](int c) { return ~((nodes[c].first << 2) | nodes[c].count); };
+  std::function<int(int, int&)> emit = [&](int i, int& need) -> int {
+    const int idx = static_cast<int>(out.size());
+    out.emplace_back();
+    DevNode4 r;
+    std::memset(&r, 0, sizeof(r));
+    int ents[4], ne = 0;
+    for (const int c : {i + 1, nodes[i].right}) {
+      if (nodes[c].count == 0) {
+        ents[ne++] = c + 1;
+        ents[ne++] = nodes[c].right;
+      } else {
+        ents[ne++] = c;
+      }
+    }
+    r.count = ne;
+    int sub = 0;
+    for (int k = 0; k < ne; ++k) {
+      const int e = ents[k];
+      for (int a = 0; a < 3; ++a) {
+        r.box[k][a] = nodes[e].bmin[a];
+        r.box[k][3 + a] = nodes[e].bmax[a];
+      }
+      if (nodes[e].count == 0) {
+        int below = 0;
+        r.child[k] = emit(e, below);
+        sub = below > sub ? below : sub;
+      } else {
+        r.child[k] = leaf_code(e);
+      }
+    }
+    out[size_t(idx)] = r;
+    need = (ne - 1) + sub;
+    return idx;
+  };
   std::memset(&root, 0, sizeof(root));
   for (int a = 0; a < 3; ++a) {
     root.lo[a] = nodes[0].bmin[a];
     root.hi[a] = nodes[0].bmax[a];
   }
-  root.ref = ref(0);
+  stack_need = 0;
+  root.ref = nodes[0].count == 0 ? emit(0, stack_need) : leaf_code(0);
   return true;
 }
 
