@@ -85,6 +85,8 @@ struct DevScene {
   double cos45;          // glm::cos(PI / 4) computed on the host (light.cpp:145)
   double ambient[3];
   double air_index;      // intensityValue of air's index (material.cpp:17-21)
+  int32_t skip_dark;     // shadow queries whose colour factor is exactly 0 may be skipped
+  int32_t pad_;
 };
 
 struct Counters {

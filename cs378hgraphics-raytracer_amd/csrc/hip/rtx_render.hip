@@ -589,6 +589,15 @@ __device__ __forceinline__ void advance_lane(LaneRef& L, const DevScene& S, cons
         dattn = light_dist_atten(L, X);
         // shadowAttenuation (light.cpp:16-20) / AreaLight (light.cpp:76-87)
         if (L.type == RTX_LIGHT_DIRECTIONAL || L.type == RTX_LIGHT_POINT) {
+          if (S.skip_dark && dscomp.x == 0.0 && dscomp.y == 0.0 && dscomp.z == 0.0) {
+            // the light's term is dattn * sattn * color * 0, and sattn is
+            // finite in this scene (kt in [0,1]), so it adds +0: the shadow
+            // ray still counts (the reference traces it) but is not traced
+            if (STATS) C.shadow++;
+            nrays++;
+            li++;
+            break;
+          }
           sdir = light_dir(L, X - rd * RTX_EPS_BACKUP);
           pick = -1;
         } else {
@@ -1261,7 +1270,7 @@ __global__ void __launch_bounds__(WG, RTX_TRACE_WAVES)
         kq = static_cast<size_t>(qb) * gb + qnext + rank;
         const dvec3 P = mk3(Q.d[0 * cap + kq], Q.d[1 * cap + kq], Q.d[2 * cap + kq]);
         const dvec3 D = mk3(Q.d[3 * cap + kq], Q.d[4 * cap + kq], Q.d[5 * cap + kq]);
-        active = trav_init<STATS>(T, S, MODE, P, D, Q.d[6 * cap + kq], Q.iv[0 * cap + kq], Q.iv[1 * cap + kq],
+        active = trav_init<STATS, MODE>(T, S, P, D, Q.d[6 * cap + kq], Q.iv[0 * cap + kq], Q.iv[1 * cap + kq],
                                   Q.d[7 * cap + kq], MODE == Q_NEXT ? Q.d[8 * cap + kq] : -RTX_INF, C);
         if (!active) finish();
       }
@@ -1271,7 +1280,7 @@ __global__ void __launch_bounds__(WG, RTX_TRACE_WAVES)
     if (__ballot(active) == 0ull) break;  // nothing claimed and nothing left
     const int thresh = exhausted ? 1 : RTX_REFILL;
     do {
-      if (active && trav_step<STATS>(T, S, stk, lane, blk, C)) {
+      if (active && trav_step<STATS, MODE>(T, S, stk, lane, blk, C)) {
         finish();
         active = false;
       }
@@ -1529,6 +1538,25 @@ rtx_status rtx_scene_create(int device, const RtxSceneDesc* d, void** out) {
   S.cos45 = std::cos(3.1415926535897932384626433832795028841971 / 4);
   for (int k = 0; k < 3; ++k) S.ambient[k] = d->ambient[k];
   S.air_index = (0.299 * 1.0) + (0.587 * 1.0) + (0.114 * 1.0);
+  {
+    // skip_dark: every shadow attenuation is finite, i.e. every kt a walk
+    // can multiply in lies in [0, 1] (textures: texel / 255) and colours are
+    // finite, so a light term with a zero colour factor is exactly +0
+    bool ok = true;
+    auto in01 = [](const double* v) {
+      for (int k = 0; k < 3; ++k)
+        if (!(v[k] >= 0.0 && v[k] <= 1.0)) return false;
+      return true;
+    };
+    for (int m = 0; m < d->n_materials; ++m)
+      if (d->materials[m].p[RTX_P_KT].tex < 0 && !in01(d->materials[m].p[RTX_P_KT].v)) ok = false;
+    for (int v = 0; v < d->n_vmats; ++v)
+      if (!in01(d->vmats[v].kt)) ok = false;
+    for (int l = 0; l < d->n_lights; ++l)
+      for (int k = 0; k < 3; ++k)
+        if (!std::isfinite(d->lights[l].color[k])) ok = false;
+    S.skip_dark = ok ? 1 : 0;
+  }
   st->cam = d->camera;
   st->lights.assign(d->lights, d->lights + d->n_lights);
   if (hipMalloc(&st->d_frame, sizeof(FrameParams)) != hipSuccess ||
@@ -1687,6 +1715,10 @@ rtx_status rtx_render(void* scene, const RtxRenderParams* params, uint8_t* rgb8,
   st->S_launch = st->S;
   DevScene& S = st->S_launch;
   S.ss_res = params->ss_res;
+  {
+    const char* e = getenv("RTX_SKIP_DARK");  // 0: trace every shadow ray (A/B)
+    if (e && atoi(e) == 0) S.skip_dark = 0;
+  }
   bool need_picks = false;
   for (const auto& L : st->lights) need_picks |= L.type >= RTX_LIGHT_AREA_RECT;
   if (need_picks && st->picks_res != params->ss_res) {

@@ -48,7 +48,6 @@ struct Trav {
   RayInv ri;
   double tp, tlimit, tlo, tblock;
   int rp, sq;
-  bool closest;
   // answer so far
   double bt;
   int bobj, bsub;
@@ -121,10 +120,9 @@ RT_HD bool visit4(const DevNode4& nd, const dvec3& o, const dvec3& d, const RayI
 
 // Start a query; false if it is already complete (empty scene or the root
 // box is missed: KdTree::intersectList starts with the root's bbox test).
-template <bool STATS>
-RT_HD bool trav_init(Trav& T, const DevScene& S, const int qmode, const dvec3& P, const dvec3& D, const double tp,
-                     const int rp, const int sq, const double tlimit, const double tblock, Counters& C) {
-  T.closest = qmode == Q_CLOSEST;
+template <bool STATS, int QMODE>
+RT_HD bool trav_init(Trav& T, const DevScene& S, const dvec3& P, const dvec3& D, const double tp, const int rp,
+                     const int sq, const double tlimit, const double tblock, Counters& C) {
   T.P = P;
   T.D = D;
   T.tp = tp;
@@ -138,7 +136,7 @@ RT_HD bool trav_init(Trav& T, const DevScene& S, const int qmode, const dvec3& P
   T.have = false;
   T.blocked = false;
   if (S.n_snodes == 0) return false;
-  T.tlo = T.closest ? -RTX_INF : tp - S.margin;
+  T.tlo = QMODE == Q_CLOSEST ? -RTX_INF : tp - S.margin;
   T.ri = ray_inv(D);
   if (STATS) C.nodes++;
   double a, b;
@@ -163,10 +161,10 @@ RT_HD bool trav_init(Trav& T, const DevScene& S, const int qmode, const dvec3& P
 }
 
 // One unit of the walk; true when the query is complete.
-template <bool STATS, class Blocker>
+template <bool STATS, int QMODE, class Blocker>
 RT_HD bool trav_step(Trav& T, const DevScene& S, int* __restrict__ stk, const int lane, const Blocker& blocker,
                      Counters& C) {
-  const bool closest = T.closest;
+  constexpr bool closest = QMODE == Q_CLOSEST;
   const double tp = T.tp, tlimit = T.tlimit, tlo = T.tlo;
   const int rp = T.rp, sq = T.sq;
   double& bt = T.bt;
@@ -425,10 +423,15 @@ RT_HD bool traverse(const DevScene& S, const int qmode, const dvec3& P, const dv
                     const int sq, const double tlimit, double& bt, int& bobj, int& bsub, int* __restrict__ stk,
                     const int lane, Counters& C) {
   Trav T;
-  if (trav_init<STATS>(T, S, qmode, P, D, tp, rp, sq, tlimit, -RTX_INF, C)) {
-    const NoBlocker nb;
-    while (!trav_step<STATS>(T, S, stk, lane, nb, C)) {
-    }
+  const NoBlocker nb;
+  if (qmode == Q_CLOSEST) {
+    if (trav_init<STATS, Q_CLOSEST>(T, S, P, D, tp, rp, sq, tlimit, -RTX_INF, C))
+      while (!trav_step<STATS, Q_CLOSEST>(T, S, stk, lane, nb, C)) {
+      }
+  } else {
+    if (trav_init<STATS, Q_NEXT>(T, S, P, D, tp, rp, sq, tlimit, -RTX_INF, C))
+      while (!trav_step<STATS, Q_NEXT>(T, S, stk, lane, nb, C)) {
+      }
   }
   bt = T.bt;
   bobj = T.bobj;
