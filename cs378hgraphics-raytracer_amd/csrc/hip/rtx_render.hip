@@ -128,7 +128,17 @@ struct HitRef {
   int vi0, vi1, vi2;
 };
 
-__device__ HitRef resolve_hit(const DevScene& S, const dvec3& P, const dvec3& D, int oi, int sub,
+// Inlined by default: out of line (-DRTX_RESOLVE_NOINLINE) the shading
+// kernel needs 4 fewer VGPRs but pays a 224-byte scratch frame per call, and
+// the frame took 130.1 ms instead of 127.8.  The kernels pass S as *Sg (the
+// device copy), so an out-of-line call never has to spill the by-value
+// kernel-argument copy.
+#ifdef RTX_RESOLVE_NOINLINE
+#define RTX_RESOLVE_ATTR __noinline__
+#else
+#define RTX_RESOLVE_ATTR __forceinline__
+#endif
+__device__ RTX_RESOLVE_ATTR HitRef resolve_hit(const DevScene& S, const dvec3& P, const dvec3& D, int oi, int sub,
                               int* rec_face, int* rec_mleaf) {
   HitRef r;
   const RtxObject& o = S.objs[oi];
@@ -290,8 +300,7 @@ struct Pending {
 // wave's access to a field is one contiguous 64-lane line set, and no kernel
 // has to hold the whole state in VGPRs: the state machine touches only the
 // fields of its current step, and the traversal's registers are not shared
-// with it.  LaneRef binds a lane's fields by reference, so the state machine
-// reads like plain per-lane code.
+// with it.  LaneRef gives a lane's fields as accessors (LR.st(), LR.acc(), ...).
 #define LANE_INT_FIELDS(X) X(st) X(sample_slot) X(rec_on) X(pass) X(camk) X(nrays) X(top) X(rdepth) X(rkind) \
   X(first_query) X(sobj) X(ssub) X(m_flags) X(li) X(pick) X(qmode) X(qrp) X(qsq) X(kdone) X(bobj) X(bsub) X(bhave)
 #define LANE_DBL_FIELDS(X) X(sx) X(sy) X(st_t) X(m_sh) X(dattn) X(last_t) X(qtp) X(bt)
@@ -343,27 +352,26 @@ inline LaneMem lane_mem_at(void* base, size_t n) {
 }
 
 struct LaneRef {
-#define M_I(f) int& f;
-#define M_D(f) double& f;
-#define M_V(f) dvec3& f;
+  LaneMem m;
+  unsigned int g;  // lane
+#define M_I(f) \
+  __device__ __forceinline__ int& f() const { return m.i[size_t(LI_##f) * m.n + g]; }
+#define M_D(f) \
+  __device__ __forceinline__ double& f() const { return m.d[size_t(LD_##f) * m.n + g]; }
+#define M_V(f) \
+  __device__ __forceinline__ dvec3& f() const { return m.v[size_t(LV_##f) * m.n + g]; }
   LANE_INT_FIELDS(M_I)
   LANE_DBL_FIELDS(M_D)
   LANE_VEC_FIELDS(M_V)
 #undef M_I
 #undef M_D
 #undef M_V
-  int dummy_;
-  __device__ __forceinline__ LaneRef(const LaneMem& m, size_t g)
-      :
-#define I_I(f) f(m.i[size_t(LI_##f) * m.n + g]),
-#define I_D(f) f(m.d[size_t(LD_##f) * m.n + g]),
-#define I_V(f) f(m.v[size_t(LV_##f) * m.n + g]),
-        LANE_INT_FIELDS(I_I) LANE_DBL_FIELDS(I_D) LANE_VEC_FIELDS(I_V)
-#undef I_I
-#undef I_D
-#undef I_V
-        dummy_(0) {
-  }
+  __device__ __forceinline__ LaneRef(const LaneMem& mm, size_t gg) : m(mm), g(static_cast<unsigned int>(gg)) {}
+  // Compiler barrier + opaque lane index: the state is memory, re-read per
+  // step, and every field address is recomputed from (uniform base, g) where
+  // it is used.  Without the opaque g, LLVM hoists the 43 per-lane 64-bit
+  // field addresses out of the state loop and keeps them all in VGPRs.
+  __device__ __forceinline__ void refresh() { asm volatile("" : "+v"(g)::"memory"); }
 };
 
 // zero one lane's state (kernel start)
@@ -379,20 +387,15 @@ __device__ __forceinline__ void lane_clear(const LaneMem& m, size_t g) {
 // The pending-ray stack lives in HBM: entry e, field f at
 // pbuf[(e * 13 + f) * nlanes + glane].
 template <bool STATS, bool ADAPTIVE>
-__device__ __forceinline__ void advance_lane(LaneRef& L, const DevScene& S, const FrameParams& F, Counters& C,
+__device__ __forceinline__ void advance_lane(LaneRef& LR, const DevScene& S, const FrameParams& F, Counters& C,
                                              double* __restrict__ sbuf, double* __restrict__ colbuf,
                                              RtxHitRecord* __restrict__ hits, int64_t apix_out, int an,
                                              double* __restrict__ pbuf, size_t nlanes, size_t glane, int pend_cap) {
-#define REF(f) auto& f = L.f;
-  LANE_INT_FIELDS(REF)
-  LANE_DBL_FIELDS(REF)
-  LANE_VEC_FIELDS(REF)
-#undef REF
   const RtxRenderParams& P = F.P;
   const double aterm = P.aterm_thresh;
   const int ncam = P.dof ? P.dof_div + 1 : 1;
   auto push = [&](int& tp, const dvec3& p, const dvec3& d, const dvec3& w, const dvec3& k, int depth, int kind) {
-    double* b = pbuf + static_cast<size_t>(tp) * 13 * nlanes + glane;
+    double* b = pbuf + static_cast<size_t>(tp) * 13 * nlanes + LR.g;
     b[0 * nlanes] = p.x; b[1 * nlanes] = p.y; b[2 * nlanes] = p.z;
     b[3 * nlanes] = d.x; b[4 * nlanes] = d.y; b[5 * nlanes] = d.z;
     b[6 * nlanes] = w.x; b[7 * nlanes] = w.y; b[8 * nlanes] = w.z;
@@ -400,35 +403,33 @@ __device__ __forceinline__ void advance_lane(LaneRef& L, const DevScene& S, cons
     b[12 * nlanes] = static_cast<double>(depth * 4 + kind);
     ++tp;
   };
-  qmode = Q_NONE;
-  while (st != ST_IDLE && qmode == Q_NONE) {
-    // compiler barrier: the lane state is memory (LaneRef); without this,
-    // LLVM promotes every field to a loop-carried register and the kernel
-    // needs ~290 VGPRs.  Each step re-reads the few fields it uses.
-    asm volatile("" ::: "memory");
-    switch (st) {
+  LR.qmode() = Q_NONE;
+  while (LR.st() != ST_IDLE && LR.qmode() == Q_NONE) {
+    // the lane state is memory: each step re-reads the few fields it uses
+    LR.refresh();
+    switch (LR.st()) {
       case ST_CAM: {
         // next camera ray of trace(x, y) (RayTracer.cpp:35-79)
-        if (camk == ncam) {
-          dvec3 ret = acc;
+        if (LR.camk() == ncam) {
+          dvec3 ret = LR.acc();
           if (P.dof) ret *= (1.0 / (P.dof_div + 1.0));
           ret = rtm::gclamp3(ret, 0.0, 1.0);
           if (ADAPTIVE) {
-            colbuf[sample_slot * 3 + 0] = ret.x;
-            colbuf[sample_slot * 3 + 1] = ret.y;
-            colbuf[sample_slot * 3 + 2] = ret.z;
-            if (rec_on) hits[apix_out * an + sample_slot].nrays = nrays;
-            st = ST_IDLE;
+            colbuf[LR.sample_slot() * 3 + 0] = ret.x;
+            colbuf[LR.sample_slot() * 3 + 1] = ret.y;
+            colbuf[LR.sample_slot() * 3 + 2] = ret.z;
+            if (LR.rec_on()) hits[apix_out * an + LR.sample_slot()].nrays = LR.nrays();
+            LR.st() = ST_IDLE;
             break;
           }
-          double* out = sbuf + static_cast<int64_t>(sample_slot) * 3;
-          if (P.anaglyph && pass == 0) {  // tracePixel (RayTracer.cpp:92-99): park pass 0 in the buffer
+          double* out = sbuf + static_cast<int64_t>(LR.sample_slot()) * 3;
+          if (P.anaglyph && LR.pass() == 0) {  // tracePixel (RayTracer.cpp:92-99): park pass 0 in the buffer
             out[0] = ret.x;
             out[1] = ret.y;
             out[2] = ret.z;
-            pass = 1;
-            camk = 0;
-            acc = mk3(0, 0, 0);
+            LR.pass() = 1;
+            LR.camk() = 0;
+            LR.acc() = mk3(0, 0, 0);
             break;
           }
           if (P.anaglyph) {
@@ -438,20 +439,20 @@ __device__ __forceinline__ void advance_lane(LaneRef& L, const DevScene& S, cons
             out[1] = ret.y;
             out[2] = ret.z;
           }
-          if (rec_on) hits[sample_slot].nrays = nrays;
-          st = ST_IDLE;
+          if (LR.rec_on()) hits[LR.sample_slot()].nrays = LR.nrays();
+          LR.st() = ST_IDLE;
           break;
         }
         const RtxCamera& cam = F.cam;
-        const dvec3 eye = pass ? ld3(cam.eye) + mk3(0.25, 0.0, 0.0) : ld3(cam.eye);
-        const double x = sx - 0.5, y = sy - 0.5;
+        const dvec3 eye = LR.pass() ? ld3(cam.eye) + mk3(0.25, 0.0, 0.0) : ld3(cam.eye);
+        const double x = LR.sx() - 0.5, y = LR.sy() - 0.5;
         const dvec3 cdir = rtm::normalize(ld3(cam.look) + x * ld3(cam.u) + y * ld3(cam.v));
-        if (camk == 0) {
-          rp = eye;
-          rd = cdir;
-          first_query = rec_on && pass == 0;
-          if (first_query) {  // default record: miss (also what depth < 0 leaves)
-            RtxHitRecord* hr = ADAPTIVE ? &hits[apix_out * an + sample_slot] : &hits[sample_slot];
+        if (LR.camk() == 0) {
+          LR.rp() = eye;
+          LR.rd() = cdir;
+          LR.first_query() = LR.rec_on() && LR.pass() == 0;
+          if (LR.first_query()) {  // default record: miss (also what depth < 0 leaves)
+            RtxHitRecord* hr = ADAPTIVE ? &hits[apix_out * an + LR.sample_slot()] : &hits[LR.sample_slot()];
             hr->object = hr->face = hr->scene_leaf = hr->mesh_leaf = -1;
             hr->t = 1000.0;
             hr->pad = 0;
@@ -463,255 +464,255 @@ __device__ __forceinline__ void advance_lane(LaneRef& L, const DevScene& S, cons
           double t = rtm::dot(fp_n, cdir);
           t = rtm::dot(fp_pt - eye, fp_n) / t;
           const dvec3 dest = rtm::ray_at(eye, cdir, t);
-          rp = eye + ld3(&F.offv[(camk - 1) * 3]);
-          rd = rtm::normalize(dest - rp);
-          first_query = false;
+          LR.rp() = eye + ld3(&F.offv[(LR.camk() - 1) * 3]);
+          LR.rd() = rtm::normalize(dest - LR.rp());
+          LR.first_query() = false;
         }
-        camk++;
+        LR.camk()++;
         if (STATS) C.camera++;
-        top = 0;
-        push(top, rp, rd, mk3(1, 1, 1), mk3(1, 1, 1), P.depth, 0);
-        st = ST_POP;
+        LR.top() = 0;
+        push(LR.top(), LR.rp(), LR.rd(), mk3(1, 1, 1), mk3(1, 1, 1), P.depth, 0);
+        LR.st() = ST_POP;
         break;
       }
       case ST_POP: {
-        if (top == 0) {
-          st = ST_CAM;
+        if (LR.top() == 0) {
+          LR.st() = ST_CAM;
           break;
         }
-        --top;
-        const double* b = pbuf + static_cast<size_t>(top) * 13 * nlanes + glane;
+        --LR.top();
+        const double* b = pbuf + static_cast<size_t>(LR.top()) * 13 * nlanes + LR.g;
         const int dk = static_cast<int>(b[12 * nlanes]);
-        nrays++;
+        LR.nrays()++;
         const int pdepth = dk >= 0 ? dk / 4 : -((-dk + 3) / 4);
         if (pdepth < 0) break;  // `depth >= 0 &&` (RayTracer.cpp:116)
-        rp = mk3(b[0 * nlanes], b[1 * nlanes], b[2 * nlanes]);
-        rd = mk3(b[3 * nlanes], b[4 * nlanes], b[5 * nlanes]);
-        W = mk3(b[6 * nlanes], b[7 * nlanes], b[8 * nlanes]);
-        area_sum = mk3(b[9 * nlanes], b[10 * nlanes], b[11 * nlanes]);  // kt factor, parked until the hit
-        rdepth = pdepth;
-        rkind = dk - pdepth * 4;
-        qmode = Q_CLOSEST;
-        qtp = -RTX_INF;
-        qrp = -1;
-        qsq = -1;
-        st = ST_HIT;
+        LR.rp() = mk3(b[0 * nlanes], b[1 * nlanes], b[2 * nlanes]);
+        LR.rd() = mk3(b[3 * nlanes], b[4 * nlanes], b[5 * nlanes]);
+        LR.W() = mk3(b[6 * nlanes], b[7 * nlanes], b[8 * nlanes]);
+        LR.area_sum() = mk3(b[9 * nlanes], b[10 * nlanes], b[11 * nlanes]);  // kt factor, parked until the hit
+        LR.rdepth() = pdepth;
+        LR.rkind() = dk - pdepth * 4;
+        LR.qmode() = Q_CLOSEST;
+        LR.qtp() = -RTX_INF;
+        LR.qrp() = -1;
+        LR.qsq() = -1;
+        LR.st() = ST_HIT;
         break;
       }
       case ST_HIT: {
         // traceRay after scene->intersect (RayTracer.cpp:116-165)
-        if (first_query) {
-          first_query = false;
-          if (bhave) {
-            RtxHitRecord* hr = ADAPTIVE ? &hits[apix_out * an + sample_slot] : &hits[sample_slot];
-            const RtxObject& o = S.objs[bobj];
+        if (LR.first_query()) {
+          LR.first_query() = false;
+          if (LR.bhave()) {
+            RtxHitRecord* hr = ADAPTIVE ? &hits[apix_out * an + LR.sample_slot()] : &hits[LR.sample_slot()];
+            const RtxObject& o = S.objs[LR.bobj()];
             hr->object = o.orig_id;
             hr->scene_leaf = o.leaf;
-            hr->t = bt;
+            hr->t = LR.bt();
             if (o.type == RTX_OBJ_TRIMESH) {
               const RtxMesh me = S.meshes[o.mesh];
-              const RtxFaceIds fi = S.fids[me.face_off + bsub];
+              const RtxFaceIds fi = S.fids[me.face_off + LR.bsub()];
               hr->face = fi.orig_id;
               hr->mesh_leaf = fi.leaf;
             }
           }
         }
-        if (!bhave) {  // miss: no cube map => black
-          st = ST_POP;
+        if (!LR.bhave()) {  // miss: no cube map => black
+          LR.st() = ST_POP;
           break;
         }
-        if (rkind == 1)
-          W = W * rtm::gmax3(rtm::gmin3(rtm::pow3(area_sum, bt), rtm::splat3(1.0)), rtm::splat3(0.0));
-        else if (rkind == 2)
-          W = W * rtm::pow3(area_sum, bt);
-        const HitRef R = resolve_hit(S, rp, rd, bobj, bsub, nullptr, nullptr);
-        N = R.N;
-        m_kd = hit_param(S, R, RTX_P_KD);
-        m_ks = hit_param(S, R, RTX_P_KS);
-        m_sh = hit_shininess(S, R);
-        m_flags = hit_flags(S, R);
-        st_t = bt;
-        sobj = bobj;
-        ssub = bsub;
+        if (LR.rkind() == 1)
+          LR.W() = LR.W() * rtm::gmax3(rtm::gmin3(rtm::pow3(LR.area_sum(), LR.bt()), rtm::splat3(1.0)), rtm::splat3(0.0));
+        else if (LR.rkind() == 2)
+          LR.W() = LR.W() * rtm::pow3(LR.area_sum(), LR.bt());
+        const HitRef R = resolve_hit(S, LR.rp(), LR.rd(), LR.bobj(), LR.bsub(), nullptr, nullptr);
+        LR.N() = R.N;
+        LR.m_kd() = hit_param(S, R, RTX_P_KD);
+        LR.m_ks() = hit_param(S, R, RTX_P_KS);
+        LR.m_sh() = hit_shininess(S, R);
+        LR.m_flags() = hit_flags(S, R);
+        LR.st_t() = LR.bt();
+        LR.sobj() = LR.bobj();
+        LR.ssub() = LR.bsub();
         if (STATS) C.shades++;
         // Material::shade (material.cpp:34-69)
-        i_out = hit_param(S, R, RTX_P_KE) + hit_param(S, R, RTX_P_KA) * mk3(S.ambient[0], S.ambient[1], S.ambient[2]);
-        li = 0;
-        st = ST_LIGHT;
+        LR.i_out() = hit_param(S, R, RTX_P_KE) + hit_param(S, R, RTX_P_KA) * mk3(S.ambient[0], S.ambient[1], S.ambient[2]);
+        LR.li() = 0;
+        LR.st() = ST_LIGHT;
         break;
       }
       case ST_LIGHT: {
-        if (li == S.n_lights) {
+        if (LR.li() == S.n_lights) {
           // colorC = shade(...); adaptive termination; recursion
-          const dvec3 col = i_out;
-          acc += W * col;
-          const int depth = rdepth - 1;
-          st = ST_POP;
+          const dvec3 col = LR.i_out();
+          LR.acc() += LR.W() * col;
+          const int depth = LR.rdepth() - 1;
+          LR.st() = ST_POP;
           if (aterm > 0.0 && rtm::dot(col, col) < aterm) break;
-          if ((m_flags & RTX_MF_RECUR) && depth > 0) {
-            const HitRef R = resolve_hit(S, rp, rd, sobj, ssub, nullptr, nullptr);
-            const bool leaving = rtm::dot(N, rd) >= 0;
-            const bool in_trans = (m_flags & RTX_MF_TRANS) != 0;
+          if ((LR.m_flags() & RTX_MF_RECUR) && depth > 0) {
+            const HitRef R = resolve_hit(S, LR.rp(), LR.rd(), LR.sobj(), LR.ssub(), nullptr, nullptr);
+            const bool leaving = rtm::dot(LR.N(), LR.rd()) >= 0;
+            const bool in_trans = (LR.m_flags() & RTX_MF_TRANS) != 0;
             const bool next_trans = leaving ? true : in_trans;  // air is transmissive
-            const dvec3 normal = (leaving ? -1.0 : 1.0) * N;
-            const double c = -1 * rtm::dot(normal, rd);
+            const dvec3 normal = (leaving ? -1.0 : 1.0) * LR.N();
+            const double c = -1 * rtm::dot(normal, LR.rd());
             const double eta =
                 next_trans ? (leaving ? hit_index(S, R) : S.air_index) / (leaving ? S.air_index : hit_index(S, R)) : 0;
             const double radicand = 1 - eta * eta * (1 - c * c);
             const bool tir = next_trans && radicand < 0;
             // push refraction first so that reflection is traced first
-            if (next_trans && !tir && top < pend_cap) {
-              const dvec3 tp = rtm::ray_at(rp, rd, st_t + RTX_RAY_EPS);
-              const dvec3 td = eta * rd + (eta * c - sqrt(radicand)) * normal;
-              push(top, tp, td, W, leaving ? mk3(1.0, 1.0, 1.0) : hit_param(S, R, RTX_P_KT), depth, 2);
+            if (next_trans && !tir && LR.top() < pend_cap) {
+              const dvec3 tp = rtm::ray_at(LR.rp(), LR.rd(), LR.st_t() + RTX_RAY_EPS);
+              const dvec3 td = eta * LR.rd() + (eta * c - sqrt(radicand)) * normal;
+              push(LR.top(), tp, td, LR.W(), leaving ? mk3(1.0, 1.0, 1.0) : hit_param(S, R, RTX_P_KT), depth, 2);
               if (STATS) C.secondary++;
             }
-            if (((m_flags & RTX_MF_REFL) || tir) && top < pend_cap) {
-              const dvec3 rdir = rd + 2 * c * normal;
-              const dvec3 rs = rtm::ray_at(rp, rd, st_t - RTX_RAY_EPS);
-              push(top, rs, rdir, W * hit_param(S, R, RTX_P_KR), leaving ? hit_param(S, R, RTX_P_KT) : mk3(1.0, 1.0, 1.0),
+            if (((LR.m_flags() & RTX_MF_REFL) || tir) && LR.top() < pend_cap) {
+              const dvec3 rdir = LR.rd() + 2 * c * normal;
+              const dvec3 rs = rtm::ray_at(LR.rp(), LR.rd(), LR.st_t() - RTX_RAY_EPS);
+              push(LR.top(), rs, rdir, LR.W() * hit_param(S, R, RTX_P_KR), leaving ? hit_param(S, R, RTX_P_KT) : mk3(1.0, 1.0, 1.0),
                    depth, 1);
               if (STATS) C.secondary++;
             }
           }
           break;
         }
-        const RtxLight& L = S.lights[li];
-        const dvec3 X = rtm::ray_at(rp, rd, st_t);
+        const RtxLight& L = S.lights[LR.li()];
+        const dvec3 X = rtm::ray_at(LR.rp(), LR.rd(), LR.st_t());
         const dvec3 l_i = light_dir(L, X);
-        const dvec3 l_r = (l_i - 2 * (rtm::dot(l_i, N)) * N);
-        double dt = rtm::dot(l_i, N);
-        if (m_flags & RTX_MF_TRANS) dt = fabs(dt);
-        const dvec3 d_comp = m_kd * rtm::gmax(0.0, dt);
+        const dvec3 l_r = (l_i - 2 * (rtm::dot(l_i, LR.N())) * LR.N());
+        double dt = rtm::dot(l_i, LR.N());
+        if (LR.m_flags() & RTX_MF_TRANS) dt = fabs(dt);
+        const dvec3 d_comp = LR.m_kd() * rtm::gmax(0.0, dt);
         // glm::pow(dvec3(x), dvec3(sh)): three identical std::pow calls, one here
-        const dvec3 s_comp = m_ks * rtm::splat3(rtm::rpow(rtm::gmax(0.0, rtm::dot(l_r, rd)), m_sh));
-        dscomp = d_comp + s_comp;
-        dattn = light_dist_atten(L, X);
+        const dvec3 s_comp = LR.m_ks() * rtm::splat3(rtm::rpow(rtm::gmax(0.0, rtm::dot(l_r, LR.rd())), LR.m_sh()));
+        LR.dscomp() = d_comp + s_comp;
+        LR.dattn() = light_dist_atten(L, X);
         // shadowAttenuation (light.cpp:16-20) / AreaLight (light.cpp:76-87)
         if (L.type == RTX_LIGHT_DIRECTIONAL || L.type == RTX_LIGHT_POINT) {
-          if (S.skip_dark && dscomp.x == 0.0 && dscomp.y == 0.0 && dscomp.z == 0.0) {
+          if (S.skip_dark && LR.dscomp().x == 0.0 && LR.dscomp().y == 0.0 && LR.dscomp().z == 0.0) {
             // the light's term is dattn * sattn * color * 0, and sattn is
             // finite in this scene (kt in [0,1]), so it adds +0: the shadow
             // ray still counts (the reference traces it) but is not traced
             if (STATS) C.shadow++;
-            nrays++;
-            li++;
+            LR.nrays()++;
+            LR.li()++;
             break;
           }
-          sdir = light_dir(L, X - rd * RTX_EPS_BACKUP);
-          pick = -1;
+          LR.sdir() = light_dir(L, X - LR.rd() * RTX_EPS_BACKUP);
+          LR.pick() = -1;
         } else {
           const dvec3 ori = ld3(L.orient), lpos = ld3(L.pos);
           if (L.type == RTX_LIGHT_SPOT &&
               !((rtm::dot(light_dir(L, X), ori) <= 0) &&
                 (rtm::dot(rtm::normalize(X - (lpos - L.offset * ori)), ori) > S.cos45))) {
-            i_out += dattn * mk3(0.0, 0.0, 0.0) * ld3(L.color) * dscomp;
-            li++;
+            LR.i_out() += LR.dattn() * mk3(0.0, 0.0, 0.0) * ld3(L.color) * LR.dscomp();
+            LR.li()++;
             break;
           }
-          area_sum = mk3(1.0, 1.0, 1.0);
-          pick = 0;
+          LR.area_sum() = mk3(1.0, 1.0, 1.0);
+          LR.pick() = 0;
         }
-        st = ST_SRS;
+        LR.st() = ST_SRS;
         break;
       }
       case ST_SRS: {
         // start one srsAttenuation (light.cpp:21-53), or finish an area light
-        const RtxLight& L = S.lights[li];
-        const dvec3 pb = rtm::ray_at(rp, rd, st_t) - rd * RTX_EPS_BACKUP;
-        if (pick >= 0) {
+        const RtxLight& L = S.lights[LR.li()];
+        const dvec3 pb = rtm::ray_at(LR.rp(), LR.rd(), LR.st_t()) - LR.rd() * RTX_EPS_BACKUP;
+        if (LR.pick() >= 0) {
           bool started = false;
-          while (pick < S.ss_res) {
-            const dvec3 lp = ld3(S.picks + (size_t(li) * S.ss_res + pick) * 3);
-            pick++;
+          while (LR.pick() < S.ss_res) {
+            const dvec3 lp = ld3(S.picks + (size_t(LR.li()) * S.ss_res + LR.pick()) * 3);
+            LR.pick()++;
             if (L.type == RTX_LIGHT_SPOT &&
                 !((rtm::dot(light_dir(L, pb), ld3(L.orient)) <= 0) &&
                   (rtm::dot(rtm::normalize(pb - lp), ld3(L.orient)) > S.cos45)))
               continue;
-            sdir = rtm::normalize(lp - pb);
+            LR.sdir() = rtm::normalize(lp - pb);
             started = true;
             break;
           }
           if (!started) {
-            dvec3 sa = area_sum;
+            dvec3 sa = LR.area_sum();
             sa *= (1.0 / (S.ss_res - 1));
-            i_out += dattn * sa * ld3(L.color) * dscomp;
-            li++;
-            st = ST_LIGHT;
+            LR.i_out() += LR.dattn() * sa * ld3(L.color) * LR.dscomp();
+            LR.li()++;
+            LR.st() = ST_LIGHT;
             break;
           }
         }
         if (STATS) C.shadow++;
-        nrays++;
-        sattn = mk3(1.0, 1.0, 1.0);
-        wpos = pb;
-        last_t = 0.0;
-        qmode = Q_NEXT;
-        qtp = -RTX_INF;
-        qrp = -1;
-        qsq = -1;
-        st = ST_WALK;
+        LR.nrays()++;
+        LR.sattn() = mk3(1.0, 1.0, 1.0);
+        LR.wpos() = pb;
+        LR.last_t() = 0.0;
+        LR.qmode() = Q_NEXT;
+        LR.qtp() = -RTX_INF;
+        LR.qrp() = -1;
+        LR.qsq() = -1;
+        LR.st() = ST_WALK;
         break;
       }
       case ST_WALK: {
-        const RtxLight& L = S.lights[li];
+        const RtxLight& L = S.lights[LR.li()];
         bool done = false;
-        dvec3 result = sattn;
-        if (!bhave) {
+        dvec3 result = LR.sattn();
+        if (!LR.bhave()) {
           done = true;
-        } else if (bhave == 2) {  // a blocker below tblock (trace_kernel's shadow early-out)
+        } else if (LR.bhave() == 2) {  // a blocker below tblock (trace_kernel's shadow early-out)
           result = mk3(0.0, 0.0, 0.0);
           done = true;
         } else {
-          const double t = bt - last_t;
-          last_t = bt;
-          const dvec3 pb = rtm::ray_at(rp, rd, st_t) - rd * RTX_EPS_BACKUP;
-          const HitRef R = resolve_hit(S, pb, sdir, bobj, bsub, nullptr, nullptr);
-          const bool is_inside = rtm::dot(R.N, sdir) > 0;
-          wpos = rtm::ray_at(wpos, sdir, t);
+          const double t = LR.bt() - LR.last_t();
+          LR.last_t() = LR.bt();
+          const dvec3 pb = rtm::ray_at(LR.rp(), LR.rd(), LR.st_t()) - LR.rd() * RTX_EPS_BACKUP;
+          const HitRef R = resolve_hit(S, pb, LR.sdir(), LR.bobj(), LR.bsub(), nullptr, nullptr);
+          const bool is_inside = rtm::dot(R.N, LR.sdir()) > 0;
+          LR.wpos() = rtm::ray_at(LR.wpos(), LR.sdir(), t);
           bool limit = false;  // sattnLimitCheck with the relative t (U14)
           if (L.type == RTX_LIGHT_POINT) {
-            limit = rtm::dot(ld3(L.pos) - rtm::ray_at(wpos, sdir, t), sdir) <= 0;
+            limit = rtm::dot(ld3(L.pos) - rtm::ray_at(LR.wpos(), LR.sdir(), t), LR.sdir()) <= 0;
           } else if (L.type != RTX_LIGHT_DIRECTIONAL) {
             const dvec3 ori = ld3(L.orient), lpos = ld3(L.pos);
-            double ti = rtm::dot(ori, sdir);
-            ti = rtm::dot(lpos - wpos, ori) / ti;
-            dvec3 imp = rtm::ray_at(wpos, sdir, ti);
+            double ti = rtm::dot(ori, LR.sdir());
+            ti = rtm::dot(lpos - LR.wpos(), ori) / ti;
+            dvec3 imp = rtm::ray_at(LR.wpos(), LR.sdir(), ti);
             if (L.type != RTX_LIGHT_AREA_RECT && !(rtm::dot(imp - lpos, imp - lpos) < (L.radius * L.radius)))
               imp = mk3(0.0, 0.0, 0.0);
-            limit = rtm::dot(imp - rtm::ray_at(wpos, sdir, t), sdir) <= 0;
+            limit = rtm::dot(imp - rtm::ray_at(LR.wpos(), LR.sdir(), t), LR.sdir()) <= 0;
           }
           if (limit) {
             done = true;
           } else {
             const bool next_trans = is_inside ? true : ((hit_flags(S, R) & RTX_MF_TRANS) != 0);
-            if (!next_trans || (aterm > 0.0 && rtm::dot(sattn, sattn) < aterm * aterm)) {
+            if (!next_trans || (aterm > 0.0 && rtm::dot(LR.sattn(), LR.sattn()) < aterm * aterm)) {
               result = mk3(0.0, 0.0, 0.0);
               done = true;
             } else {
               const dvec3 kt = is_inside ? hit_param(S, R, RTX_P_KT) : mk3(1.0, 1.0, 1.0);
-              sattn *= rtm::pow3(kt, t);
-              qmode = Q_NEXT;
-              qtp = bt;
-              qrp = bobj;
-              qsq = bsub;
+              LR.sattn() *= rtm::pow3(kt, t);
+              LR.qmode() = Q_NEXT;
+              LR.qtp() = LR.bt();
+              LR.qrp() = LR.bobj();
+              LR.qsq() = LR.bsub();
             }
           }
         }
         if (done) {
-          if (pick < 0) {
-            i_out += dattn * result * ld3(L.color) * dscomp;
-            li++;
-            st = ST_LIGHT;
+          if (LR.pick() < 0) {
+            LR.i_out() += LR.dattn() * result * ld3(L.color) * LR.dscomp();
+            LR.li()++;
+            LR.st() = ST_LIGHT;
           } else {
-            area_sum += result;
-            st = ST_SRS;
+            LR.area_sum() += result;
+            LR.st() = ST_SRS;
           }
         }
         break;
       }
       default:
-        st = ST_IDLE;
+        LR.st() = ST_IDLE;
         break;
     }
   }
@@ -719,7 +720,7 @@ __device__ __forceinline__ void advance_lane(LaneRef& L, const DevScene& S, cons
 }
 
 template <bool STATS, bool ADAPTIVE>
-__global__ void __launch_bounds__(WG) render_kernel(DevScene S, const FrameParams* __restrict__ Fp,
+__global__ void __launch_bounds__(WG) render_kernel(DevScene S, const DevScene* __restrict__ Sg, const FrameParams* __restrict__ Fp,
                                                      unsigned long long* __restrict__ work,
                                                      double* __restrict__ sbuf, RtxHitRecord* __restrict__ hits,
                                                      uint8_t* __restrict__ rgb8, double* __restrict__ rgbf,
@@ -746,14 +747,9 @@ __global__ void __launch_bounds__(WG) render_kernel(DevScene S, const FrameParam
 
   // ---- lane state (HBM, see LaneRef)
   lane_clear(lm, glane);
-  LaneRef L(lm, glane);
-#define REF(f) auto& f = L.f;
-  LANE_INT_FIELDS(REF)
-  LANE_DBL_FIELDS(REF)
-  LANE_VEC_FIELDS(REF)
-#undef REF
-  st = ST_IDLE;
-  sample_slot = -1;
+  LaneRef LR(lm, glane);
+  LR.st() = ST_IDLE;
+  LR.sample_slot() = -1;
 
   // ---- wave-uniform scheduler state
   unsigned long long qnext = 0, qend = 0;
@@ -766,9 +762,10 @@ __global__ void __launch_bounds__(WG) render_kernel(DevScene S, const FrameParam
   const int an = F.spp;
 
   for (;;) {
+    LR.refresh();
     // ------------------------------------------------ scheduling
     if (!ADAPTIVE) {
-      unsigned long long idle = __ballot(st == ST_IDLE);
+      unsigned long long idle = __ballot(LR.st() == ST_IDLE);
       while (idle != 0ull) {
         if (qnext >= qend) {
           if (exhausted) break;
@@ -788,7 +785,7 @@ __global__ void __launch_bounds__(WG) render_kernel(DevScene S, const FrameParam
         const unsigned long long avail = qend - qnext;
         const unsigned int nidle = __popcll(idle);
         const unsigned int take = avail < nidle ? static_cast<unsigned int>(avail) : nidle;
-        if (st == ST_IDLE && rank < take) {
+        if (LR.st() == ST_IDLE && rank < take) {
           const int64_t sid = static_cast<int64_t>(qnext + rank);
           const int64_t item = sid / (F.ppw * F.spp);
           const int slot = static_cast<int>(sid % (F.ppw * F.spp));
@@ -805,27 +802,27 @@ __global__ void __launch_bounds__(WG) render_kernel(DevScene S, const FrameParam
               ssy = F.s;
             }
             // tracePixel (RayTracer.cpp:87-88)
-            sx = double(pi) / (double(P.width) * ssx);
-            sy = double(pj) / (double(P.height) * ssy);
-            sample_slot = static_cast<int>(oidx * F.spp + smp);
-            rec_on = hits != nullptr;
-            pass = 0;
-            camk = 0;
-            nrays = 0;
-            acc = mk3(0, 0, 0);
-            st = ST_CAM;
+            LR.sx() = double(pi) / (double(P.width) * ssx);
+            LR.sy() = double(pj) / (double(P.height) * ssy);
+            LR.sample_slot() = static_cast<int>(oidx * F.spp + smp);
+            LR.rec_on() = hits != nullptr;
+            LR.pass() = 0;
+            LR.camk() = 0;
+            LR.nrays() = 0;
+            LR.acc() = mk3(0, 0, 0);
+            LR.st() = ST_CAM;
           }
           // out-of-image slots stay idle and are simply consumed
         }
         qnext += take;
-        idle = __ballot(st == ST_IDLE);
+        idle = __ballot(LR.st() == ST_IDLE);
         if (take == 0) break;
         if (qnext < qend) break;  // every idle lane got work (or was consumed)
       }
     } else {
       // adaptive: one pixel per wave; all lanes idle => chunk finished.
       // Frames f: frbuf[f*8 + 0..3] = x1, x2, y1, y2; [4..6] = acc; [7] = child
-      if (__ballot(st != ST_IDLE) == 0ull) {
+      if (__ballot(LR.st() != ST_IDLE) == 0ull) {
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -850,7 +847,7 @@ __global__ void __launch_bounds__(WG) render_kernel(DevScene S, const FrameParam
             set_acc(fsp - 1, facc(fsp - 1) + mu);
             frbuf[(fsp - 1) * 8 + 7] += 1.0;
           } else {
-            acc = mu;  // pixel value
+            LR.acc() = mu;  // pixel value
           }
         };
         bool need_new_pixel = fsp == 0;
@@ -904,14 +901,14 @@ __global__ void __launch_bounds__(WG) render_kernel(DevScene S, const FrameParam
         if (fsp == 0 && !need_new_pixel) {
           if (lane == 0) {  // setPixel (RayTracer.cpp:388-394)
             if (rgb8) {
-              rgb8[apix_out * 3 + 0] = (uint8_t)(int)(255.0 * acc.x);
-              rgb8[apix_out * 3 + 1] = (uint8_t)(int)(255.0 * acc.y);
-              rgb8[apix_out * 3 + 2] = (uint8_t)(int)(255.0 * acc.z);
+              rgb8[apix_out * 3 + 0] = (uint8_t)(int)(255.0 * LR.acc().x);
+              rgb8[apix_out * 3 + 1] = (uint8_t)(int)(255.0 * LR.acc().y);
+              rgb8[apix_out * 3 + 2] = (uint8_t)(int)(255.0 * LR.acc().z);
             }
             if (rgbf) {
-              rgbf[apix_out * 3 + 0] = acc.x;
-              rgbf[apix_out * 3 + 1] = acc.y;
-              rgbf[apix_out * 3 + 2] = acc.z;
+              rgbf[apix_out * 3 + 0] = LR.acc().x;
+              rgbf[apix_out * 3 + 1] = LR.acc().y;
+              rgbf[apix_out * 3 + 2] = LR.acc().z;
             }
           }
           need_new_pixel = true;
@@ -959,38 +956,38 @@ __global__ void __launch_bounds__(WG) render_kernel(DevScene S, const FrameParam
           const int f = fsp - 1;
           const double x1 = frbuf[f * 8 + 0], x2 = frbuf[f * 8 + 1], y1 = frbuf[f * 8 + 2], y2 = frbuf[f * 8 + 3];
           const double w = x2 - x1, h = y2 - y1;
-          sx = radinv2(k) * w + x1;    // hammersley x
-          sy = (0.0 / an) * h + y1;    // hammersley y is always 0 (U7)
-          sample_slot = k;
-          rec_on = hits != nullptr && atop;
-          pass = 0;
-          camk = 0;
-          nrays = 0;
-          acc = mk3(0, 0, 0);
-          st = ST_CAM;
+          LR.sx() = radinv2(k) * w + x1;    // hammersley x
+          LR.sy() = (0.0 / an) * h + y1;    // hammersley y is always 0 (U7)
+          LR.sample_slot() = k;
+          LR.rec_on() = hits != nullptr && atop;
+          LR.pass() = 0;
+          LR.camk() = 0;
+          LR.nrays() = 0;
+          LR.acc() = mk3(0, 0, 0);
+          LR.st() = ST_CAM;
         }
       }
     }
 
     // ------------------------------------------------ advance lanes to their next query
-    advance_lane<STATS, ADAPTIVE>(L, S, F, C, sbuf, colbuf, hits, apix_out, an, pbuf, nlanes, glane, pend_cap);
+    advance_lane<STATS, ADAPTIVE>(LR, *Sg, F, C, sbuf, colbuf, hits, apix_out, an, pbuf, nlanes, glane, pend_cap);
 
     // ------------------------------------------------ exit / traversal
-    const unsigned long long busy = __ballot(qmode != Q_NONE);
+    const unsigned long long busy = __ballot(LR.qmode() != Q_NONE);
     if (busy == 0ull) {
-      if (__ballot(st != ST_IDLE) == 0ull && exhausted) break;
+      if (__ballot(LR.st() != ST_IDLE) == 0ull && exhausted) break;
       continue;
     }
-    if (qmode != Q_NONE) {
-      dvec3 qP = rp, qD = rd;
+    if (LR.qmode() != Q_NONE) {
+      dvec3 qP = LR.rp(), qD = LR.rd();
       double qlim = RTX_INF;
-      if (qmode == Q_NEXT) {
-        qP = rtm::ray_at(rp, rd, st_t) - rd * RTX_EPS_BACKUP;
-        qD = sdir;
+      if (LR.qmode() == Q_NEXT) {
+        qP = rtm::ray_at(LR.rp(), LR.rd(), LR.st_t()) - LR.rd() * RTX_EPS_BACKUP;
+        qD = LR.sdir();
         double qblk;
-        shadow_bounds(S, S.lights[li], qP, qrp < 0, qlim, qblk);
+        shadow_bounds(S, S.lights[LR.li()], qP, LR.qrp() < 0, qlim, qblk);
       }
-      bhave = traverse<STATS>(S, qmode, qP, qD, qtp, qrp, qsq, qlim, bt, bobj, bsub, stk, lane, C);
+      LR.bhave() = traverse<STATS>(S, LR.qmode(), qP, qD, LR.qtp(), LR.qrp(), LR.qsq(), qlim, LR.bt(), LR.bobj(), LR.bsub(), stk, lane, C);
     }
   }
   if (STATS) {
@@ -1063,11 +1060,11 @@ __device__ __forceinline__ int64_t slot_sample(const FrameParams& F, int slot, i
 // scheduler of the megakernel does with its queue).
 __device__ __forceinline__ void claim_sample(LaneRef& L, const FrameParams& F, RtxHitRecord* hits, int slot) {
   const RtxRenderParams& P = F.P;
-  while (L.st == ST_IDLE) {
+  while (L.st() == ST_IDLE) {
     int64_t band_end;
-    const int64_t sid = slot_sample(F, slot, L.kdone, band_end);
+    const int64_t sid = slot_sample(F, slot, L.kdone(), band_end);
     if (sid >= band_end) return;
-    L.kdone++;
+    L.kdone()++;
     const int64_t item = sid / (F.ppw * F.spp);
     const int sl = static_cast<int>(sid % (F.ppw * F.spp));
     const int pix = sl / F.spp, smp = sl % F.spp;
@@ -1082,20 +1079,20 @@ __device__ __forceinline__ void claim_sample(LaneRef& L, const FrameParams& F, R
       ssx = F.s;
       ssy = F.s;
     }
-    L.sx = double(pi) / (double(P.width) * ssx);  // tracePixel (RayTracer.cpp:87-88)
-    L.sy = double(pj) / (double(P.height) * ssy);
-    L.sample_slot = static_cast<int>(oidx * F.spp + smp);
-    L.rec_on = hits != nullptr;
-    L.pass = 0;
-    L.camk = 0;
-    L.nrays = 0;
-    L.acc = mk3(0, 0, 0);
-    L.st = ST_CAM;
+    L.sx() = double(pi) / (double(P.width) * ssx);  // tracePixel (RayTracer.cpp:87-88)
+    L.sy() = double(pj) / (double(P.height) * ssy);
+    L.sample_slot() = static_cast<int>(oidx * F.spp + smp);
+    L.rec_on() = hits != nullptr;
+    L.pass() = 0;
+    L.camk() = 0;
+    L.nrays() = 0;
+    L.acc() = mk3(0, 0, 0);
+    L.st() = ST_CAM;
   }
 }
 
 template <bool STATS>
-__global__ void __launch_bounds__(WG, RTX_ADV_WAVES) advance_kernel(DevScene S, const FrameParams* __restrict__ Fp, LaneMem lm,
+__global__ void __launch_bounds__(WG, RTX_ADV_WAVES) advance_kernel(DevScene S, const DevScene* __restrict__ Sg, const FrameParams* __restrict__ Fp, LaneMem lm,
                                                       double* __restrict__ sbuf, RtxHitRecord* __restrict__ hits,
                                                       double* __restrict__ pbuf, int pend_cap, QList q0, QList q1,
                                                       unsigned int* __restrict__ counters,
@@ -1108,17 +1105,17 @@ __global__ void __launch_bounds__(WG, RTX_ADV_WAVES) advance_kernel(DevScene S, 
   LaneRef L(lm, static_cast<size_t>(slot));
   int qm = Q_NONE;
   int64_t band_end;
-  if (L.st != ST_IDLE || slot_sample(F, slot, L.kdone, band_end) < band_end) {
-    // the previous iteration's query result is already in L.bt/bobj/bsub/bhave
-    L.qmode = Q_NONE;
+  if (L.st() != ST_IDLE || slot_sample(F, slot, L.kdone(), band_end) < band_end) {
+    // the previous iteration's query result is already in L.bt()/bobj/bsub/bhave
+    L.qmode() = Q_NONE;
     for (;;) {
       claim_sample(L, F, hits, slot);
-      if (L.st == ST_IDLE) break;
-      advance_lane<STATS, false>(L, S, F, C, sbuf, nullptr, hits, 0, 0, pbuf, lm.n, static_cast<size_t>(slot),
+      if (L.st() == ST_IDLE) break;
+      advance_lane<STATS, false>(L, *Sg, F, C, sbuf, nullptr, hits, 0, 0, pbuf, lm.n, static_cast<size_t>(slot),
                                  pend_cap);
-      if (L.qmode != Q_NONE) break;
+      if (L.qmode() != Q_NONE) break;
     }
-    qm = L.qmode;
+    qm = L.qmode();
   }
   // compaction: append queries to their list, one atomic per wave per list
   const int lane = threadIdx.x & 63;
@@ -1134,12 +1131,12 @@ __global__ void __launch_bounds__(WG, RTX_ADV_WAVES) advance_kernel(DevScene S, 
       const QList& Q = m == Q_CLOSEST ? q0 : q1;
       const size_t cap = Q.cap;
       const size_t k = static_cast<size_t>(band) * F.wf_gb + base + lane_prefix(mask);
-      dvec3 qP = L.rp, qD = L.rd;
+      dvec3 qP = L.rp(), qD = L.rd();
       double qlim = RTX_INF, qblk = -RTX_INF;
       if (m == Q_NEXT) {
-        qP = rtm::ray_at(L.rp, L.rd, L.st_t) - L.rd * RTX_EPS_BACKUP;
-        qD = L.sdir;
-        shadow_bounds(S, S.lights[L.li], qP, L.qrp < 0, qlim, qblk);
+        qP = rtm::ray_at(L.rp(), L.rd(), L.st_t()) - L.rd() * RTX_EPS_BACKUP;
+        qD = L.sdir();
+        shadow_bounds(S, S.lights[L.li()], qP, L.qrp() < 0, qlim, qblk);
       }
       Q.d[8 * cap + k] = qblk;
       Q.slot[k] = slot;
@@ -1149,13 +1146,13 @@ __global__ void __launch_bounds__(WG, RTX_ADV_WAVES) advance_kernel(DevScene S, 
       Q.d[3 * cap + k] = qD.x;
       Q.d[4 * cap + k] = qD.y;
       Q.d[5 * cap + k] = qD.z;
-      Q.d[6 * cap + k] = L.qtp;
+      Q.d[6 * cap + k] = L.qtp();
       Q.d[7 * cap + k] = qlim;
-      Q.iv[0 * cap + k] = L.qrp;
-      Q.iv[1 * cap + k] = L.qsq;
+      Q.iv[0 * cap + k] = L.qrp();
+      Q.iv[1 * cap + k] = L.qsq();
     }
   }
-  const unsigned long long alive = __ballot(L.st != ST_IDLE);
+  const unsigned long long alive = __ballot(L.st() != ST_IDLE);
   if (lane == 0 && alive) atomicAdd(&counters[CNT_ALIVE], static_cast<unsigned int>(__popcll(alive)));
   if (STATS) {
     int64_t v[7] = {C.camera, C.secondary, C.shadow, C.nodes, C.objects, C.tris, C.shades};
@@ -1760,6 +1757,10 @@ rtx_status rtx_render(void* scene, const RtxRenderParams* params, uint8_t* rgb8,
     }
   }
   HIP_TRY(hipMemsetAsync(st->d_work, 0, sizeof(unsigned long long), stream));
+  // device copy of the scene record: functions called out of line read it
+  // through this pointer (a kernel-argument copy has no address)
+  if (!st->d_scene) HIP_TRY(hipMalloc(&st->d_scene, sizeof(DevScene)));
+  HIP_TRY(hipMemcpyAsync(st->d_scene, &st->S_launch, sizeof(DevScene), hipMemcpyHostToDevice, stream));
   if (stats) HIP_TRY(hipMemsetAsync(st->d_stats, 0, 8 * sizeof(unsigned long long), stream));
   const int pend_cap = (params->depth > 0 ? params->depth : 0) + 2;
   auto get_event = [&](hipEvent_t* e) -> rtx_status {
@@ -1833,19 +1834,19 @@ rtx_status rtx_render(void* scene, const RtxRenderParams* params, uint8_t* rgb8,
     HIP_TRY(hipEventRecord(e0, stream));
     if (stats) {
       if (adaptive)
-        hipLaunchKernelGGL((render_kernel<true, true>), dim3(grid), dim3(WG), lds, stream, st->S_launch, st->d_frame,
+        hipLaunchKernelGGL((render_kernel<true, true>), dim3(grid), dim3(WG), lds, stream, st->S_launch, st->d_scene, st->d_frame,
                            st->d_work, sb, d_hits, d_rgb8, d_rgbf, st->d_stats, st->stack_cap, st->d_pbuf, pend_cap, lm);
       else
-        hipLaunchKernelGGL((render_kernel<true, false>), dim3(grid), dim3(WG), lds, stream, st->S_launch,
+        hipLaunchKernelGGL((render_kernel<true, false>), dim3(grid), dim3(WG), lds, stream, st->S_launch, st->d_scene,
                            st->d_frame, st->d_work, sb, d_hits, d_rgb8, d_rgbf, st->d_stats, st->stack_cap,
                            st->d_pbuf, pend_cap, lm);
     } else {
       if (adaptive)
-        hipLaunchKernelGGL((render_kernel<false, true>), dim3(grid), dim3(WG), lds, stream, st->S_launch,
+        hipLaunchKernelGGL((render_kernel<false, true>), dim3(grid), dim3(WG), lds, stream, st->S_launch, st->d_scene,
                            st->d_frame, st->d_work, sb, d_hits, d_rgb8, d_rgbf, st->d_stats, st->stack_cap,
                            st->d_pbuf, pend_cap, lm);
       else
-        hipLaunchKernelGGL((render_kernel<false, false>), dim3(grid), dim3(WG), lds, stream, st->S_launch,
+        hipLaunchKernelGGL((render_kernel<false, false>), dim3(grid), dim3(WG), lds, stream, st->S_launch, st->d_scene,
                            st->d_frame, st->d_work, sb, d_hits, d_rgb8, d_rgbf, st->d_stats, st->stack_cap,
                            st->d_pbuf, pend_cap, lm);
     }
@@ -1893,8 +1894,6 @@ rtx_status rtx_render(void* scene, const RtxRenderParams* params, uint8_t* rgb8,
       return rc;
     if (!st->d_counters) HIP_TRY(hipMalloc(&st->d_counters, 16 * CNT_PER_GROUP * sizeof(unsigned int)));
     if (!st->h_counters) HIP_TRY(hipHostMalloc(&st->h_counters, 16 * CNT_PER_GROUP * sizeof(unsigned int)));
-    if (!st->d_scene) HIP_TRY(hipMalloc(&st->d_scene, sizeof(DevScene)));
-    HIP_TRY(hipMemcpyAsync(st->d_scene, &st->S_launch, sizeof(DevScene), hipMemcpyHostToDevice, stream));
     // group 0 runs on the caller's stream, groups 1.. on their own streams
     // (GPU_MAX_HW_QUEUES is 4 by default: more streams than queues would
     // serialize groups behind each other)
@@ -1958,10 +1957,10 @@ rtx_status rtx_render(void* scene, const RtxRenderParams* params, uint8_t* rgb8,
         const int gbi = static_cast<int>(gb);
         HIP_TRY(hipMemsetAsync(cnt, 0, CNT_PER_GROUP * sizeof(unsigned int), sg));
         if (stats)
-          hipLaunchKernelGGL((advance_kernel<true>), dim3(per), dim3(WG), 0, sg, S, st->d_frame, A, sb, d_hits,
+          hipLaunchKernelGGL((advance_kernel<true>), dim3(per), dim3(WG), 0, sg, S, st->d_scene, st->d_frame, A, sb, d_hits,
                              st->d_pbuf, pend_cap, q0, q1, cnt, st->d_stats, static_cast<int>(g * gslots));
         else
-          hipLaunchKernelGGL((advance_kernel<false>), dim3(per), dim3(WG), 0, sg, S, st->d_frame, A, sb, d_hits,
+          hipLaunchKernelGGL((advance_kernel<false>), dim3(per), dim3(WG), 0, sg, S, st->d_scene, st->d_frame, A, sb, d_hits,
                              st->d_pbuf, pend_cap, q0, q1, cnt, st->d_stats, static_cast<int>(g * gslots));
         if (stats) {
           hipLaunchKernelGGL((trace_kernel<true, Q_CLOSEST>), dim3(tgrid), dim3(WG), lds, sg, S, st->d_scene, q0,
