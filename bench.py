@@ -213,6 +213,9 @@ def main():
                          "avg_kernel_ms": round(avg_kernel_ms, 3), "launches_per_frame": launches_per_frame,
                          "algorithmic_bytes_per_launch": algo_bytes},
             "cpu_baseline": cpu,
+            # traversal work of one frame (the counting pass of the same kernels)
+            "work": {k: st[k] for k in ("rays", "camera_rays", "secondary_rays", "shadow_rays", "node_visits",
+                                        "object_tests", "tri_tests", "shades")},
         }
         if cpu:
             line["gpu_over_cpu"] = round(value / cpu["value"], 2)

@@ -71,12 +71,7 @@ struct FrameParams {
   int64_t n_items;           // work items (pixel blocks)
   int64_t n_samples;         // n_items * ppw * spp  (sample ids)
   int qchunk;                // samples per queue atomic (multiple of 64)
-  // wavefront path: slots are numbered (group, band, local); band b owns
-  // samples [b * wf_band_n, (b+1) * wf_band_n) (see slot_sample)
-  int wf_gb;                 // slots per (group, band), a multiple of WG
-  int wf_nb;                 // bands
-  int wf_band_slots;         // slots per band over all groups
-  int64_t wf_band_n;         // samples per band
+  int wf_nslot;              // wavefront path: path slots (samples dealt slot + k * wf_nslot)
 };
 
 // Work item -> pixel; out_index is the output slot (packed tile order or
@@ -1005,55 +1000,33 @@ __global__ void __launch_bounds__(WG) render_kernel(DevScene S, const DevScene* 
 // Path slots: NSLOT lanes whose LaneRef state lives in HBM.  Each iteration:
 //   advance_kernel  — one thread per slot: take the last query's result, run
 //                     the state machine to the next ray query, append it to
-//                     its band's closest-hit or next-hit list (wave ballot +
-//                     popc + one atomic per wave, mbcnt for the offset:
-//                     compaction of the active-ray mask);
-//   trace_kernel<Q> — persistent traversal of the compacted lists; a lane
-//                     whose query ended takes the next one at once, results
-//                     go into the slots' state.
-// XCD affinity: the frame's samples are cut into wf_nb contiguous bands
-// (horizontal strips of the image, or runs of tiles), each with its own
-// slots and its own query sub-lists.  A trace wave drains the band numbered
-// like its XCD (HW_REG_XCC_ID) first and only then helps the others, so an
-// XCD's 4 MB L2 holds the nodes and faces one strip touches instead of the
-// whole scene's.
+//                     the closest-hit or next-hit list (wave ballot + popc +
+//                     one atomic per wave, mbcnt for the offset: compaction
+//                     of the active-ray mask);
+//   trace_kernel<Q> — persistent traversal of a compacted list, writing each
+//                     result into its slot's state.
+// Samples are dealt to slots statically (sample slot + k * NSLOT).
 struct QList {
   int* slot;    // [cap]
   double* d;    // Px Py Pz Dx Dy Dz tp tlimit tblock, field-major [QL_D][cap]
   int* iv;      // rp, sq  [2][cap]
-  size_t cap;   // band b's sub-list is [b * wf_gb, (b+1) * wf_gb)
+  size_t cap;
 };
 #define QL_D 9
-#define MAX_BANDS 8
-// per-group counters (unsigned ints): [m * MAX_BANDS + b] queries of mode
-// m (0 closest, 1 next) in band b; [CNT_ALIVE] live slots;
-// [CNT_CLAIM + m * MAX_BANDS + b] the trace kernel's claim cursors
-#define CNT_ALIVE 16
-#define CNT_CLAIM 32
-#define CNT_PER_GROUP 64
+// per-group counters (unsigned ints), each on its own 128-byte line (the
+// appends, claims and liveness atomics of three concurrent groups must not
+// share lines: packed 4 bytes apart the frame took 5% longer):
+// [CNT_Q + m * CNT_LINE] queries of mode m (0 closest, 1 next),
+// [CNT_ALIVE] live slots, [CNT_CLAIM + m * CNT_LINE] the trace claim cursors
+#define CNT_LINE 32
+#define CNT_Q 0
+#define CNT_ALIVE (2 * CNT_LINE)
+#define CNT_CLAIM (3 * CNT_LINE)
+#define CNT_PER_GROUP (5 * CNT_LINE)
 
 __device__ __forceinline__ unsigned int lane_prefix(unsigned long long mask) {
   return __builtin_amdgcn_mbcnt_hi(static_cast<unsigned int>(mask >> 32),
                                    __builtin_amdgcn_mbcnt_lo(static_cast<unsigned int>(mask), 0u));
-}
-
-// XCD (XCC) of the executing wave, 0..7 — for L2 affinity only, never for
-// correctness (placement is not part of the HIP contract).
-__device__ __forceinline__ int xcc_id() {
-  unsigned int v;
-  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(v));
-  return static_cast<int>(v & 7u);
-}
-
-// Sample id of a slot's kdone-th claim.  Slots are numbered (group, band,
-// local); band b deals its samples round-robin over its wf_band_slots slots.
-__device__ __forceinline__ int64_t slot_sample(const FrameParams& F, int slot, int kdone, int64_t& band_end) {
-  const int gslots = F.wf_gb * F.wf_nb;
-  const int g = slot / gslots, r = slot - g * gslots;
-  const int b = r / F.wf_gb, ls = r - b * F.wf_gb;
-  const int64_t start = static_cast<int64_t>(b) * F.wf_band_n;
-  band_end = start + F.wf_band_n < F.n_samples ? start + F.wf_band_n : F.n_samples;
-  return start + static_cast<int64_t>(g) * F.wf_gb + ls + static_cast<int64_t>(kdone) * F.wf_band_slots;
 }
 
 // Claim the next statically dealt sample for an idle slot (what the
@@ -1061,9 +1034,8 @@ __device__ __forceinline__ int64_t slot_sample(const FrameParams& F, int slot, i
 __device__ __forceinline__ void claim_sample(LaneRef& L, const FrameParams& F, RtxHitRecord* hits, int slot) {
   const RtxRenderParams& P = F.P;
   while (L.st() == ST_IDLE) {
-    int64_t band_end;
-    const int64_t sid = slot_sample(F, slot, L.kdone(), band_end);
-    if (sid >= band_end) return;
+    const int64_t sid = static_cast<int64_t>(slot) + static_cast<int64_t>(L.kdone()) * F.wf_nslot;
+    if (sid >= F.n_samples) return;
     L.kdone()++;
     const int64_t item = sid / (F.ppw * F.spp);
     const int sl = static_cast<int>(sid % (F.ppw * F.spp));
@@ -1098,14 +1070,11 @@ __global__ void __launch_bounds__(WG, RTX_ADV_WAVES) advance_kernel(DevScene S, 
                                                       unsigned int* __restrict__ counters,
                                                       unsigned long long* __restrict__ stats, int slot_off) {
   const FrameParams& F = *Fp;
-  const int local = blockIdx.x * WG + threadIdx.x;  // the grid covers this group's slots exactly
-  const int slot = slot_off + local;
-  const int band = local / F.wf_gb;                 // wf_gb is a multiple of WG: one band per workgroup
+  const int slot = slot_off + blockIdx.x * WG + threadIdx.x;  // the grid covers this group's slots exactly
   Counters C = {0, 0, 0, 0, 0, 0, 0};
   LaneRef L(lm, static_cast<size_t>(slot));
   int qm = Q_NONE;
-  int64_t band_end;
-  if (L.st() != ST_IDLE || slot_sample(F, slot, L.kdone(), band_end) < band_end) {
+  if (L.st() != ST_IDLE || static_cast<int64_t>(slot) + static_cast<int64_t>(L.kdone()) * F.wf_nslot < F.n_samples) {
     // the previous iteration's query result is already in L.bt()/bobj/bsub/bhave
     L.qmode() = Q_NONE;
     for (;;) {
@@ -1125,12 +1094,12 @@ __global__ void __launch_bounds__(WG, RTX_ADV_WAVES) advance_kernel(DevScene S, 
     if (mask == 0ull) continue;
     unsigned int base = 0;
     if (lane == 0)
-      base = atomicAdd(&counters[(m - 1) * MAX_BANDS + band], static_cast<unsigned int>(__popcll(mask)));
+      base = atomicAdd(&counters[CNT_Q + (m - 1) * CNT_LINE], static_cast<unsigned int>(__popcll(mask)));
     base = __shfl(base, 0);
     if (qm == m) {
       const QList& Q = m == Q_CLOSEST ? q0 : q1;
       const size_t cap = Q.cap;
-      const size_t k = static_cast<size_t>(band) * F.wf_gb + base + lane_prefix(mask);
+      const size_t k = base + lane_prefix(mask);
       dvec3 qP = L.rp(), qD = L.rd();
       double qlim = RTX_INF, qblk = -RTX_INF;
       if (m == Q_NEXT) {
@@ -1198,23 +1167,21 @@ struct ShadowBlocker {
 #define RTX_REFILL 1
 #endif
 
-// Persistent traversal of one group's compacted query lists.  A wave claims
-// 64 queries at a time (one atomic) from its XCD's band, then from the other
-// bands; inside the wave, lanes whose query ended take the next ones of the
-// claim (ballot + mbcnt) while the others keep stepping, so a wave's time
-// follows its total work rather than its slowest ray.
+// Persistent traversal of one group's compacted query list.  A wave claims
+// 64 queries at a time (one atomic); lanes whose query ended take the next
+// ones of the claim (ballot + mbcnt) once fewer than RTX_REFILL lanes are
+// still stepping.
 template <bool STATS, int MODE>
 __global__ void __launch_bounds__(WG, RTX_TRACE_WAVES)
-    trace_kernel(DevScene S, const DevScene* __restrict__ Sg, QList Q, unsigned int* __restrict__ counters, int gb,
-                 int nbands, LaneMem lm, int stack_cap, unsigned long long* __restrict__ stats) {
+    trace_kernel(DevScene S, const DevScene* __restrict__ Sg, QList Q, unsigned int* __restrict__ counters,
+                 LaneMem lm, int stack_cap, unsigned long long* __restrict__ stats) {
   extern __shared__ int lds_stack[];
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   int* stk = lds_stack + wave * stack_cap * 64;
   const size_t cap = Q.cap;
-  const unsigned int* n_band = counters + (MODE - 1) * MAX_BANDS;
-  unsigned int* claim = counters + CNT_CLAIM + (MODE - 1) * MAX_BANDS;
-  const int b0 = xcc_id() % nbands;
+  const unsigned int nq = counters[CNT_Q + (MODE - 1) * CNT_LINE];
+  unsigned int* claim = counters + CNT_CLAIM + (MODE - 1) * CNT_LINE;
 #ifdef RTX_EARLYOUT
   using Blk = typename std::conditional<MODE == Q_NEXT, ShadowBlocker, NoBlocker>::type;
 #else
@@ -1225,9 +1192,8 @@ __global__ void __launch_bounds__(WG, RTX_TRACE_WAVES)
   Trav T;
   bool active = false;
   size_t kq = 0;
-  // wave-uniform claim state: [qnext, qend) of band qb's sub-list
+  // wave-uniform claim state: [qnext, qend) of the list
   unsigned int qnext = 0, qend = 0;
-  int qb = 0, bi = 0;
   bool exhausted = false;
   auto finish = [&]() {
     const size_t slot = static_cast<size_t>(Q.slot[kq]);
@@ -1240,22 +1206,14 @@ __global__ void __launch_bounds__(WG, RTX_TRACE_WAVES)
     unsigned long long idle = __ballot(!active);
     while (idle != 0ull && !exhausted) {
       if (qnext >= qend) {
-        for (;;) {  // claim: this XCD's band first, then help the others
-          if (bi >= nbands) {
-            exhausted = true;
-            break;
-          }
-          qb = (b0 + bi) % nbands;
-          const unsigned int nq = n_band[qb];
-          unsigned int base = nq;
-          if (lane == 0 && nq > 0) base = atomicAdd(&claim[qb], 64u);
-          base = __shfl(base, 0);
-          if (base < nq) {
-            qnext = base;
-            qend = base + 64u < nq ? base + 64u : nq;
-            break;
-          }
-          ++bi;
+        unsigned int base = nq;
+        if (lane == 0) base = atomicAdd(claim, 64u);
+        base = __shfl(base, 0);
+        if (base >= nq) {
+          exhausted = true;
+        } else {
+          qnext = base;
+          qend = base + 64u < nq ? base + 64u : nq;
         }
         if (exhausted) break;
       }
@@ -1264,7 +1222,7 @@ __global__ void __launch_bounds__(WG, RTX_TRACE_WAVES)
       const unsigned int nidle = __popcll(idle);
       const unsigned int take = avail < nidle ? avail : nidle;
       if (!active && rank < take) {
-        kq = static_cast<size_t>(qb) * gb + qnext + rank;
+        kq = static_cast<size_t>(qnext) + rank;
         const dvec3 P = mk3(Q.d[0 * cap + kq], Q.d[1 * cap + kq], Q.d[2 * cap + kq]);
         const dvec3 D = mk3(Q.d[3 * cap + kq], Q.d[4 * cap + kq], Q.d[5 * cap + kq]);
         active = trav_init<STATS, MODE>(T, S, P, D, Q.d[6 * cap + kq], Q.iv[0 * cap + kq], Q.iv[1 * cap + kq],
@@ -1865,23 +1823,11 @@ rtx_status rtx_render(void* scene, const RtxRenderParams* params, uint8_t* rgb8,
     const char* g_env = getenv("RTX_GROUPS");
     if (g_env && atoi(g_env) > 0) G = atoi(g_env);
     if (G > 16) G = 16;
-    // XCD-affine bands: off by default (1).  With 8 bands the headline frame
-    // took 218 ms instead of 182: each band's slots walk only that strip's
-    // samples, so the costliest strip sets the iteration count.
-    int NB = 1;
-    const char* b_env = getenv("RTX_BANDS");
-    if (b_env && atoi(b_env) > 0) NB = atoi(b_env);
-    if (NB > MAX_BANDS) NB = MAX_BANDS;
     if (nslot64 > F.n_samples) nslot64 = F.n_samples;
-    const int64_t unit = static_cast<int64_t>(G) * NB * WG;
-    const int64_t gb = (nslot64 + unit - 1) / unit * WG;  // slots per (group, band)
-    const int64_t gslots = gb * NB;
-    const int64_t per = gslots / WG;                      // workgroups per group
+    const int64_t per = (nslot64 + G * WG - 1) / (G * WG);  // workgroups per group
+    const int64_t gslots = per * WG;
     nslot64 = gslots * G;
-    F.wf_gb = static_cast<int>(gb);
-    F.wf_nb = NB;
-    F.wf_band_slots = static_cast<int>(gb * G);
-    F.wf_band_n = (F.n_samples + NB - 1) / NB;
+    F.wf_nslot = static_cast<int>(nslot64);
     const size_t ns = static_cast<size_t>(nslot64);
     const size_t gs = static_cast<size_t>(gslots);
     const size_t bytes_q = gs * (sizeof(int) + QL_D * sizeof(double) + 2 * sizeof(int)) + 1024;
@@ -1954,7 +1900,6 @@ rtx_status rtx_render(void* scene, const RtxRenderParams* params, uint8_t* rgb8,
         unsigned int* cnt = st->d_counters + CNT_PER_GROUP * g;
         const QList& q0 = ql[size_t(g) * 2];
         const QList& q1 = ql[size_t(g) * 2 + 1];
-        const int gbi = static_cast<int>(gb);
         HIP_TRY(hipMemsetAsync(cnt, 0, CNT_PER_GROUP * sizeof(unsigned int), sg));
         if (stats)
           hipLaunchKernelGGL((advance_kernel<true>), dim3(per), dim3(WG), 0, sg, S, st->d_scene, st->d_frame, A, sb, d_hits,
@@ -1964,14 +1909,14 @@ rtx_status rtx_render(void* scene, const RtxRenderParams* params, uint8_t* rgb8,
                              st->d_pbuf, pend_cap, q0, q1, cnt, st->d_stats, static_cast<int>(g * gslots));
         if (stats) {
           hipLaunchKernelGGL((trace_kernel<true, Q_CLOSEST>), dim3(tgrid), dim3(WG), lds, sg, S, st->d_scene, q0,
-                             cnt, gbi, NB, A, st->stack_cap, st->d_stats);
+                             cnt, A, st->stack_cap, st->d_stats);
           hipLaunchKernelGGL((trace_kernel<true, Q_NEXT>), dim3(tgrid), dim3(WG), lds, sg, S, st->d_scene, q1, cnt,
-                             gbi, NB, A, st->stack_cap, st->d_stats);
+                             A, st->stack_cap, st->d_stats);
         } else {
           hipLaunchKernelGGL((trace_kernel<false, Q_CLOSEST>), dim3(tgrid), dim3(WG), lds, sg, S, st->d_scene, q0,
-                             cnt, gbi, NB, A, st->stack_cap, st->d_stats);
+                             cnt, A, st->stack_cap, st->d_stats);
           hipLaunchKernelGGL((trace_kernel<false, Q_NEXT>), dim3(tgrid), dim3(WG), lds, sg, S, st->d_scene, q1, cnt,
-                             gbi, NB, A, st->stack_cap, st->d_stats);
+                             A, st->stack_cap, st->d_stats);
         }
         HIP_TRY(hipGetLastError());
         if (it % check_every == check_every - 1) {
@@ -1982,15 +1927,9 @@ rtx_status rtx_render(void* scene, const RtxRenderParams* params, uint8_t* rgb8,
             HIP_TRY(hipEventSynchronize(st->wf_check[size_t(g)]));
             const unsigned int* hc = st->h_counters + CNT_PER_GROUP * g;
             const unsigned int alive = hc[CNT_ALIVE];
-            if (dbg) {
-              unsigned int nc = 0, nn = 0;
-              for (int b = 0; b < NB; ++b) {
-                nc += hc[b];
-                nn += hc[MAX_BANDS + b];
-              }
+            if (dbg)
               fprintf(stderr, "rtx group %d iter %d: alive %u (closest %u next %u)\n", g, pending_check[size_t(g)],
-                      alive, nc, nn);
-            }
+                      alive, hc[CNT_Q], hc[CNT_Q + CNT_LINE]);
             if (alive == 0) {
               done[size_t(g)] = 1;
               ++ndone;

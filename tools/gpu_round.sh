@@ -5,7 +5,7 @@ set -o pipefail
 cd $GRAFT_REPO_ROOT
 TAG=${1:-run}
 mkdir -p gpurun_out
-timeout -k 10 600 python -m pytest tests/ -x -q -m gpu --tb=short > gpurun_out/pytest_gpu_$TAG.log 2>&1; rc=$?
+timeout -k 10 600 python -u -m pytest tests/ -x -q -m gpu --tb=short --timeout 300 --timeout-method thread > gpurun_out/pytest_gpu_$TAG.log 2>&1; rc=$?
 echo pytest_rc=$rc; tail -3 gpurun_out/pytest_gpu_$TAG.log
 [ $rc -eq 0 ] || exit 1
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > gpurun_out/smoke_$TAG.log 2>&1 || { tail -5 gpurun_out/smoke_$TAG.log; exit 1; }
