@@ -1195,6 +1195,7 @@ __global__ void __launch_bounds__(WG, RTX_TRACE_WAVES)
   // wave-uniform claim state: [qnext, qend) of the list
   unsigned int qnext = 0, qend = 0;
   bool exhausted = false;
+  int64_t wsteps = 0, lsteps = 0;
   auto finish = [&]() {
     const size_t slot = static_cast<size_t>(Q.slot[kq]);
     lm.d[size_t(LD_bt) * lm.n + slot] = T.bt;
@@ -1235,6 +1236,10 @@ __global__ void __launch_bounds__(WG, RTX_TRACE_WAVES)
     if (__ballot(active) == 0ull) break;  // nothing claimed and nothing left
     const int thresh = exhausted ? 1 : RTX_REFILL;
     do {
+      if (STATS) {  // SIMD efficiency of the walk (RTX_DEBUG report)
+        wsteps++;
+        lsteps += __popcll(__ballot(active));
+      }
       if (active && trav_step<STATS, MODE>(T, S, stk, lane, blk, C)) {
         finish();
         active = false;
@@ -1248,6 +1253,10 @@ __global__ void __launch_bounds__(WG, RTX_TRACE_WAVES)
       int64_t x = v[k];
       for (int off = 32; off > 0; off >>= 1) x += __shfl_down(x, off);
       if (lane == 0 && x) atomicAdd(&stats[3 + k], static_cast<unsigned long long>(x));
+    }
+    if (lane == 0) {
+      atomicAdd(&stats[8 + 2 * (MODE - 1)], static_cast<unsigned long long>(wsteps));
+      atomicAdd(&stats[9 + 2 * (MODE - 1)], static_cast<unsigned long long>(lsteps));
     }
   }
 }
@@ -1516,7 +1525,7 @@ rtx_status rtx_scene_create(int device, const RtxSceneDesc* d, void** out) {
   st->lights.assign(d->lights, d->lights + d->n_lights);
   if (hipMalloc(&st->d_frame, sizeof(FrameParams)) != hipSuccess ||
       hipMalloc(&st->d_work, sizeof(unsigned long long)) != hipSuccess ||
-      hipMalloc(&st->d_stats, 8 * sizeof(unsigned long long)) != hipSuccess) {
+      hipMalloc(&st->d_stats, 16 * sizeof(unsigned long long)) != hipSuccess) {
     g_err = "rtx_scene_create: hipMalloc failed";
     rtx_scene_destroy(st);
     return RTX_ERR_HIP;
@@ -1719,7 +1728,7 @@ rtx_status rtx_render(void* scene, const RtxRenderParams* params, uint8_t* rgb8,
   // through this pointer (a kernel-argument copy has no address)
   if (!st->d_scene) HIP_TRY(hipMalloc(&st->d_scene, sizeof(DevScene)));
   HIP_TRY(hipMemcpyAsync(st->d_scene, &st->S_launch, sizeof(DevScene), hipMemcpyHostToDevice, stream));
-  if (stats) HIP_TRY(hipMemsetAsync(st->d_stats, 0, 8 * sizeof(unsigned long long), stream));
+  if (stats) HIP_TRY(hipMemsetAsync(st->d_stats, 0, 16 * sizeof(unsigned long long), stream));
   const int pend_cap = (params->depth > 0 ? params->depth : 0) + 2;
   auto get_event = [&](hipEvent_t* e) -> rtx_status {
     if (!st->ev_pool.empty()) {
@@ -1969,9 +1978,15 @@ rtx_status rtx_render(void* scene, const RtxRenderParams* params, uint8_t* rgb8,
     for (void* p : tmp) (void)hipFree(p);
   }
   if (stats) {
-    unsigned long long c[8];
+    unsigned long long c[16];
     HIP_TRY(hipMemcpyAsync(c, st->d_stats, sizeof(c), hipMemcpyDeviceToHost, stream));
     HIP_TRY(hipStreamSynchronize(stream));
+    {
+      const char* dbg = getenv("RTX_DEBUG");
+      if (dbg && atoi(dbg) != 0)
+        fprintf(stderr, "rtx trace SIMD efficiency: closest %llu wave steps, %.3f active; next %llu, %.3f\n", c[8],
+                c[8] ? double(c[9]) / (64.0 * c[8]) : 0.0, c[10], c[10] ? double(c[11]) / (64.0 * c[10]) : 0.0);
+    }
     std::memset(stats, 0, sizeof(*stats));
     stats->camera_rays = c[0];
     stats->secondary_rays = c[1];
