@@ -37,22 +37,31 @@ using rtm::mk3;
 // reference's binary KdTree collapsed to 4-wide records.  A record stands
 // for one internal node and holds the boxes of its children, where an
 // internal child is replaced by ITS two children (so 2..4 entries): one
-// 256-byte fetch tests up to four boxes and the walk needs half as many
-// dependent fetches as on the binary tree.  Skipping the intermediate box is
-// exact: node boxes are merges of their children's (kdTree.h:30-39), and the
-// slab test (bbox.cc:33-70) is monotone under box containment in floating
-// point too (per axis, (lo - o) / d rounds monotonically), so a child box is
-// only ever hit when its parent's is.  child[k] >= 0: index of the child's
-// record; child[k] < 0: the child is a leaf, ~child[k] = first_item << 2 |
-// count (count 1..3, kdTree.h:6).  Item ranks (DFS-leaf order) are
-// unchanged, so the winner of the lexicographic (t, rank) minimum does not
-// depend on the visiting order.
+// 128-byte line tests up to four boxes and the walk needs half as many
+// dependent fetches as on the binary tree.
+//
+// Exactness.  Node boxes are merges of their children's (kdTree.h:30-39) and
+// the slab test (bbox.cc:33-70) is monotone under box containment in
+// floating point too (per axis, (lo - o) / d rounds monotonically), so a box
+// is only ever hit when its ancestors' are: the reference's candidates are
+// exactly the faces whose LEAF box passes the exact slab test (and the
+// objects whose world box does — Geometry::intersect re-tests it).  Internal
+// boxes therefore only steer the walk, and any test that never rejects a
+// box the exact one accepts is as good.  The records store them as floats
+// rounded outward (a superset box) tested conservatively (box_cons); the
+// exact test runs where it decides a result: on each object's world box and
+// on the leaf box of every face hit that would enter the answer (leaf_ok).
+// child[k] >= 0: index of the child's record; child[k] < 0: the child is a
+// leaf, ~child[k] = first_item << 2 | count (count 1..3, kdTree.h:6).  Item
+// ranks (DFS-leaf order) are unchanged, so the winner of the lexicographic
+// (t, rank) minimum does not depend on the visiting order.
 struct DevNode4 {
-  double box[4][6];    // per entry: lo xyz, hi xyz
+  float lo[3][4];      // [axis][entry], rounded down
+  float hi[3][4];      // [axis][entry], rounded up
   int32_t child[4];
   int32_t count;       // entries, 2..4
-  int32_t pad[11];
-};                     // 256 bytes
+  int32_t pad[3];
+};                     // 128 bytes
 
 // Root of a BVH (scene or one mesh): its own box + the reference to descend.
 struct DevRoot {
@@ -170,6 +179,32 @@ RT_HD bool box_test(const double* lo, const double* hi, const dvec3& o, const dv
     return true;
   }
   return slab(lo, hi, o, d, a, b);
+}
+
+// Conservative slab on a record entry (float box, superset of the exact
+// one): never rejects a box the exact test accepts, and returns a lower bound
+// of the entry distance and an upper bound of the exit, so pruning with them
+// is safe.  Same reciprocal margins as box_test, minus the exact fallback.
+RT_HD bool box_cons(const DevNode4& nd, int k, const dvec3& o, const dvec3& d, const RayInv& ri, double& a,
+                    double& b) {
+  const double lo[3] = {nd.lo[0][k], nd.lo[1][k], nd.lo[2][k]};
+  const double hi[3] = {nd.hi[0][k], nd.hi[1][k], nd.hi[2][k]};
+  if (!ri.fast) return slab(lo, hi, o, d, a, b);
+  double tmin = -1.0e308, tmax = 1.0e308;
+#pragma unroll
+  for (int q = 0; q < 3; ++q) {
+    if (rtm::get(d, q) == 0.0) continue;
+    const double iv = rtm::get(ri.inv, q), oa = rtm::get(o, q);
+    const double t1 = (lo[q] - oa) * iv;
+    const double t2 = (hi[q] - oa) * iv;
+    tmin = fmax(tmin, fmin(t1, t2));
+    tmax = fmin(tmax, fmax(t1, t2));
+  }
+  const double e1 = 1e-15 * fabs(tmin) + 1e-300, e2 = 1e-15 * fabs(tmax) + 1e-300;
+  if (tmin - e1 > tmax + e2 || tmax + e2 < RTX_RAY_EPS) return false;  // certain miss
+  a = tmin - e1;
+  b = tmax + e2;
+  return true;
 }
 
 // ------------------------------------------------------------------ textures

@@ -5,6 +5,7 @@
 #pragma once
 
 #include <climits>
+#include <cmath>
 #include <cstring>
 #include <functional>
 #include <vector>
@@ -59,7 +60,7 @@ struct Trav {
   dvec3 lp, ld;
   RayInv lri;
   double len, mbest;
-  int moi, mbase, mfoff, mface;
+  int moi, mbase, mfoff, mnoff, mface;
   bool mhave;
 };
 
@@ -70,8 +71,17 @@ struct NoBlocker {
   RT_HD bool operator()(const Trav&, int, int) const { return false; }
 };
 
-// Visit one 4-wide record: test its entries' boxes (exact slab verdicts,
-// pruned to [lo, hi]), continue with the nearest entry hit and push the
+// A face hit counts only if its mesh-BVH leaf box passes the exact slab test
+// in the mesh's local frame (KdTree::intersectList collects the items of hit
+// leaves, kdTree.h:100-117): the walk's internal tests are conservative.
+RT_HD bool leaf_ok(const Trav& T, const DevScene& S, int f) {
+  const RtxNode& lf = S.mnodes[T.mnoff + S.fids[T.mfoff + f].leaf];
+  double a, b;
+  return slab(lf.bmin, lf.bmax, T.lp, T.ld, a, b);
+}
+
+// Visit one 4-wide record:// Visit one 4-wide record: test its entries' boxes (conservatively, pruned
+// to [lo, hi]), continue with the nearest entry hit and push the
 // other hits farthest first, so the walk stays near-first.  False if no
 // entry was hit (the caller pops).
 template <bool STATS>
@@ -85,7 +95,7 @@ RT_HD bool visit4(const DevNode4& nd, const dvec3& o, const dvec3& d, const RayI
     if (k < cnt) {
       if (STATS) C.nodes++;
       double ta, tb;
-      if (box_test(nd.box[k], nd.box[k] + 3, o, d, ri, ta, tb) && !(ta > hi) && !(tb < lo)) {
+      if (box_cons(nd, k, o, d, ri, ta, tb) && !(ta > hi) && !(tb < lo)) {
         ak = ta;
         rk = nd.child[k];
       }
@@ -155,6 +165,7 @@ RT_HD bool trav_init(Trav& T, const DevScene& S, const dvec3& P, const dvec3& D,
   T.moi = 0;
   T.mbase = 0;
   T.mfoff = 0;
+  T.mnoff = 0;
   T.mface = -1;
   T.mhave = false;
   return true;
@@ -214,6 +225,7 @@ RT_HD bool trav_step(Trav& T, const DevScene& S, int* __restrict__ stk, const in
             T.moi = oi;
             T.mbase = sp;
             T.mfoff = S.meshes[o.mesh].face_off;
+            T.mnoff = S.meshes[o.mesh].node_off;
             ref = mr.ref;
             T.mhave = false;
             T.mbest = RTX_INF;
@@ -364,14 +376,14 @@ RT_HD bool trav_step(Trav& T, const DevScene& S, int* __restrict__ stk, const in
       double tf;
       if (tri_hit(S.faces[T.mfoff + f], T.lp, T.ld, tcap, tf)) {
         if (closest) {
-          if (!T.mhave || tf < T.mbest || (tf == T.mbest && f < T.mface)) {
+          if ((!T.mhave || tf < T.mbest || (tf == T.mbest && f < T.mface)) && leaf_ok(T, S, f)) {
             T.mbest = tf;
             T.mface = f;
             T.mhave = true;
           }
         } else {
           const double tw = tf / len;
-          if (key_less(tp, rp, sq, tw, T.moi, f) && tw <= tlimit) {
+          if (key_less(tp, rp, sq, tw, T.moi, f) && tw <= tlimit && leaf_ok(T, S, f)) {
             if (tw < T.tblock && blocker(T, T.moi, f)) {
               bt = tw;
               bobj = T.moi;
@@ -440,7 +452,19 @@ RT_HD bool traverse(const DevScene& S, const int qmode, const dvec3& P, const dv
 }
 
 
-// 4-wide records (DevNode4) of one DFS-pre-order RtxNode tree nodes[0..n)
+// float bounds of a double box rounded outward (the record holds a superset)
+inline float round_down_f(double x) {
+  float f = static_cast<float>(x);
+  if (static_cast<double>(f) > x) f = std::nextafter(f, -HUGE_VALF);
+  return f;
+}
+inline float round_up_f(double x) {
+  float f = static_cast<float>(x);
+  if (static_cast<double>(f) < x) f = std::nextafter(f, HUGE_VALF);
+  return f;
+}
+
+// 4-wide records (DevNode4) of one DFS-pre-order RtxNode tree// 4-wide records (DevNode4) of one DFS-pre-order RtxNode tree nodes[0..n)
 // (child0 = i + 1, child1 = right, tree-relative; leaf items [first,
 // first + count)), emitted in DFS pre-order after the records already in
 // `out`.  stack_need: the most stack entries a walk of this tree can hold
@@ -467,12 +491,19 @@ inline bool build_node4(const RtxNode* nodes, int n, std::vector<DevNode4>& out,
       }
     }
     r.count = ne;
+    for (int k = ne; k < 4; ++k) {  // unused entries: empty boxes, never visited (k >= count)
+      for (int a = 0; a < 3; ++a) {
+        r.lo[a][k] = HUGE_VALF;
+        r.hi[a][k] = -HUGE_VALF;
+      }
+      r.child[k] = 0;
+    }
     int sub = 0;
     for (int k = 0; k < ne; ++k) {
       const int e = ents[k];
       for (int a = 0; a < 3; ++a) {
-        r.box[k][a] = nodes[e].bmin[a];
-        r.box[k][3 + a] = nodes[e].bmax[a];
+        r.lo[a][k] = round_down_f(nodes[e].bmin[a]);
+        r.hi[a][k] = round_up_f(nodes[e].bmax[a]);
       }
       if (nodes[e].count == 0) {
         int below = 0;
