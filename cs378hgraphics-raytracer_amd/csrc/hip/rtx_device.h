@@ -82,6 +82,8 @@ struct DevScene {
   const RtxNode* mnodes;
   const RtxFace* faces;
   const RtxFaceIds* fids;
+  const RtxFace* tfaces;   // faces in traversal-tree leaf order (per mesh)
+  const int32_t* trank;    // reference rank (index in faces) of each tfaces entry
   const double* vnormals;
   const RtxVertexMaterial* vmats;
   const RtxLight* lights;
@@ -201,7 +203,10 @@ RT_HD bool box_cons(const DevNode4& nd, int k, const dvec3& o, const dvec3& d, c
     tmax = fmin(tmax, fmax(t1, t2));
   }
   const double e1 = 1e-15 * fabs(tmin) + 1e-300, e2 = 1e-15 * fabs(tmax) + 1e-300;
-  if (tmin - e1 > tmax + e2 || tmax + e2 < RTX_RAY_EPS) return false;  // certain miss
+  // certain miss.  No 1e-8 cut on the exit here (bbox.cc:66-67): a box of
+  // the device's own trees may be tighter than the reference leaf around a
+  // hit with t < 1e-8; leaf_ok applies the reference's cut exactly.
+  if (tmin - e1 > tmax + e2 || tmax + e2 < 0.0) return false;
   a = tmin - e1;
   b = tmax + e2;
   return true;

@@ -1467,31 +1467,22 @@ rtx_status rtx_scene_create(int device, const RtxSceneDesc* d, void** out) {
   UP(d->texels, d->n_texels, S.texels);
 #undef UP
   {
-    std::vector<DevNode4> sn4, mn4;
-    std::vector<DevRoot> mroots(size_t(d->n_meshes));
-    bool ok = true;
-    int sneed = 0, mneed = 0;
-    std::memset(&S.sroot, 0, sizeof(S.sroot));
-    if (d->n_scene_nodes > 0) ok = build_node4(d->scene_nodes, d->n_scene_nodes, sn4, S.sroot, sneed);
-    for (int m = 0; ok && m < d->n_meshes; ++m) {
-      const RtxMesh& me = d->meshes[m];
-      std::memset(&mroots[size_t(m)], 0, sizeof(DevRoot));
-      int need = 0;
-      if (me.node_count > 0) ok = build_node4(d->mesh_nodes + me.node_off, me.node_count, mn4, mroots[size_t(m)], need);
-      mneed = need > mneed ? need : mneed;
-    }
-    if (!ok) {
+    TravTrees tt;
+    if (!build_trav_trees(d, tt)) {
       g_err = "rtx_scene_create: malformed BVH (leaf with more than 3 items or bad child link)";
       rtx_scene_destroy(st);
       return RTX_ERR_INVALID;
     }
+    S.sroot = tt.sroot;
     // per-lane LDS stack: scene-level entries stay below a mesh walk's
-    st->stack_cap = sneed + mneed + 2;
+    st->stack_cap = tt.sneed + tt.mneed + 2;
 #define UP(src, n, dst) \
   if ((rc = upload(*st, src, size_t(n), &dst)) != RTX_OK) { rtx_scene_destroy(st); return rc; }
-    UP(sn4.data(), sn4.size(), S.snode4);
-    UP(mn4.data(), mn4.size(), S.mnode4);
-    UP(mroots.data(), mroots.size(), S.mroots);
+    UP(tt.sn4.data(), tt.sn4.size(), S.snode4);
+    UP(tt.mn4.data(), tt.mn4.size(), S.mnode4);
+    UP(tt.mroots.data(), tt.mroots.size(), S.mroots);
+    UP(tt.tfaces.data(), tt.tfaces.size(), S.tfaces);
+    UP(tt.trank.data(), tt.trank.size(), S.trank);
 #undef UP
   }
   S.n_snodes = d->n_scene_nodes;

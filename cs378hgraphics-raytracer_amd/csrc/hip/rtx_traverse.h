@@ -4,6 +4,7 @@
 // restatement without a GPU).
 #pragma once
 
+#include <algorithm>
 #include <climits>
 #include <cmath>
 #include <cstring>
@@ -374,28 +375,29 @@ RT_HD bool trav_step(Trav& T, const DevScene& S, int* __restrict__ stk, const in
     for (int f = f0; f < f1; ++f) {
       if (STATS) C.tris++;
       double tf;
-      if (tri_hit(S.faces[T.mfoff + f], T.lp, T.ld, tcap, tf)) {
+      if (tri_hit(S.tfaces[T.mfoff + f], T.lp, T.ld, tcap, tf)) {
+        const int rk = S.trank[T.mfoff + f];  // the face's reference rank (ties, answer)
         if (closest) {
-          if ((!T.mhave || tf < T.mbest || (tf == T.mbest && f < T.mface)) && leaf_ok(T, S, f)) {
+          if ((!T.mhave || tf < T.mbest || (tf == T.mbest && rk < T.mface)) && leaf_ok(T, S, rk)) {
             T.mbest = tf;
-            T.mface = f;
+            T.mface = rk;
             T.mhave = true;
           }
         } else {
           const double tw = tf / len;
-          if (key_less(tp, rp, sq, tw, T.moi, f) && tw <= tlimit && leaf_ok(T, S, f)) {
-            if (tw < T.tblock && blocker(T, T.moi, f)) {
+          if (key_less(tp, rp, sq, tw, T.moi, rk) && tw <= tlimit && leaf_ok(T, S, rk)) {
+            if (tw < T.tblock && blocker(T, T.moi, rk)) {
               bt = tw;
               bobj = T.moi;
-              bsub = f;
+              bsub = rk;
               have = true;
               T.blocked = true;
               return true;
             }
-            if (!have || key_less(tw, T.moi, f, bt, bobj, bsub)) {
+            if (!have || key_less(tw, T.moi, rk, bt, bobj, bsub)) {
               bt = tw;
               bobj = T.moi;
-              bsub = f;
+              bsub = rk;
               have = true;
             }
           }
@@ -524,6 +526,213 @@ inline bool build_node4(const RtxNode* nodes, int n, std::vector<DevNode4>& out,
   }
   stack_need = 0;
   root.ref = nodes[0].count == 0 ? emit(0, stack_need) : leaf_code(0);
+  return true;
+}
+
+// ------------------------------------------------------------------ traversal trees
+// The device walks BVHs of its own, built here from the flat scene:
+// binned-SAH trees over face boxes (leaves of <= 3 faces) per mesh, and a
+// one-object-per-leaf tree over the objects' world boxes.  Results are the
+// reference's all the same (DESIGN.md "Traversal trees"): an object is a
+// candidate iff its exact world-box test passes (Geometry::intersect,
+// scene.cpp:15, implies its leaf's), a face iff its REFERENCE leaf box
+// passes the exact slab test (leaf_ok) — both are tested exactly where they
+// decide — and every box of these trees contains its items, so the
+// conservative walk reaches every object and every face a ray hits.  Ties
+// keep the reference ranks (object index, face index in DFS-leaf order).
+struct TBox {
+  double lo[3], hi[3];
+};
+
+inline double tbox_area(const TBox& b) {
+  const double x = b.hi[0] - b.lo[0], y = b.hi[1] - b.lo[1], z = b.hi[2] - b.lo[2];
+  return x * y + y * z + z * x;
+}
+inline void tbox_grow(TBox& a, const TBox& b) {
+  for (int k = 0; k < 3; ++k) {
+    a.lo[k] = b.lo[k] < a.lo[k] ? b.lo[k] : a.lo[k];
+    a.hi[k] = b.hi[k] > a.hi[k] ? b.hi[k] : a.hi[k];
+  }
+}
+inline TBox tbox_empty() {
+  TBox b;
+  for (int k = 0; k < 3; ++k) {
+    b.lo[k] = HUGE_VAL;
+    b.hi[k] = -HUGE_VAL;
+  }
+  return b;
+}
+
+// Binned SAH (16 bins, traversal cost 1.2 per node against 1 per item) over
+// item boxes.  Emits nodes in DFS pre-order (child0 = i + 1, right), leaves
+// [first, first + count) into `order`, a permutation of the items.
+inline void tree_build(const std::vector<TBox>& box, int max_leaf, std::vector<RtxNode>& nodes,
+                       std::vector<int>& order) {
+  const int n = static_cast<int>(box.size());
+  order.resize(size_t(n));
+  for (int i = 0; i < n; ++i) order[size_t(i)] = i;
+  nodes.clear();
+  if (n == 0) return;
+  std::vector<double> cen(size_t(n) * 3);
+  for (int i = 0; i < n; ++i)
+    for (int k = 0; k < 3; ++k) cen[size_t(i) * 3 + k] = 0.5 * (box[size_t(i)].lo[k] + box[size_t(i)].hi[k]);
+  const int NBIN = 16;
+  std::function<void(int, int, int)> rec = [&](int l, int r, int depth) {
+    const int me = static_cast<int>(nodes.size());
+    nodes.emplace_back();
+    TBox b = tbox_empty(), cb = tbox_empty();
+    for (int i = l; i < r; ++i) {
+      const int it = order[size_t(i)];
+      tbox_grow(b, box[size_t(it)]);
+      TBox c;
+      for (int k = 0; k < 3; ++k) c.lo[k] = c.hi[k] = cen[size_t(it) * 3 + k];
+      tbox_grow(cb, c);
+    }
+    RtxNode nd;
+    std::memset(&nd, 0, sizeof(nd));
+    for (int k = 0; k < 3; ++k) {
+      nd.bmin[k] = b.lo[k];
+      nd.bmax[k] = b.hi[k];
+    }
+    nd.depth = depth;
+    const int cnt = r - l;
+    auto make_leaf = [&]() {
+      nd.right = -1;
+      nd.first = l;
+      nd.count = cnt;
+      nodes[size_t(me)] = nd;
+    };
+    if (cnt == 1) {
+      make_leaf();
+      return;
+    }
+    // best binned split over the three axes
+    double best = HUGE_VAL;
+    int bax = -1, bbin = -1;
+    for (int k = 0; k < 3; ++k) {
+      const double ext = cb.hi[k] - cb.lo[k];
+      if (!(ext > 0.0)) continue;
+      int bc[NBIN] = {0};
+      TBox bb[NBIN];
+      for (int q = 0; q < NBIN; ++q) bb[q] = tbox_empty();
+      for (int i = l; i < r; ++i) {
+        const int it = order[size_t(i)];
+        int q = static_cast<int>((cen[size_t(it) * 3 + k] - cb.lo[k]) / ext * NBIN);
+        q = q < 0 ? 0 : (q >= NBIN ? NBIN - 1 : q);
+        bc[q]++;
+        tbox_grow(bb[q], box[size_t(it)]);
+      }
+      double ra[NBIN];
+      int rc[NBIN];
+      TBox acc = tbox_empty();
+      int ac = 0;
+      for (int q = NBIN - 1; q > 0; --q) {
+        tbox_grow(acc, bb[q]);
+        ac += bc[q];
+        ra[q] = tbox_area(acc);
+        rc[q] = ac;
+      }
+      acc = tbox_empty();
+      ac = 0;
+      for (int q = 0; q < NBIN - 1; ++q) {
+        tbox_grow(acc, bb[q]);
+        ac += bc[q];
+        if (ac == 0 || rc[q + 1] == 0) continue;
+        const double c = tbox_area(acc) * ac + ra[q + 1] * rc[q + 1];
+        if (c < best) {
+          best = c;
+          bax = k;
+          bbin = q;
+        }
+      }
+    }
+    const double area = tbox_area(b);
+    const double split_cost = area > 0.0 && bax >= 0 ? 1.2 + best / area : HUGE_VAL;
+    if (cnt <= max_leaf && cnt <= split_cost) {
+      make_leaf();
+      return;
+    }
+    int m = l + cnt / 2;
+    if (bax >= 0) {
+      const double ext = cb.hi[bax] - cb.lo[bax];
+      auto left = [&](int it) {
+        int q = static_cast<int>((cen[size_t(it) * 3 + bax] - cb.lo[bax]) / ext * NBIN);
+        q = q < 0 ? 0 : (q >= NBIN ? NBIN - 1 : q);
+        return q <= bbin;
+      };
+      m = static_cast<int>(std::partition(order.begin() + l, order.begin() + r, left) - order.begin());
+      if (m == l || m == r) m = l + cnt / 2;
+    }
+    rec(l, m, depth + 1);
+    nd.right = static_cast<int>(nodes.size());
+    nd.first = -1;
+    nd.count = 0;
+    nodes[size_t(me)] = nd;
+    rec(m, r, depth + 1);
+  };
+  rec(0, n, 0);
+}
+
+// Everything rtx_scene_create uploads for the walk.
+struct TravTrees {
+  std::vector<DevNode4> sn4, mn4;
+  std::vector<DevRoot> mroots;
+  DevRoot sroot;
+  std::vector<RtxFace> tfaces;
+  std::vector<int32_t> trank;
+  int sneed = 0, mneed = 0;
+};
+
+inline bool build_trav_trees(const RtxSceneDesc* d, TravTrees& T) {
+  std::memset(&T.sroot, 0, sizeof(T.sroot));
+  std::vector<RtxNode> nodes;
+  std::vector<int> order;
+  std::vector<TBox> boxes;
+  if (d->n_objects > 0 && d->n_scene_nodes > 0) {
+    boxes.resize(size_t(d->n_objects));
+    for (int i = 0; i < d->n_objects; ++i)
+      for (int k = 0; k < 3; ++k) {
+        boxes[size_t(i)].lo[k] = d->objects[i].wmin[k];
+        boxes[size_t(i)].hi[k] = d->objects[i].wmax[k];
+      }
+    tree_build(boxes, 1, nodes, order);
+    for (auto& nd : nodes)
+      if (nd.count > 0) nd.first = order[size_t(nd.first)];  // one object per leaf: the leaf names it
+    if (!build_node4(nodes.data(), static_cast<int>(nodes.size()), T.sn4, T.sroot, T.sneed)) return false;
+    for (int k = 0; k < 3; ++k) {  // the root test is the reference's own (KdTree::intersectList)
+      T.sroot.lo[k] = d->scene_nodes[0].bmin[k];
+      T.sroot.hi[k] = d->scene_nodes[0].bmax[k];
+    }
+  }
+  T.mroots.assign(size_t(d->n_meshes), DevRoot());
+  T.tfaces.assign(size_t(d->n_faces), RtxFace());
+  T.trank.assign(size_t(d->n_faces), 0);
+  for (int m = 0; m < d->n_meshes; ++m) {
+    const RtxMesh& me = d->meshes[m];
+    std::memset(&T.mroots[size_t(m)], 0, sizeof(DevRoot));
+    if (me.node_count <= 0 || me.face_count <= 0) continue;
+    boxes.resize(size_t(me.face_count));
+    for (int f = 0; f < me.face_count; ++f) {
+      const RtxFace& F = d->faces[me.face_off + f];
+      for (int k = 0; k < 3; ++k) {
+        boxes[size_t(f)].lo[k] = fmin(fmin(F.v0[k], F.v1[k]), F.v2[k]);
+        boxes[size_t(f)].hi[k] = fmax(fmax(F.v0[k], F.v1[k]), F.v2[k]);
+      }
+    }
+    tree_build(boxes, 3, nodes, order);
+    for (int j = 0; j < me.face_count; ++j) {
+      T.tfaces[size_t(me.face_off + j)] = d->faces[me.face_off + order[size_t(j)]];
+      T.trank[size_t(me.face_off + j)] = order[size_t(j)];
+    }
+    int need = 0;
+    if (!build_node4(nodes.data(), static_cast<int>(nodes.size()), T.mn4, T.mroots[size_t(m)], need)) return false;
+    const RtxNode& rr = d->mesh_nodes[me.node_off];  // the reference's root test
+    for (int k = 0; k < 3; ++k) {
+      T.mroots[size_t(m)].lo[k] = rr.bmin[k];
+      T.mroots[size_t(m)].hi[k] = rr.bmax[k];
+    }
+    T.mneed = need > T.mneed ? need : T.mneed;
+  }
   return true;
 }
 

@@ -18,28 +18,20 @@ std::string g_err;
 
 struct HostScene {
   DevScene S;
-  std::vector<DevNode4> sn4, mn4;
-  std::vector<DevRoot> mroots;
+  TravTrees T;
   int stack_cap = 0;
 };
 
 bool make_scene(const RtxSceneDesc* d, HostScene& H) {
   std::memset(&H.S, 0, sizeof(H.S));
   DevScene& S = H.S;
-  int sneed = 0, mneed = 0;
-  if (d->n_scene_nodes > 0 && !build_node4(d->scene_nodes, d->n_scene_nodes, H.sn4, S.sroot, sneed)) return false;
-  H.mroots.resize(size_t(d->n_meshes));
-  for (int m = 0; m < d->n_meshes; ++m) {
-    const RtxMesh& me = d->meshes[m];
-    std::memset(&H.mroots[size_t(m)], 0, sizeof(DevRoot));
-    int need = 0;
-    if (me.node_count > 0 && !build_node4(d->mesh_nodes + me.node_off, me.node_count, H.mn4, H.mroots[size_t(m)], need))
-      return false;
-    mneed = need > mneed ? need : mneed;
-  }
-  S.snode4 = H.sn4.data();
-  S.mnode4 = H.mn4.data();
-  S.mroots = H.mroots.data();
+  if (!build_trav_trees(d, H.T)) return false;
+  S.sroot = H.T.sroot;
+  S.snode4 = H.T.sn4.data();
+  S.mnode4 = H.T.mn4.data();
+  S.mroots = H.T.mroots.data();
+  S.tfaces = H.T.tfaces.data();
+  S.trank = H.T.trank.data();
   S.snodes = d->scene_nodes;
   S.objs = d->objects;
   S.mats = d->materials;
@@ -51,7 +43,7 @@ bool make_scene(const RtxSceneDesc* d, HostScene& H) {
   S.n_objs = d->n_objects;
   S.margin = 1e-9 * scene_extent(d);
   S.lmargin = 1e-9 * mesh_extent(d);
-  H.stack_cap = sneed + mneed + 2;
+  H.stack_cap = H.T.sneed + H.T.mneed + 2;
   return true;
 }
 }  // namespace
