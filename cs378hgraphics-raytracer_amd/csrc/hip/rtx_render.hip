@@ -72,6 +72,8 @@ struct FrameParams {
   int64_t n_samples;         // n_items * ppw * spp  (sample ids)
   int qchunk;                // samples per queue atomic (multiple of 64)
   int wf_nslot;              // wavefront path: path slots (samples dealt slot + k * wf_nslot)
+  int ncam;                  // camera rays per sample (1, or divs + 1 with DoF)
+  int cam_split;             // 1: each DoF camera ray is its own work unit (wavefront path)
 };
 
 // Work item -> pixel; out_index is the output slot (packed tile order or
@@ -297,7 +299,7 @@ struct Pending {
 // fields of its current step, and the traversal's registers are not shared
 // with it.  LaneRef gives a lane's fields as accessors (LR.st(), LR.acc(), ...).
 #define LANE_INT_FIELDS(X) X(st) X(sample_slot) X(rec_on) X(pass) X(camk) X(nrays) X(top) X(rdepth) X(rkind) \
-  X(first_query) X(sobj) X(ssub) X(m_flags) X(li) X(pick) X(qmode) X(qrp) X(qsq) X(kdone) X(bobj) X(bsub) X(bhave)
+  X(first_query) X(cam_end) X(sobj) X(ssub) X(m_flags) X(li) X(pick) X(qmode) X(qrp) X(qsq) X(kdone) X(bobj) X(bsub) X(bhave)
 #define LANE_DBL_FIELDS(X) X(sx) X(sy) X(st_t) X(m_sh) X(dattn) X(last_t) X(qtp) X(bt)
 #define LANE_VEC_FIELDS(X) X(acc) X(rp) X(rd) X(W) X(N) X(i_out) X(dscomp) X(m_kd) X(m_ks) X(area_sum) X(sdir) \
   X(wpos) X(sattn)
@@ -405,7 +407,21 @@ __device__ __forceinline__ void advance_lane(LaneRef& LR, const DevScene& S, con
     switch (LR.st()) {
       case ST_CAM: {
         // next camera ray of trace(x, y) (RayTracer.cpp:35-79)
-        if (LR.camk() == ncam) {
+        if (LR.camk() == LR.cam_end()) {
+          if (F.cam_split) {
+            // one camera ray of a DoF sample (RayTracer.cpp:47-75): its own
+            // sum; reduce_kernel adds the sample's rays in order, scales and
+            // clamps
+            const int64_t u = static_cast<int64_t>(LR.sample_slot()) * F.ncam + (LR.cam_end() - 1);
+            sbuf[u * 3 + 0] = LR.acc().x;
+            sbuf[u * 3 + 1] = LR.acc().y;
+            sbuf[u * 3 + 2] = LR.acc().z;
+            // per-sample ray count over the sample's units; the record starts
+            // at -1 (0xff fill), the first ray's unit adds the 1 back
+            if (LR.rec_on()) atomicAdd(&hits[LR.sample_slot()].nrays, LR.nrays() + (LR.cam_end() == 1 ? 1 : 0));
+            LR.st() = ST_IDLE;
+            break;
+          }
           dvec3 ret = LR.acc();
           if (P.dof) ret *= (1.0 / (P.dof_div + 1.0));
           ret = rtm::gclamp3(ret, 0.0, 1.0);
@@ -803,6 +819,7 @@ __global__ void __launch_bounds__(WG) render_kernel(DevScene S, const DevScene* 
             LR.rec_on() = hits != nullptr;
             LR.pass() = 0;
             LR.camk() = 0;
+            LR.cam_end() = ncam;
             LR.nrays() = 0;
             LR.acc() = mk3(0, 0, 0);
             LR.st() = ST_CAM;
@@ -957,6 +974,7 @@ __global__ void __launch_bounds__(WG) render_kernel(DevScene S, const DevScene* 
           LR.rec_on() = hits != nullptr && atop;
           LR.pass() = 0;
           LR.camk() = 0;
+          LR.cam_end() = ncam;
           LR.nrays() = 0;
           LR.acc() = mk3(0, 0, 0);
           LR.st() = ST_CAM;
@@ -1034,9 +1052,12 @@ __device__ __forceinline__ unsigned int lane_prefix(unsigned long long mask) {
 __device__ __forceinline__ void claim_sample(LaneRef& L, const FrameParams& F, RtxHitRecord* hits, int slot) {
   const RtxRenderParams& P = F.P;
   while (L.st() == ST_IDLE) {
-    const int64_t sid = static_cast<int64_t>(slot) + static_cast<int64_t>(L.kdone()) * F.wf_nslot;
-    if (sid >= F.n_samples) return;
+    const int64_t unit = static_cast<int64_t>(slot) + static_cast<int64_t>(L.kdone()) * F.wf_nslot;
+    if (unit >= F.n_samples) return;
     L.kdone()++;
+    // work unit -> sample (and, with cam_split, which of its camera rays)
+    const int64_t sid = F.cam_split ? unit / F.ncam : unit;
+    const int cam0 = F.cam_split ? static_cast<int>(unit - sid * F.ncam) : 0;
     const int64_t item = sid / (F.ppw * F.spp);
     const int sl = static_cast<int>(sid % (F.ppw * F.spp));
     const int pix = sl / F.spp, smp = sl % F.spp;
@@ -1056,7 +1077,8 @@ __device__ __forceinline__ void claim_sample(LaneRef& L, const FrameParams& F, R
     L.sample_slot() = static_cast<int>(oidx * F.spp + smp);
     L.rec_on() = hits != nullptr;
     L.pass() = 0;
-    L.camk() = 0;
+    L.camk() = cam0;
+    L.cam_end() = F.cam_split ? cam0 + 1 : F.ncam;
     L.nrays() = 0;
     L.acc() = mk3(0, 0, 0);
     L.st() = ST_CAM;
@@ -1282,9 +1304,24 @@ __global__ void __launch_bounds__(WG) reduce_kernel(const FrameParams* __restric
     const int tile_id = (j / F.th) * F.tiles_x + (i / F.tw);
     if (tile_id % F.P.nshards != F.P.shard) return;
   }
-  const double* s = sbuf + o * F.spp * 3;
   dvec3 acc = mk3(0.0, 0.0, 0.0);
-  for (int q = 0; q < F.spp; ++q) acc += mk3(s[q * 3 + 0], s[q * 3 + 1], s[q * 3 + 2]);
+  if (F.cam_split) {
+    // DoF split: a sample = its camera rays' sums added in order, then
+    // trace()'s scale and clamp (RayTracer.cpp:73-77)
+    const double* s = sbuf + o * F.spp * F.ncam * 3;
+    for (int q = 0; q < F.spp; ++q) {
+      dvec3 ret = mk3(s[q * F.ncam * 3 + 0], s[q * F.ncam * 3 + 1], s[q * F.ncam * 3 + 2]);
+      for (int k = 1; k < F.ncam; ++k) {
+        const double* r = s + (q * F.ncam + k) * 3;
+        ret += mk3(r[0], r[1], r[2]);
+      }
+      ret *= (1.0 / (F.P.dof_div + 1.0));
+      acc += rtm::gclamp3(ret, 0.0, 1.0);
+    }
+  } else {
+    const double* s = sbuf + o * F.spp * 3;
+    for (int q = 0; q < F.spp; ++q) acc += mk3(s[q * 3 + 0], s[q * 3 + 1], s[q * 3 + 2]);
+  }
   if (F.P.aa_mode != RTX_AA_NONE) acc = acc / double(F.s * F.s);
   if (rgb8) {
     rgb8[o * 3 + 0] = (uint8_t)(int)(255.0 * acc.x);
@@ -1622,6 +1659,8 @@ static rtx_status build_frame(const SceneState* st, const RtxRenderParams* p, Fr
   F.items_per_tile = F.bx_per_tile * ((F.th + F.bh - 1) / F.bh);
   F.n_items = static_cast<int64_t>(F.items_per_tile) * F.n_owned;
   F.n_samples = F.n_items * F.ppw * F.spp;
+  F.ncam = p->dof ? p->dof_div + 1 : 1;
+  F.cam_split = 0;
   // DoF eye offsets: (cos(a) * V + sin(a) * U) * sz (RayTracer.cpp:62-67)
   if (p->dof) {
     const double PI = 3.1415926535897932384626433832795028841971;
@@ -1704,8 +1743,20 @@ rtx_status rtx_render(void* scene, const RtxRenderParams* params, uint8_t* rgb8,
     }
   }
   const bool adaptive = params->aa_mode == RTX_AA_ADAPTIVE;
+  // wavefront path by default; adaptive AA (per-pixel sample frames) and
+  // RTX_MEGAKERNEL=1 use the persistent megakernel (DESIGN.md: kernels)
+  const char* mk_env = getenv("RTX_MEGAKERNEL");
+  const bool megakernel = adaptive || (mk_env && atoi(mk_env) != 0);
+  // DoF on the wavefront path: each of a sample's divs + 1 camera rays is a
+  // work unit of its own (17x the parallel units, paths 17x shorter)
+  const char* split_env = getenv("RTX_DOF_SPLIT");
+  if (!megakernel && params->dof && !params->anaglyph && !(split_env && atoi(split_env) == 0)) {
+    F.cam_split = 1;
+    F.n_samples *= F.ncam;
+  }
+  if (F.cam_split && hits) HIP_TRY(hipMemsetAsync(d_hits, 0xff, npix * F.spp * sizeof(RtxHitRecord), stream));
   if (!adaptive) {
-    const size_t need = size_t(npix) * F.spp * 3 * sizeof(double);
+    const size_t need = size_t(npix) * F.spp * (F.cam_split ? F.ncam : 1) * 3 * sizeof(double);
     if (need > st->sbuf_bytes) {
       if (st->d_sbuf) (void)hipFree(st->d_sbuf);
       st->d_sbuf = nullptr;
@@ -1740,10 +1791,6 @@ rtx_status rtx_render(void* scene, const RtxRenderParams* params, uint8_t* rgb8,
     }
     return RTX_OK;
   };
-  // wavefront path by default; adaptive AA (per-pixel sample frames) and
-  // RTX_MEGAKERNEL=1 use the persistent megakernel (DESIGN.md: kernels)
-  const char* mk_env = getenv("RTX_MEGAKERNEL");
-  const bool megakernel = adaptive || (mk_env && atoi(mk_env) != 0);
   double* sb = adaptive ? nullptr : st->d_sbuf;
   std::vector<std::pair<hipEvent_t, hipEvent_t>> frame_events;
 
