@@ -20,6 +20,7 @@
 //     region recursion kept wave-uniform.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <climits>
 #include <cstdlib>
 #include <cmath>
@@ -1035,12 +1036,17 @@ struct QList {
 // appends, claims and liveness atomics of three concurrent groups must not
 // share lines: packed 4 bytes apart the frame took 5% longer):
 // [CNT_Q + m * CNT_LINE] queries of mode m (0 closest, 1 next),
-// [CNT_ALIVE] live slots, [CNT_CLAIM + m * CNT_LINE] the trace claim cursors
+// [CNT_CLAIM + m * CNT_LINE] the trace claim cursors, and two live-slot
+// counts used ping-pong: an even iteration appends its live slots to list A
+// (count at line 0) and reads list B (line 5), an odd one the reverse, so
+// one memset per iteration (lines 0-4 or 1-5) clears exactly the out-count
+// and the query / claim counters
 #define CNT_LINE 32
-#define CNT_Q 0
-#define CNT_ALIVE (2 * CNT_LINE)
+#define CNT_ALIVE_A 0
+#define CNT_Q (1 * CNT_LINE)
 #define CNT_CLAIM (3 * CNT_LINE)
-#define CNT_PER_GROUP (5 * CNT_LINE)
+#define CNT_ALIVE_B (5 * CNT_LINE)
+#define CNT_PER_GROUP (6 * CNT_LINE)
 
 __device__ __forceinline__ unsigned int lane_prefix(unsigned long long mask) {
   return __builtin_amdgcn_mbcnt_hi(static_cast<unsigned int>(mask >> 32),
@@ -1090,13 +1096,21 @@ __global__ void __launch_bounds__(WG, RTX_ADV_WAVES) advance_kernel(DevScene S, 
                                                       double* __restrict__ sbuf, RtxHitRecord* __restrict__ hits,
                                                       double* __restrict__ pbuf, int pend_cap, QList q0, QList q1,
                                                       unsigned int* __restrict__ counters,
-                                                      unsigned long long* __restrict__ stats, int slot_off) {
+                                                      unsigned long long* __restrict__ stats, int slot_off,
+                                                      const int* __restrict__ live_in, int* __restrict__ live_out,
+                                                      int first, int in_cnt, int out_cnt) {
   const FrameParams& F = *Fp;
-  const int slot = slot_off + blockIdx.x * WG + threadIdx.x;  // the grid covers this group's slots exactly
+  // live slots only: the first iteration covers the group's slots, later
+  // ones the slots the previous iteration left alive (its live_out list), so
+  // the frame's tail iterations cost what their few live slots cost
+  const int tid = blockIdx.x * WG + threadIdx.x;
+  const bool valid = first || tid < static_cast<int>(counters[in_cnt]);
+  const int slot = first ? slot_off + tid : (valid ? live_in[tid] : slot_off);
   Counters C = {0, 0, 0, 0, 0, 0, 0};
   LaneRef L(lm, static_cast<size_t>(slot));
   int qm = Q_NONE;
-  if (L.st() != ST_IDLE || static_cast<int64_t>(slot) + static_cast<int64_t>(L.kdone()) * F.wf_nslot < F.n_samples) {
+  if (valid && (L.st() != ST_IDLE ||
+                static_cast<int64_t>(slot) + static_cast<int64_t>(L.kdone()) * F.wf_nslot < F.n_samples)) {
     // the previous iteration's query result is already in L.bt()/bobj/bsub/bhave
     L.qmode() = Q_NONE;
     for (;;) {
@@ -1143,8 +1157,14 @@ __global__ void __launch_bounds__(WG, RTX_ADV_WAVES) advance_kernel(DevScene S, 
       Q.iv[1 * cap + k] = L.qsq();
     }
   }
-  const unsigned long long alive = __ballot(L.st() != ST_IDLE);
-  if (lane == 0 && alive) atomicAdd(&counters[CNT_ALIVE], static_cast<unsigned int>(__popcll(alive)));
+  const bool live = valid && L.st() != ST_IDLE;  // a query pending: advance it again next iteration
+  const unsigned long long alive = __ballot(live);
+  if (alive) {
+    unsigned int base = 0;
+    if (lane == 0) base = atomicAdd(&counters[out_cnt], static_cast<unsigned int>(__popcll(alive)));
+    base = __shfl(base, 0);
+    if (live) live_out[base + lane_prefix(alive)] = slot;
+  }
   if (STATS) {
     int64_t v[7] = {C.camera, C.secondary, C.shadow, C.nodes, C.objects, C.tris, C.shades};
 #pragma unroll
@@ -1879,7 +1899,9 @@ rtx_status rtx_render(void* scene, const RtxRenderParams* params, uint8_t* rgb8,
     const size_t gs = static_cast<size_t>(gslots);
     const size_t bytes_q = gs * (sizeof(int) + QL_D * sizeof(double) + 2 * sizeof(int)) + 1024;
     auto al = [](size_t x) { return (x + 255) & ~size_t(255); };
-    if ((rc = ensure(&st->d_wf, &st->wf_bytes, size_t(G) * 2 * al(bytes_q))) != RTX_OK) return rc;
+    // per group: two query lists, then two live-slot lists (ping-pong)
+    if ((rc = ensure(&st->d_wf, &st->wf_bytes, size_t(G) * (2 * al(bytes_q) + 2 * al(gs * sizeof(int))))) != RTX_OK)
+      return rc;
     if ((rc = ensure(&st->d_lane, &st->lane_bytes, lane_mem_bytes(ns))) != RTX_OK) return rc;
     const LaneMem A = lane_mem_at(st->d_lane, ns);
     if ((rc = ensure(reinterpret_cast<void**>(&st->d_pbuf), &st->pbuf_bytes,
@@ -1912,6 +1934,17 @@ rtx_status rtx_render(void* scene, const RtxRenderParams* params, uint8_t* rgb8,
         base += al(bytes_q);
       }
     }
+    std::vector<int*> live(size_t(G) * 2);  // [g * 2 + 0]: list A, [g * 2 + 1]: list B
+    {
+      char* base = static_cast<char*>(st->d_wf) + size_t(G) * 2 * al(bytes_q);
+      for (size_t k = 0; k < live.size(); ++k) {
+        live[k] = reinterpret_cast<int*>(base);
+        base += al(gs * sizeof(int));
+      }
+    }
+    // upper bound of each group's live slots (counts only fall; read back by
+    // the pipelined checks): sizes the tail iterations' grids
+    std::vector<int64_t> live_bound(size_t(G), gslots);
     F.qchunk = 64;
     HIP_TRY(hipMemcpyAsync(st->d_frame, &F, sizeof(FrameParams), hipMemcpyHostToDevice, stream));
     // every slot ST_IDLE, kdone = 0, no pending query
@@ -1947,22 +1980,33 @@ rtx_status rtx_render(void* scene, const RtxRenderParams* params, uint8_t* rgb8,
         unsigned int* cnt = st->d_counters + CNT_PER_GROUP * g;
         const QList& q0 = ql[size_t(g) * 2];
         const QList& q1 = ql[size_t(g) * 2 + 1];
-        HIP_TRY(hipMemsetAsync(cnt, 0, CNT_PER_GROUP * sizeof(unsigned int), sg));
+        // ping-pong live-slot lists: even iterations append to A, read B
+        const bool odd = (it & 1) != 0;
+        const int out_cnt = odd ? CNT_ALIVE_B : CNT_ALIVE_A, in_cnt = odd ? CNT_ALIVE_A : CNT_ALIVE_B;
+        int* live_out = live[size_t(g) * 2 + (odd ? 1 : 0)];
+        const int* live_in = live[size_t(g) * 2 + (odd ? 0 : 1)];
+        HIP_TRY(hipMemsetAsync(cnt + (odd ? CNT_LINE : 0), 0, 5 * CNT_LINE * sizeof(unsigned int), sg));
+        const int first = it == 0 ? 1 : 0;
+        const int64_t lb = live_bound[size_t(g)];
+        const int64_t agrid = first ? per : std::max<int64_t>(1, std::min<int64_t>(per, (lb + WG - 1) / WG));
+        const int64_t tg = std::max<int64_t>(1, std::min<int64_t>(tgrid, (lb + WG - 1) / WG));
         if (stats)
-          hipLaunchKernelGGL((advance_kernel<true>), dim3(per), dim3(WG), 0, sg, S, st->d_scene, st->d_frame, A, sb, d_hits,
-                             st->d_pbuf, pend_cap, q0, q1, cnt, st->d_stats, static_cast<int>(g * gslots));
+          hipLaunchKernelGGL((advance_kernel<true>), dim3(agrid), dim3(WG), 0, sg, S, st->d_scene, st->d_frame, A, sb,
+                             d_hits, st->d_pbuf, pend_cap, q0, q1, cnt, st->d_stats, static_cast<int>(g * gslots),
+                             live_in, live_out, first, in_cnt, out_cnt);
         else
-          hipLaunchKernelGGL((advance_kernel<false>), dim3(per), dim3(WG), 0, sg, S, st->d_scene, st->d_frame, A, sb, d_hits,
-                             st->d_pbuf, pend_cap, q0, q1, cnt, st->d_stats, static_cast<int>(g * gslots));
+          hipLaunchKernelGGL((advance_kernel<false>), dim3(agrid), dim3(WG), 0, sg, S, st->d_scene, st->d_frame, A, sb,
+                             d_hits, st->d_pbuf, pend_cap, q0, q1, cnt, st->d_stats, static_cast<int>(g * gslots),
+                             live_in, live_out, first, in_cnt, out_cnt);
         if (stats) {
-          hipLaunchKernelGGL((trace_kernel<true, Q_CLOSEST>), dim3(tgrid), dim3(WG), lds, sg, S, st->d_scene, q0,
+          hipLaunchKernelGGL((trace_kernel<true, Q_CLOSEST>), dim3(tg), dim3(WG), lds, sg, S, st->d_scene, q0,
                              cnt, A, st->stack_cap, st->d_stats);
-          hipLaunchKernelGGL((trace_kernel<true, Q_NEXT>), dim3(tgrid), dim3(WG), lds, sg, S, st->d_scene, q1, cnt,
+          hipLaunchKernelGGL((trace_kernel<true, Q_NEXT>), dim3(tg), dim3(WG), lds, sg, S, st->d_scene, q1, cnt,
                              A, st->stack_cap, st->d_stats);
         } else {
-          hipLaunchKernelGGL((trace_kernel<false, Q_CLOSEST>), dim3(tgrid), dim3(WG), lds, sg, S, st->d_scene, q0,
+          hipLaunchKernelGGL((trace_kernel<false, Q_CLOSEST>), dim3(tg), dim3(WG), lds, sg, S, st->d_scene, q0,
                              cnt, A, st->stack_cap, st->d_stats);
-          hipLaunchKernelGGL((trace_kernel<false, Q_NEXT>), dim3(tgrid), dim3(WG), lds, sg, S, st->d_scene, q1, cnt,
+          hipLaunchKernelGGL((trace_kernel<false, Q_NEXT>), dim3(tg), dim3(WG), lds, sg, S, st->d_scene, q1, cnt,
                              A, st->stack_cap, st->d_stats);
         }
         HIP_TRY(hipGetLastError());
@@ -1973,7 +2017,8 @@ rtx_status rtx_render(void* scene, const RtxRenderParams* params, uint8_t* rgb8,
           if (pending_check[size_t(g)] >= 0) {
             HIP_TRY(hipEventSynchronize(st->wf_check[size_t(g)]));
             const unsigned int* hc = st->h_counters + CNT_PER_GROUP * g;
-            const unsigned int alive = hc[CNT_ALIVE];
+            const unsigned int alive = hc[(pending_check[size_t(g)] & 1) ? CNT_ALIVE_B : CNT_ALIVE_A];
+            live_bound[size_t(g)] = alive;
             if (dbg)
               fprintf(stderr, "rtx group %d iter %d: alive %u (closest %u next %u)\n", g, pending_check[size_t(g)],
                       alive, hc[CNT_Q], hc[CNT_Q + CNT_LINE]);

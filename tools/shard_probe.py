@@ -1,0 +1,48 @@
+#!/usr/bin/env python3
+"""Per-rank frame time of the tile-sharded headline frame, measured on ONE
+GPU: rank r of N renders tiles t % N == r (what bench.py --gpus N runs on
+each GPU).  The slowest shard's time bounds the N-GPU frame (plus the RCCL
+gather of a few MB).  Prints one JSON line per N.
+usage (GPU box): python tools/shard_probe.py [N ...]"""
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    import bench
+    import torch
+
+    pkg = bench.load_package()
+    ns = [int(a) for a in sys.argv[1:]] or [1, 2, 4, 8]
+    opts = pkg.RenderOptions.from_cli("-w 1920 -r 5 -O r -A 4".split())
+    host = pkg.HostScene(os.path.join(ROOT, "scenes", "trimesh2.ray"))
+    dev = pkg.DeviceScene(host, 0)
+    h = host.height_for(opts.width)
+    stream = torch.cuda.current_stream().cuda_stream
+    for n in ns:
+        times = []
+        for r in range(n):
+            tile = 32 if n > 1 else 0
+            npix = pkg.shard_pixels(opts, h, tile, r, n, n > 1)
+            out = torch.zeros(npix * 3, dtype=torch.uint8, device="cuda")
+            dev.render_device(opts, out.data_ptr(), 0, stream, tile=tile, shard=r, nshards=n, packed=n > 1)
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for _ in range(3):
+                dev.render_device(opts, out.data_ptr(), 0, stream, tile=tile, shard=r, nshards=n, packed=n > 1)
+            torch.cuda.synchronize()
+            times.append((time.perf_counter() - t0) / 3 * 1e3)
+            if n == 8 and r >= 1:  # shards of 8 are alike; two are enough
+                break
+        full = 1e3 if n == 1 else None
+        print(json.dumps({"n": n, "shard_ms": [round(t, 2) for t in times], "max_ms": round(max(times), 2)}),
+              flush=True)
+
+
+if __name__ == "__main__":
+    main()
