@@ -1176,6 +1176,66 @@ __global__ void __launch_bounds__(WG, RTX_ADV_WAVES) advance_kernel(DevScene S, 
   }
 }
 
+// Tail of a slot group: once few slots are left, each remaining slot runs
+// its own chain — state machine, query, state machine, ... — to the end in
+// one persistent launch (the megakernel's inner loop over the wavefront's
+// lane state).  In the batched iterations every launch waits for its slowest
+// query (grazing rays take up to ~1700 steps), so a frame's tail costs
+// (iterations) x (worst query); here each lane only waits for its own.
+template <bool STATS>
+__global__ void __launch_bounds__(WG) tail_kernel(DevScene S, const DevScene* __restrict__ Sg,
+                                                   const FrameParams* __restrict__ Fp, LaneMem lm,
+                                                   double* __restrict__ sbuf, RtxHitRecord* __restrict__ hits,
+                                                   double* __restrict__ pbuf, int pend_cap,
+                                                   const unsigned int* __restrict__ counters,
+                                                   const int* __restrict__ live_in, int in_cnt, int stack_cap,
+                                                   unsigned long long* __restrict__ stats) {
+  extern __shared__ int lds_stack[];
+  const FrameParams& F = *Fp;
+  const int lane = threadIdx.x & 63;
+  int* stk = lds_stack + (threadIdx.x >> 6) * stack_cap * 64;
+  const int tid = blockIdx.x * WG + threadIdx.x;
+  Counters C = {0, 0, 0, 0, 0, 0, 0};
+  if (tid < static_cast<int>(counters[in_cnt])) {
+    const int slot = live_in[tid];
+    LaneRef L(lm, static_cast<size_t>(slot));
+    for (;;) {
+      // the last query's result is in L.bt()/bobj/bsub/bhave
+      L.qmode() = Q_NONE;
+      claim_sample(L, F, hits, slot);
+      if (L.st() == ST_IDLE) break;
+      advance_lane<STATS, false>(L, *Sg, F, C, sbuf, nullptr, hits, 0, 0, pbuf, lm.n, static_cast<size_t>(slot),
+                                 pend_cap);
+      const int qm = L.qmode();
+      if (qm == Q_NONE) continue;
+      dvec3 qP = L.rp(), qD = L.rd();
+      double qlim = RTX_INF;
+      if (qm == Q_NEXT) {
+        qP = rtm::ray_at(L.rp(), L.rd(), L.st_t()) - L.rd() * RTX_EPS_BACKUP;
+        qD = L.sdir();
+        double qblk;
+        shadow_bounds(S, S.lights[L.li()], qP, L.qrp() < 0, qlim, qblk);
+      }
+      double bt;
+      int bobj, bsub;
+      const bool have = traverse<STATS>(S, qm, qP, qD, L.qtp(), L.qrp(), L.qsq(), qlim, bt, bobj, bsub, stk, lane, C);
+      L.bt() = bt;
+      L.bobj() = bobj;
+      L.bsub() = bsub;
+      L.bhave() = have ? 1 : 0;
+    }
+  }
+  if (STATS) {
+    int64_t v[7] = {C.camera, C.secondary, C.shadow, C.nodes, C.objects, C.tris, C.shades};
+#pragma unroll
+    for (int k = 0; k < 7; ++k) {
+      int64_t x = v[k];
+      for (int off = 32; off > 0; off >>= 1) x += __shfl_down(x, off);
+      if (lane == 0 && x) atomicAdd(&stats[k], static_cast<unsigned long long>(x));
+    }
+  }
+}
+
 // Blocker of the shadow early-out (rtx_traverse.h): hit (oi, sb) of the
 // lane's query is entered from outside (N.dir <= 0) an opaque material —
 // the walk's own resolve_hit normal and flags (ST_WALK).  Out of line: run
@@ -1238,6 +1298,7 @@ __global__ void __launch_bounds__(WG, RTX_TRACE_WAVES)
   unsigned int qnext = 0, qend = 0;
   bool exhausted = false;
   int64_t wsteps = 0, lsteps = 0;
+  int qsteps = 0;
   auto finish = [&]() {
     const size_t slot = static_cast<size_t>(Q.slot[kq]);
     lm.d[size_t(LD_bt) * lm.n + slot] = T.bt;
@@ -1282,9 +1343,17 @@ __global__ void __launch_bounds__(WG, RTX_TRACE_WAVES)
         wsteps++;
         lsteps += __popcll(__ballot(active));
       }
-      if (active && trav_step<STATS, MODE>(T, S, stk, lane, blk, C)) {
-        finish();
-        active = false;
+      if (active) {
+        if (STATS) qsteps++;
+        if (trav_step<STATS, MODE>(T, S, stk, lane, blk, C)) {
+          finish();
+          active = false;
+          if (STATS) {  // per-query step statistics (RTX_DEBUG report)
+            atomicMax(&stats[12 + (MODE - 1)], static_cast<unsigned long long>(qsteps));
+            if (qsteps > 100) atomicAdd(&stats[14 + (MODE - 1)], 1ull);
+          }
+          qsteps = 0;
+        }
       }
     } while (static_cast<int>(__popcll(__ballot(active))) >= thresh);
   }
@@ -1945,6 +2014,11 @@ rtx_status rtx_render(void* scene, const RtxRenderParams* params, uint8_t* rgb8,
     // upper bound of each group's live slots (counts only fall; read back by
     // the pipelined checks): sizes the tail iterations' grids
     std::vector<int64_t> live_bound(size_t(G), gslots);
+    // tail switch: a group whose live slots fall to this many finishes in
+    // tail_kernel (RTX_TAIL, default 1/64 of the group's slots)
+    int64_t tail_slots = gslots / 64;
+    const char* tail_env = getenv("RTX_TAIL");
+    if (tail_env) tail_slots = atoll(tail_env);
     F.qchunk = 64;
     HIP_TRY(hipMemcpyAsync(st->d_frame, &F, sizeof(FrameParams), hipMemcpyHostToDevice, stream));
     // every slot ST_IDLE, kdone = 0, no pending query
@@ -1980,6 +2054,25 @@ rtx_status rtx_render(void* scene, const RtxRenderParams* params, uint8_t* rgb8,
         unsigned int* cnt = st->d_counters + CNT_PER_GROUP * g;
         const QList& q0 = ql[size_t(g) * 2];
         const QList& q1 = ql[size_t(g) * 2 + 1];
+        if (it > 0 && live_bound[size_t(g)] <= tail_slots) {
+          // few slots left: finish them in one persistent launch
+          const bool odd = (it & 1) != 0;  // this iteration would read the list the last one wrote
+          const int in_cnt = odd ? CNT_ALIVE_A : CNT_ALIVE_B;
+          const int* live_in = live[size_t(g) * 2 + (odd ? 0 : 1)];
+          const int64_t lb = live_bound[size_t(g)];
+          const int64_t grid = std::max<int64_t>(1, (lb + WG - 1) / WG);
+          if (stats)
+            hipLaunchKernelGGL((tail_kernel<true>), dim3(grid), dim3(WG), lds, sg, S, st->d_scene, st->d_frame, A, sb,
+                               d_hits, st->d_pbuf, pend_cap, cnt, live_in, in_cnt, st->stack_cap, st->d_stats);
+          else
+            hipLaunchKernelGGL((tail_kernel<false>), dim3(grid), dim3(WG), lds, sg, S, st->d_scene, st->d_frame, A, sb,
+                               d_hits, st->d_pbuf, pend_cap, cnt, live_in, in_cnt, st->stack_cap, st->d_stats);
+          HIP_TRY(hipGetLastError());
+          done[size_t(g)] = 1;
+          ++ndone;
+          HIP_TRY(hipEventRecord(st->wf_join[size_t(g)], sg));
+          continue;
+        }
         // ping-pong live-slot lists: even iterations append to A, read B
         const bool odd = (it & 1) != 0;
         const int out_cnt = odd ? CNT_ALIVE_B : CNT_ALIVE_A, in_cnt = odd ? CNT_ALIVE_A : CNT_ALIVE_B;
@@ -2067,8 +2160,12 @@ rtx_status rtx_render(void* scene, const RtxRenderParams* params, uint8_t* rgb8,
     {
       const char* dbg = getenv("RTX_DEBUG");
       if (dbg && atoi(dbg) != 0)
+      {
         fprintf(stderr, "rtx trace SIMD efficiency: closest %llu wave steps, %.3f active; next %llu, %.3f\n", c[8],
                 c[8] ? double(c[9]) / (64.0 * c[8]) : 0.0, c[10], c[10] ? double(c[11]) / (64.0 * c[10]) : 0.0);
+        fprintf(stderr, "rtx trace steps per query: max closest %llu next %llu; queries over 100 steps: %llu / %llu\n",
+                c[12], c[13], c[14], c[15]);
+      }
     }
     std::memset(stats, 0, sizeof(*stats));
     stats->camera_rays = c[0];

@@ -35,15 +35,17 @@ def _compare(gpu, ref, spp):
 
 # render paths (DESIGN.md "Kernels"): the wavefront advance/trace pipeline
 # (default, 3 slot groups on 3 streams), the persistent megakernel, one slot
-# group, and a tiny slot pool so every slot walks many samples
-# (claim_sample's static deal)
+# group, a tiny slot pool so every slot walks many samples (claim_sample's
+# static deal), and the tail kernel finishing almost everything
 PATHS = {"wavefront": {}, "mega": {"RTX_MEGAKERNEL": "1"}, "wavefront_1g": {"RTX_GROUPS": "1"},
-         "wavefront_256": {"RTX_SLOTS": "256"}}
+         "wavefront_256": {"RTX_SLOTS": "256"},
+         # tail_kernel takes over right after the first batched iteration
+         "wavefront_tail": {"RTX_TAIL": "1000000000"}}
 
 
 @pytest.fixture(params=list(PATHS), ids=list(PATHS))
 def render_path(request):
-    saved = {k: os.environ.get(k) for k in ("RTX_MEGAKERNEL", "RTX_SLOTS", "RTX_GROUPS")}
+    saved = {k: os.environ.get(k) for k in ("RTX_MEGAKERNEL", "RTX_SLOTS", "RTX_GROUPS", "RTX_TAIL")}
     for k in saved:
         os.environ.pop(k, None)
     os.environ.update(PATHS[request.param])
