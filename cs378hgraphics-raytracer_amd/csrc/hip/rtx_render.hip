@@ -1199,6 +1199,8 @@ __global__ void __launch_bounds__(WG) tail_kernel(DevScene S, const DevScene* __
   if (tid < static_cast<int>(counters[in_cnt])) {
     const int slot = live_in[tid];
     LaneRef L(lm, static_cast<size_t>(slot));
+    const unsigned long long t_start = STATS ? __builtin_readcyclecounter() : 0ull;
+    int64_t queries = 0;
     for (;;) {
       // the last query's result is in L.bt()/bobj/bsub/bhave
       L.qmode() = Q_NONE;
@@ -1223,6 +1225,11 @@ __global__ void __launch_bounds__(WG) tail_kernel(DevScene S, const DevScene* __
       L.bobj() = bobj;
       L.bsub() = bsub;
       L.bhave() = have ? 1 : 0;
+      if (STATS) queries++;
+    }
+    if (STATS) {  // the slowest chain of the tail (RTX_DEBUG report)
+      atomicMax(&stats[6 + 10], static_cast<unsigned long long>(__builtin_readcyclecounter() - t_start));
+      atomicMax(&stats[7 + 10], static_cast<unsigned long long>(queries));
     }
   }
   if (STATS) {
@@ -1642,7 +1649,7 @@ rtx_status rtx_scene_create(int device, const RtxSceneDesc* d, void** out) {
   st->lights.assign(d->lights, d->lights + d->n_lights);
   if (hipMalloc(&st->d_frame, sizeof(FrameParams)) != hipSuccess ||
       hipMalloc(&st->d_work, sizeof(unsigned long long)) != hipSuccess ||
-      hipMalloc(&st->d_stats, 16 * sizeof(unsigned long long)) != hipSuccess) {
+      hipMalloc(&st->d_stats, 18 * sizeof(unsigned long long)) != hipSuccess) {
     g_err = "rtx_scene_create: hipMalloc failed";
     rtx_scene_destroy(st);
     return RTX_ERR_HIP;
@@ -1859,7 +1866,7 @@ rtx_status rtx_render(void* scene, const RtxRenderParams* params, uint8_t* rgb8,
   // through this pointer (a kernel-argument copy has no address)
   if (!st->d_scene) HIP_TRY(hipMalloc(&st->d_scene, sizeof(DevScene)));
   HIP_TRY(hipMemcpyAsync(st->d_scene, &st->S_launch, sizeof(DevScene), hipMemcpyHostToDevice, stream));
-  if (stats) HIP_TRY(hipMemsetAsync(st->d_stats, 0, 16 * sizeof(unsigned long long), stream));
+  if (stats) HIP_TRY(hipMemsetAsync(st->d_stats, 0, 18 * sizeof(unsigned long long), stream));
   const int pend_cap = (params->depth > 0 ? params->depth : 0) + 2;
   auto get_event = [&](hipEvent_t* e) -> rtx_status {
     if (!st->ev_pool.empty()) {
@@ -2015,8 +2022,9 @@ rtx_status rtx_render(void* scene, const RtxRenderParams* params, uint8_t* rgb8,
     // the pipelined checks): sizes the tail iterations' grids
     std::vector<int64_t> live_bound(size_t(G), gslots);
     // tail switch: a group whose live slots fall to this many finishes in
-    // tail_kernel (RTX_TAIL, default 1/64 of the group's slots)
-    int64_t tail_slots = gslots / 64;
+    // tail_kernel (RTX_TAIL; headline frame 92.6 / 91.0 / 99.5 ms and an
+    // 8-way shard 32.3 / 25.0 / 24.9 ms at 65k / 200k / 400k)
+    int64_t tail_slots = 200000;
     const char* tail_env = getenv("RTX_TAIL");
     if (tail_env) tail_slots = atoll(tail_env);
     F.qchunk = 64;
@@ -2154,7 +2162,7 @@ rtx_status rtx_render(void* scene, const RtxRenderParams* params, uint8_t* rgb8,
     for (void* p : tmp) (void)hipFree(p);
   }
   if (stats) {
-    unsigned long long c[16];
+    unsigned long long c[18];
     HIP_TRY(hipMemcpyAsync(c, st->d_stats, sizeof(c), hipMemcpyDeviceToHost, stream));
     HIP_TRY(hipStreamSynchronize(stream));
     {
@@ -2165,6 +2173,7 @@ rtx_status rtx_render(void* scene, const RtxRenderParams* params, uint8_t* rgb8,
                 c[8] ? double(c[9]) / (64.0 * c[8]) : 0.0, c[10], c[10] ? double(c[11]) / (64.0 * c[10]) : 0.0);
         fprintf(stderr, "rtx trace steps per query: max closest %llu next %llu; queries over 100 steps: %llu / %llu\n",
                 c[12], c[13], c[14], c[15]);
+        fprintf(stderr, "rtx tail: slowest chain %llu cycles, longest chain %llu queries\n", c[16], c[17]);
       }
     }
     std::memset(stats, 0, sizeof(*stats));
