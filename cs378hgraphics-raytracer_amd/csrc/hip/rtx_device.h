@@ -73,6 +73,7 @@ struct DevRoot {
 struct DevScene {
   const DevNode4* snode4;  // scene BVH records
   const DevNode4* mnode4;  // all mesh BVHs' records (global indices)
+  const DevNode4* mhot;    // mesh records [0, n_mhot): a copy in LDS where a kernel stages one (else = mnode4)
   const DevRoot* mroots;   // per mesh (valid when meshes[m].node_count > 0)
   DevRoot sroot;           // scene BVH root
   const RtxNode* snodes;
@@ -91,6 +92,7 @@ struct DevScene {
   const uint8_t* texels;
   const double* picks;   // area-light sample positions [light][ss_res][3]
   int32_t n_snodes, n_objs, n_lights, ss_res;
+  int32_t n_srec, n_mhot;  // scene-tree records; hot mesh records (mesh roots first)
   double margin;         // world-space pruning slack
   double lmargin;        // mesh-local pruning slack
   double cos45;          // glm::cos(PI / 4) computed on the host (light.cpp:145)

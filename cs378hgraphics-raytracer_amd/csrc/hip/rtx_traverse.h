@@ -364,7 +364,8 @@ RT_HD bool trav_step(Trav& T, const DevScene& S, int* __restrict__ stk, const in
   if (closest && T.mhave) hi = rtm::gmin(hi, T.mbest + S.lmargin);
   const double lo = closest ? -RTX_INF : tlo * len * (1.0 - 1e-12) - S.lmargin;
   if (ref >= 0) {
-    if (visit4<STATS>(S.mnode4[ref], T.lp, T.ld, T.lri, hi, lo, stk, lane, sp, ref, C)) return false;
+    if (visit4<STATS>((ref < S.n_mhot ? S.mhot : S.mnode4)[ref], T.lp, T.ld, T.lri, hi, lo, stk, lane, sp, ref, C))
+      return false;
   } else {
     const int code = ~ref;
     const int f0 = code >> 2, f1 = f0 + (code & 3);
@@ -681,7 +682,45 @@ struct TravTrees {
   std::vector<RtxFace> tfaces;
   std::vector<int32_t> trank;
   int sneed = 0, mneed = 0;
+  int n_mhot = 0;  // mesh records [0, n_mhot) are the hot ones (renumbered first)
 };
+
+// Renumber the mesh records so the hottest come first — every mesh's root
+// record, then their children while `cap` allows — for kernels that stage
+// [0, n_mhot) in LDS (every walk into a mesh starts there).
+inline void hot_mesh_records(TravTrees& T, int cap) {
+  const int n = static_cast<int>(T.mn4.size());
+  std::vector<int> hot;
+  std::vector<char> is_hot(size_t(n), 0);
+  auto take = [&](int r) {
+    if (r >= 0 && r < n && !is_hot[size_t(r)] && static_cast<int>(hot.size()) < cap) {
+      is_hot[size_t(r)] = 1;
+      hot.push_back(r);
+    }
+  };
+  for (const DevRoot& mr : T.mroots) take(mr.ref);
+  const size_t nroots = hot.size();
+  for (size_t i = 0; i < nroots; ++i) {
+    const DevNode4& nd = T.mn4[size_t(hot[i])];
+    for (int k = 0; k < nd.count; ++k) take(nd.child[k]);
+  }
+  std::vector<int> remap(size_t(n), -1);
+  int next = 0;
+  for (int r : hot) remap[size_t(r)] = next++;
+  for (int r = 0; r < n; ++r)
+    if (!is_hot[size_t(r)]) remap[size_t(r)] = next++;
+  std::vector<DevNode4> out(static_cast<size_t>(n));
+  for (int r = 0; r < n; ++r) {
+    DevNode4 nd = T.mn4[size_t(r)];
+    for (int k = 0; k < nd.count; ++k)
+      if (nd.child[k] >= 0) nd.child[k] = remap[size_t(nd.child[k])];
+    out[size_t(remap[size_t(r)])] = nd;
+  }
+  T.mn4.swap(out);
+  for (DevRoot& mr : T.mroots)
+    if (mr.ref >= 0 && mr.ref < n) mr.ref = remap[size_t(mr.ref)];
+  T.n_mhot = static_cast<int>(hot.size());
+}
 
 inline bool build_trav_trees(const RtxSceneDesc* d, TravTrees& T) {
   std::memset(&T.sroot, 0, sizeof(T.sroot));
@@ -733,6 +772,7 @@ inline bool build_trav_trees(const RtxSceneDesc* d, TravTrees& T) {
     }
     T.mneed = need > T.mneed ? need : T.mneed;
   }
+  hot_mesh_records(T, 64);
   return true;
 }
 

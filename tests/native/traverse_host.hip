@@ -29,6 +29,9 @@ bool make_scene(const RtxSceneDesc* d, HostScene& H) {
   S.sroot = H.T.sroot;
   S.snode4 = H.T.sn4.data();
   S.mnode4 = H.T.mn4.data();
+  S.mhot = S.mnode4;
+  S.n_mhot = H.T.n_mhot;
+  S.n_srec = static_cast<int32_t>(H.T.sn4.size());
   S.mroots = H.T.mroots.data();
   S.tfaces = H.T.tfaces.data();
   S.trank = H.T.trank.data();
