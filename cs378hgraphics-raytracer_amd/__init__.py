@@ -56,6 +56,7 @@ class RtxSceneDesc(C.Structure):
         ("ambient", C.c_double * 3),
         ("scene_depth", C.c_int32),
         ("mesh_depth", C.c_int32),
+        ("obj_params", C.c_void_p),
     ]
 
 

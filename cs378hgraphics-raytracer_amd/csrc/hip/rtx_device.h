@@ -78,6 +78,7 @@ struct DevScene {
   DevRoot sroot;           // scene BVH root
   const RtxNode* snodes;
   const RtxObject* objs;
+  const double* oprm;      // RTX_OBJ_PARAMS per object (cone shapes)
   const RtxMaterial* mats;
   const RtxMesh* meshes;
   const RtxNode* mnodes;
@@ -107,6 +108,34 @@ struct Counters {
 };
 
 __host__ __device__ __forceinline__ dvec3 ld3(const double* p) { return mk3(p[0], p[1], p[2]); }
+
+// Cone quadric in the object frame (Cone.cpp:19-37): coefficients and the
+// two roots in the reference's names (nearRoot = (-b + sqrt) / 2a).
+struct ConeRoots {
+  double near_t, far_t;
+  bool ok;  // a != 0 and discriminant > 0
+};
+__host__ __device__ __forceinline__ ConeRoots cone_roots(const double* prm, const dvec3& R0, const dvec3& Rd) {
+  const double b2 = prm[RTX_CONE_B2], g = prm[RTX_CONE_G];
+  ConeRoots cr;
+  cr.near_t = cr.far_t = 0.0;
+  cr.ok = false;
+  const double a = Rd.x * Rd.x + Rd.y * Rd.y - b2 * Rd.z * Rd.z;
+  if (a == 0.0) return cr;
+  const double b = 2 * (R0.x * Rd.x + R0.y * Rd.y - b2 * ((R0.z + g) * Rd.z));
+  const double c = -b2 * (g + R0.z) * (g + R0.z) + R0.x * R0.x + R0.y * R0.y;
+  double disc = b * b - 4 * a * c;
+  if (disc <= 0) return cr;
+  disc = sqrt(disc);
+  cr.near_t = (-b + disc) / (2 * a);
+  cr.far_t = (-b - disc) / (2 * a);
+  cr.ok = true;
+  return cr;
+}
+// Cone::isGoodRoot (Cone.cpp:212-218)
+__host__ __device__ __forceinline__ bool cone_good(const double* prm, const dvec3& P) {
+  return !(P.z < 0 || P.z > prm[RTX_CONE_H]);
+}
 
 // ------------------------------------------------------------------ slab
 // BoundingBox::intersect (bbox.cc:33-70), exact: same divisions, same

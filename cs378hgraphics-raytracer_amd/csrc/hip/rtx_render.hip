@@ -208,6 +208,20 @@ __device__ RTX_RESOLVE_ATTR HitRef resolve_hit(const DevScene& S, const dvec3& P
         const dvec3 Q = rtm::ray_at(pos, dir, t);
         nl = rtm::normalize(mk3(Q.x, Q.y, 0.0));
       }
+    } else if (o.type == RTX_OBJ_CONE) {  // Cone.cpp:45-101 normals
+      const double* prm = S.oprm + size_t(oi) * RTX_OBJ_PARAMS;
+      const double dz = dir.z;
+      if (sub == 2) {
+        nl = dz > 0.0 ? mk3(0.0, 0.0, -1.0) : mk3(0.0, 0.0, 1.0);
+      } else if (sub == 3) {
+        nl = dz > 0.0 ? mk3(0.0, 0.0, 1.0) : mk3(0.0, 0.0, -1.0);
+      } else {
+        const ConeRoots cr = cone_roots(prm, pos, dir);
+        const dvec3 Q = rtm::ray_at(pos, dir, sub == 0 ? cr.near_t : cr.far_t);
+        dvec3 n = mk3(Q.x, Q.y, -2.0 * prm[RTX_CONE_B2] * (Q.z + prm[RTX_CONE_G]));
+        if (!(prm[RTX_CONE_CAP] != 0.0) && rtm::dot(n, dir) > 0) n = -n;
+        nl = rtm::normalize(n);
+      }
     } else if (o.type == RTX_OBJ_SQUARE) {
       const double t = -pos.z / dir.z;
       const dvec3 Q = rtm::ray_at(pos, dir, t);
@@ -1683,6 +1697,7 @@ rtx_status rtx_scene_create(int device, const RtxSceneDesc* d, void** out) {
   if ((rc = upload(*st, src, size_t(n), &dst)) != RTX_OK) { rtx_scene_destroy(st); return rc; }
   UP(d->scene_nodes, d->n_scene_nodes, S.snodes);
   UP(d->objects, d->n_objects, S.objs);
+  UP(d->obj_params, size_t(d->n_objects) * RTX_OBJ_PARAMS, S.oprm);
   UP(d->materials, d->n_materials, S.mats);
   UP(d->meshes, d->n_meshes, S.meshes);
   UP(d->mesh_nodes, d->n_mesh_nodes, S.mnodes);

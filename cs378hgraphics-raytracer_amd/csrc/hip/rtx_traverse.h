@@ -328,6 +328,52 @@ RT_HD bool trav_step(Trav& T, const DevScene& S, int* __restrict__ stk, const in
               }
             }
           }
+        } else if (o.type == RTX_OBJ_CONE) {
+          // entries: 0 near body root, 1 far body root, 2 cap z=0, 3 cap z=h
+          const double* prm = S.oprm + size_t(oi) * RTX_OBJ_PARAMS;
+          const ConeRoots cr = cone_roots(prm, pos, dir);
+          if (cr.ok) {
+            const double pz = pos.z, dz = dir.z;
+            const bool capped = prm[RTX_CONE_CAP] != 0.0;
+            const double t1 = (-pz) / dz;
+            const double t2 = (prm[RTX_CONE_H] - pz) / dz;
+            const dvec3 p1 = rtm::ray_at(pos, dir, t1);
+            const dvec3 p2 = rtm::ray_at(pos, dir, t2);
+            const double br = prm[RTX_CONE_BR], tr = prm[RTX_CONE_TR];
+            const bool in1 = capped && p1.x * p1.x + p1.y * p1.y <= br * br;
+            const bool in2 = capped && p2.x * p2.x + p2.y * p2.y <= tr * tr;
+            const bool near_good = cone_good(prm, rtm::ray_at(pos, dir, cr.near_t));
+            const bool far_good = cone_good(prm, rtm::ray_at(pos, dir, cr.far_t));
+            if (closest) {
+              // intersectLocal's own root choice (Cone.cpp:41-98), not the
+              // nearest list entry: a far root replaces the near one whenever
+              // it is good and beyond RAY_EPSILON
+              double root = RTX_RAY_EPS;
+              int sb = -1;
+              if (near_good && cr.near_t > root) {
+                root = cr.near_t;
+                sb = 0;
+              }
+              if (far_good && ((near_good && cr.far_t < root) || cr.far_t > RTX_RAY_EPS)) {
+                root = cr.far_t;
+                sb = 1;
+              }
+              if (in1 && t1 < root && t1 > RTX_RAY_EPS) {
+                root = t1;
+                sb = 2;
+              }
+              if (in2 && t2 < root && t2 > RTX_RAY_EPS) {
+                root = t2;
+                sb = 3;
+              }
+              if (!(root <= RTX_RAY_EPS)) entry(root, sb);
+            } else {  // intersectLocalList (Cone.cpp:108-210)
+              if (near_good && cr.near_t > RTX_RAY_EPS) entry(cr.near_t, 0);
+              if (cr.far_t != cr.near_t && far_good && cr.far_t > RTX_RAY_EPS) entry(cr.far_t, 1);
+              if (in1 && t1 > RTX_RAY_EPS) entry(t1, 2);
+              if (in2 && t2 > RTX_RAY_EPS) entry(t2, 3);
+            }
+          }
         } else if (o.type == RTX_OBJ_SQUARE) {  // Square.cpp:9-51
           if (!(dir.z == 0.0)) {
             const double t = -pos.z / dir.z;

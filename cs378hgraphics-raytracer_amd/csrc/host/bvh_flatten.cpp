@@ -118,6 +118,7 @@ void put3(double* d, const dvec3& v) { d[0] = v.x; d[1] = v.y; d[2] = v.z; }
 struct HostScene {
   std::vector<RtxNode> scene_nodes;
   std::vector<RtxObject> objects;
+  std::vector<double> obj_params;  // RTX_OBJ_PARAMS per object
   std::vector<RtxMaterial> materials;
   std::vector<RtxMesh> meshes;
   std::vector<RtxNode> mesh_nodes;
@@ -262,6 +263,17 @@ std::unique_ptr<HostScene> flatten(const SceneModel& sc) {
     ro.orig_id = oi;
     ro.leaf = obj_leaf[oi];
     H.objects.push_back(ro);
+    double prm[RTX_OBJ_PARAMS] = {0.0};
+    if (o.type == OBJ_CONE) {
+      prm[RTX_CONE_H] = o.cone_h;
+      prm[RTX_CONE_BR] = o.cone_br;
+      prm[RTX_CONE_TR] = o.cone_tr;
+      prm[RTX_CONE_B2] = o.cone_b2;
+      prm[RTX_CONE_G] = o.cone_g;
+      prm[RTX_CONE_CAP] = o.cone_capped ? 1.0 : 0.0;
+      H.info.n_cones++;
+    }
+    H.obj_params.insert(H.obj_params.end(), prm, prm + RTX_OBJ_PARAMS);
   }
   // rewrite scene-leaf item ranges: already DFS-leaf order == object rank
   for (const Material& m : sc.materials) H.materials.push_back(to_material(m));
@@ -375,6 +387,7 @@ rtx_status rtx_host_desc(void* handle, RtxSceneDesc* d) {
   for (int k = 0; k < 3; ++k) d->ambient[k] = H.ambient[k];
   d->scene_depth = H.info.scene_depth;
   d->mesh_depth = H.info.mesh_depth;
+  d->obj_params = H.obj_params.data();
   return RTX_OK;
 }
 

@@ -548,16 +548,39 @@ class Parser {
   void parseCone(const Transform* tf, const Material& mat) {  // Parser.cpp:472-518
     tk_.read(CONE);
     tk_.read(LBRACE);
+    bool haveMat = false;
+    Material newMat;
+    double bottomRadius = 1.0, topRadius = 0.0, height = 1.0;
+    bool capped = true;  // capped by default
     for (;;) {
       switch (tk_.peek().kind) {
-        case MATERIAL: parseMaterialExpression(mat); break;
+        case MATERIAL: newMat = parseMaterialExpression(mat); haveMat = true; break;
         case NAME: parseIdentExpression(); break;
-        case CAPPED: parseBooleanExpression(); break;
-        case BOTTOM_RADIUS: case TOP_RADIUS: case HEIGHT: parseScalarExpression(); break;
-        case RBRACE:
+        case CAPPED: capped = parseBooleanExpression(); break;
+        case BOTTOM_RADIUS: bottomRadius = parseScalarExpression(); break;
+        case TOP_RADIUS: topRadius = parseScalarExpression(); break;
+        case HEIGHT: height = parseScalarExpression(); break;
+        case RBRACE: {
           tk_.read(RBRACE);
-          (void)tf;
-          throw ParseError("Parser: fatal exception cone primitives are not supported by this build (SURVEY 8(f) rank 2)");
+          Object o;
+          o.type = OBJ_CONE;
+          o.tf = *rootOr(tf);
+          // Cone::Cone (Cone.h:11-37), same operations in the same order
+          o.cone_h = height;
+          o.cone_br = (bottomRadius < 0.0f) ? (-bottomRadius) : (bottomRadius);
+          o.cone_tr = (topRadius < 0.0f) ? (-topRadius) : (topRadius);
+          o.cone_capped = capped;
+          if (o.cone_br < 0.0001) o.cone_br = 0.0001;
+          if (o.cone_tr < 0.0001) o.cone_tr = 0.0001;
+          double beta = (o.cone_tr - o.cone_br) / o.cone_h;
+          if (std::fabs(beta) < 0.001) beta = 0.001;
+          double gamma = beta < 0.0 ? o.cone_tr / beta : o.cone_br / beta;
+          o.cone_b2 = beta * beta;
+          if (gamma < 0.0) gamma = gamma - o.cone_h;
+          o.cone_g = gamma;
+          addObject(o, haveMat ? newMat : mat);
+          return;
+        }
         default: tk_.syntax("Expected: cone attributes");
       }
     }
@@ -572,6 +595,12 @@ class Parser {
       case OBJ_BOX: lmin = mk3(-0.5, -0.5, -0.5); lmax = mk3(0.5, 0.5, 0.5); break;
       case OBJ_CYLINDER: lmin = mk3(-1, -1, 0); lmax = mk3(1, 1, 1); break;
       case OBJ_SQUARE: lmin = mk3(-0.5, -0.5, -0.00000001); lmax = mk3(0.5, 0.5, 0.00000001); break;
+      case OBJ_CONE: {  // Cone::ComputeLocalBoundingBox (Cone.h:42-50)
+        const double big = (o.cone_br > o.cone_tr) ? (o.cone_br) : (o.cone_tr);
+        lmin = mk3(-big, -big, (o.cone_h < 0.0f) ? (o.cone_h) : (0.0f));
+        lmax = mk3(big, big, (o.cone_h < 0.0f) ? (0.0f) : (o.cone_h));
+        break;
+      }
       case OBJ_TRIMESH: {
         const Mesh& me = sc_.meshes[o.mesh];
         lmin = me.lmin;

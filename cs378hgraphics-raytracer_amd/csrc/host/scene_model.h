@@ -62,6 +62,9 @@ struct Object {
   Transform tf;
   dvec3 wmin{0, 0, 0}, wmax{0, 0, 0};
   bool has_box = true;  // hasBoundingBoxCapability() (true for every supported primitive)
+  // Cone (Cone.h:11-37): height, b_radius, t_radius, beta_squared, gamma
+  double cone_h = 1.0, cone_br = 1.0, cone_tr = 0.0, cone_b2 = 0.0, cone_g = 0.0;
+  bool cone_capped = true;
 };
 
 // Trimesh (SceneObjects/trimesh.h:18-91).  faces holds only the

@@ -57,7 +57,13 @@ typedef struct RtxNode {
 } RtxNode;         /* 64 bytes */
 
 enum { RTX_OBJ_SPHERE = 0, RTX_OBJ_BOX = 1, RTX_OBJ_CYLINDER = 2,
-       RTX_OBJ_SQUARE = 3, RTX_OBJ_TRIMESH = 4 };
+       RTX_OBJ_SQUARE = 3, RTX_OBJ_TRIMESH = 4, RTX_OBJ_CONE = 5 };
+
+/* Per-object shape parameters, RTX_OBJ_PARAMS doubles per object (parallel
+ * to objects).  Cone (SceneObjects/Cone.h:11-37): height, b_radius,
+ * t_radius, beta_squared, gamma, capped (0/1); unused otherwise. */
+#define RTX_OBJ_PARAMS 8
+enum { RTX_CONE_H = 0, RTX_CONE_BR, RTX_CONE_TR, RTX_CONE_B2, RTX_CONE_G, RTX_CONE_CAP };
 
 /* Scene object (Geometry + TransformNode, scene/scene.h:64-188). */
 typedef struct RtxObject {
@@ -163,6 +169,7 @@ typedef struct RtxSceneDesc {
   double ambient[3];
   int32_t scene_depth;          /* max scene-BVH depth                         */
   int32_t mesh_depth;           /* max mesh-BVH depth over all meshes          */
+  const double* obj_params;     /* RTX_OBJ_PARAMS per object (cone shapes)     */
 } RtxSceneDesc;
 
 /* ---- render parameters (TraceUI flags, ui/TraceUI.h:34-129) ---- */

@@ -590,6 +590,92 @@ struct Square : Geom {
   }
 };
 
+struct Cone : Geom {
+  // Cone.h:11-37 parameters (computed by the host parser's parseCone)
+  double height = 1.0, b_radius = 1.0, t_radius = 0.0, beta_squared = 0.0, gamma = 0.0;
+  bool capped = true;
+  bool isGoodRoot(const dvec3& root) const { return !(root[2] < 0 || root[2] > height); }  // Cone.cpp:212-218
+  dvec3 bodyNormal(const Ray& r, double t) const {
+    const dvec3 q = r.at(t);
+    return mk3(q[0], q[1], -2.0 * beta_squared * (q[2] + gamma));
+  }
+  // quadric roots: nearRoot = (-b + sqrt) / 2a, farRoot = (-b - sqrt) / 2a (Cone.cpp:19-37)
+  bool roots(const Ray& r, double& nearRoot, double& farRoot) const {
+    const dvec3 R0 = r.p, Rd = r.d;
+    const double a = Rd[0] * Rd[0] + Rd[1] * Rd[1] - beta_squared * Rd[2] * Rd[2];
+    if (a == 0.0) return false;
+    const double b = 2 * (R0[0] * Rd[0] + R0[1] * Rd[1] - beta_squared * ((R0[2] + gamma) * Rd[2]));
+    const double c = -beta_squared * (gamma + R0[2]) * (gamma + R0[2]) + R0[0] * R0[0] + R0[1] * R0[1];
+    double disc = b * b - 4 * a * c;
+    if (disc <= 0) return false;
+    disc = sqrt(disc);
+    nearRoot = (-b + disc) / (2 * a);
+    farRoot = (-b - disc) / (2 * a);
+    return true;
+  }
+  bool intersectLocal(Ray& r, Isect& i) const override {  // Cone.cpp:7-107
+    double nearRoot, farRoot;
+    if (!roots(r, nearRoot, farRoot)) return false;
+    double theRoot = RAY_EPSILON;
+    dvec3 normal{0, 0, 0};
+    const bool nearGood = isGoodRoot(r.at(nearRoot));
+    if (nearGood && nearRoot > theRoot) {
+      theRoot = nearRoot;
+      normal = bodyNormal(r, theRoot);
+    }
+    const bool farGood = isGoodRoot(r.at(farRoot));
+    if (farGood && ((nearGood && farRoot < theRoot) || farRoot > RAY_EPSILON)) {
+      theRoot = farRoot;
+      normal = bodyNormal(r, theRoot);
+    }
+    if (!capped && rtm::dot(normal, r.d) > 0) normal = -normal;
+    const double pz = r.p[2], dz = r.d[2];
+    const double t1 = (-pz) / dz, t2 = (height - pz) / dz;
+    if (capped) {
+      const dvec3 p = r.at(t1);
+      if (p[0] * p[0] + p[1] * p[1] <= b_radius * b_radius && t1 < theRoot && t1 > RAY_EPSILON) {
+        theRoot = t1;
+        normal = dz > 0.0 ? mk3(0.0, 0.0, -1.0) : mk3(0.0, 0.0, 1.0);
+      }
+      const dvec3 q = r.at(t2);
+      if (q[0] * q[0] + q[1] * q[1] <= t_radius * t_radius && t2 < theRoot && t2 > RAY_EPSILON) {
+        theRoot = t2;
+        normal = dz > 0.0 ? mk3(0.0, 0.0, 1.0) : mk3(0.0, 0.0, -1.0);
+      }
+    }
+    if (theRoot <= RAY_EPSILON) return false;
+    i.obj = this;
+    i.t = theRoot;
+    i.N = rtm::normalize(normal);
+    return true;
+  }
+  void intersectLocalList(Ray& r, std::vector<Isect>& iv) const override {  // Cone.cpp:108-210
+    double nearRoot, farRoot;
+    if (!roots(r, nearRoot, farRoot)) return;
+    auto push = [&](double t, dvec3 n, bool body) {
+      if (body && !capped && rtm::dot(n, r.d) > 0) n = -n;
+      Isect i;
+      i.obj = this;
+      i.t = t;
+      i.N = rtm::normalize(n);
+      iv.push_back(i);
+    };
+    if (isGoodRoot(r.at(nearRoot)) && nearRoot > RAY_EPSILON) push(nearRoot, bodyNormal(r, nearRoot), true);
+    if (farRoot != nearRoot && isGoodRoot(r.at(farRoot)) && farRoot > RAY_EPSILON)
+      push(farRoot, bodyNormal(r, farRoot), true);
+    const double pz = r.p[2], dz = r.d[2];
+    const double t1 = (-pz) / dz, t2 = (height - pz) / dz;
+    if (capped) {
+      const dvec3 p = r.at(t1);
+      if (p[0] * p[0] + p[1] * p[1] <= b_radius * b_radius && t1 > RAY_EPSILON)
+        push(t1, dz > 0.0 ? mk3(0.0, 0.0, -1.0) : mk3(0.0, 0.0, 1.0), false);
+      const dvec3 q = r.at(t2);
+      if (q[0] * q[0] + q[1] * q[1] <= t_radius * t_radius && t2 > RAY_EPSILON)
+        push(t2, dz > 0.0 ? mk3(0.0, 0.0, 1.0) : mk3(0.0, 0.0, -1.0), false);
+    }
+  }
+};
+
 struct Mesh {
   const rtxh::Mesh* m = nullptr;
   std::unique_ptr<KdTree> kd;
@@ -1108,6 +1194,17 @@ std::unique_ptr<Scene> build_scene(const std::string& path) {
       case rtxh::OBJ_CYLINDER: g = new Cylinder(); break;
       case rtxh::OBJ_SQUARE: g = new Square(); break;
       case rtxh::OBJ_TRIMESH: g = new Trimesh(); break;
+      case rtxh::OBJ_CONE: {
+        Cone* c = new Cone();
+        c->height = o.cone_h;
+        c->b_radius = o.cone_br;
+        c->t_radius = o.cone_tr;
+        c->beta_squared = o.cone_b2;
+        c->gamma = o.cone_g;
+        c->capped = o.cone_capped;
+        g = c;
+        break;
+      }
       default: throw rtxh::ParseError("unsupported primitive");
     }
     g->type = o.type;

@@ -17,4 +17,6 @@ CASES = [
     ("spheres_aterm", "spheres_overlap.ray", "-w 48 -r 5 -O c -A 0.01"),
     ("spheres_r0", "spheres_overlap.ray", "-w 32 -r 0"),
     ("distance_aa3", "distance.ray", "-w 24 -r 2 -O r -A 3"),
+    ("cones_r4", "cones.ray", "-w 64 -r 4"),
+    ("cones_aa", "cones.ray", "-w 32 -r 3 -O r -A 2"),
 ]

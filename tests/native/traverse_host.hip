@@ -37,6 +37,7 @@ bool make_scene(const RtxSceneDesc* d, HostScene& H) {
   S.trank = H.T.trank.data();
   S.snodes = d->scene_nodes;
   S.objs = d->objects;
+  S.oprm = d->obj_params;
   S.mats = d->materials;
   S.meshes = d->meshes;
   S.mnodes = d->mesh_nodes;

@@ -156,6 +156,40 @@ def test_kat_cylinder(pkg, orc):
     assert hit and t == 4.0 and n == (1.0, 0.0, 0.0)  # body
 
 
+def test_kat_cone(pkg, orc):
+    # default cone: bottom 1, top 0 -> 0.0001, height 1, capped (Parser.cpp:472-518,
+    # Cone.h:11-37): beta = -0.9999, gamma = 0.0001 / beta - 1
+    # on the axis the quadric has a double root: discriminant 0 -> miss, the
+    # caps are never tested (Cone.cpp:31)
+    hit, *_ = _probe(pkg, orc, "cone.ray", (0, 0, 5), (0, 0, -1))
+    assert not hit
+    # body at z = 0.5: radius 0.9999 * 0.50010001 = 0.50005
+    hit, t, n, obj, face = _probe(pkg, orc, "cone.ray", (5, 0, 0.5), (-1, 0, 0))
+    assert hit and abs(t - 4.49995) < 1e-12 and obj == 0 and face == -1
+    nn = np.array([0.50005, 0.0, 2 * 0.9999 ** 2 * 0.50010001])
+    assert np.abs(np.array(n) - nn / np.linalg.norm(nn)).max() < 1e-12
+    # from below, off axis: the bottom cap (t = 5) beats the body root (5.50005)
+    hit, t, n, _, _ = _probe(pkg, orc, "cone.ray", (0.5, 0, -5), (0, 0, 1))
+    assert hit and t == 5.0 and n == (0.0, 0.0, -1.0)
+
+
+def test_kat_cone_uncapped_quirks(pkg, orc):
+    # bottom 1, top 0.5, height 2: beta = -0.25, gamma = 0.5 / beta - 2 = -4
+    hit, t, n, _, _ = _probe(pkg, orc, "cone_open.ray", (5, 0, 0.5), (-1, 0, 0))
+    assert hit and t == 4.125
+    nn = np.array([0.875, 0.0, 0.4375])
+    assert np.abs(np.array(n) - nn / np.linalg.norm(nn)).max() < 1e-15
+    # from inside: the far root (-0.875) replaces the near one because it is
+    # good and below theRoot (Cone.cpp:48), then theRoot <= RAY_EPSILON: the
+    # closest-hit query misses ...
+    hit, *_ = _probe(pkg, orc, "cone_open.ray", (0, 0, 0.5), (1, 0, 0))
+    assert not hit
+    # ... while intersectLocalList keeps the near root (shadow walks see it)
+    path = os.path.join(KAT, "cone_open.ray")
+    t, o, f, nh = orc.query_batch(pkg, path, np.array([[0.0, 0.0, 0.5]]), np.array([[1.0, 0.0, 0.0]]), 1, 4)
+    assert nh[0] == 1 and t[0, 0] == 0.875 and o[0, 0] == 0
+
+
 def test_kat_triangle_edges(pkg, orc):
     hit, t, n, obj, face = _probe(pkg, orc, "triangle.ray", (0.25, 0.25, 1), (0, 0, -1))
     assert hit and t == 1.0 and n == (0.0, 0.0, 1.0) and face == 0

@@ -88,7 +88,7 @@ def _rays(host, n, seed):
 
 
 SCENES = [("hitchcock.ray", 3000), ("spheres_overlap.ray", 1500), ("box_cyl_opaque_shadow_spotlight.ray", 1500),
-          ("distance.ray", 1500), ("trimesh2_square.ray", 1500), ("trimesh2.ray", 900)]
+          ("distance.ray", 1500), ("trimesh2_square.ray", 1500), ("trimesh2.ray", 900), ("cones.ray", 3000)]
 
 
 @pytest.mark.parametrize("scene,n", SCENES, ids=[s[0] for s in SCENES])
@@ -107,8 +107,10 @@ def test_closest_hit_matches_restatement(pkg, orc, scene, n):
     assert hit.mean() > 0.05  # the ray set actually hits things
 
 
-@pytest.mark.parametrize("scene,n", SCENES[:4] + [("trimesh2_square.ray", 600)],
-                         ids=[s[0] for s in SCENES[:4]] + ["trimesh2_square.ray"])
+NEXT_SCENES = SCENES[:4] + [("trimesh2_square.ray", 600), ("cones.ray", 3000)]
+
+
+@pytest.mark.parametrize("scene,n", NEXT_SCENES, ids=[s[0] for s in NEXT_SCENES])
 def test_next_hit_walk_matches_sorted_list(pkg, orc, scene, n):
     L = _harness(pkg)
     path = scene_path(scene)

@@ -21,6 +21,7 @@ GOLDEN_CASES = [
     ("lava_box", "lava_box.ray", "-w 20 -r 3"),
     ("hitchcock", "hitchcock.ray", "-w 24 -r 3 -O r -A 2"),
     ("trimesh2_square", "trimesh2_square.ray", "-w 20 -r 5"),
+    ("cones", "cones.ray", "-w 24 -r 4"),
 ]
 
 
@@ -28,7 +29,10 @@ def main():
     pkg = load_package()
     orc = load_oracle()
     out = os.path.join(ROOT, "tests", "golden")
+    only = set(sys.argv[1:])  # names to (re)generate; default all
     for name, scene, flags in GOLDEN_CASES:
+        if only and name not in only:
+            continue
         opts = pkg.RenderOptions.from_cli(flags.split())
         r = orc.render(pkg, scene_path(scene), opts, want_hits=True)
         np.savez_compressed(os.path.join(out, f"oracle_{name}.npz"), rgb=r["rgb"], rgb8=r["rgb8"],
