@@ -15,6 +15,7 @@ from __future__ import annotations
 
 import ctypes as C
 import os
+import sys
 from dataclasses import dataclass, field
 from typing import Optional
 
@@ -57,6 +58,7 @@ class RtxSceneDesc(C.Structure):
         ("scene_depth", C.c_int32),
         ("mesh_depth", C.c_int32),
         ("obj_params", C.c_void_p),
+        ("cubemap", C.c_int32 * 6),
     ]
 
 
@@ -118,6 +120,7 @@ def host_lib():
         lib.rtx_host_desc.argtypes = [C.c_void_p, C.POINTER(RtxSceneDesc)]
         lib.rtx_host_info.argtypes = [C.c_void_p, C.POINTER(RtxHostInfo)]
         lib.rtx_host_free.argtypes = [C.c_void_p]
+        lib.rtx_host_cubemap.argtypes = [C.c_void_p, C.c_char_p]
         lib.rtx_write_image.argtypes = [C.c_char_p, C.c_int32, C.c_int32, C.c_void_p]
         lib.rtx_image_height.argtypes = [C.c_int32, C.c_double]
         lib.rtx_image_height.restype = C.c_int32
@@ -151,7 +154,7 @@ def hip_lib():
 HIP_SYMBOLS = ["rtx_last_error", "rtx_device_count", "rtx_scene_create", "rtx_scene_destroy", "rtx_render",
                "rtx_shard_pixels", "rtx_kernel_time"]
 HOST_SYMBOLS = ["rtx_host_last_error", "rtx_host_load", "rtx_host_desc", "rtx_host_info", "rtx_host_free",
-                "rtx_write_image", "rtx_image_height"]
+                "rtx_host_cubemap", "rtx_write_image", "rtx_image_height"]
 
 
 def _check(rc, lib, what):
@@ -176,6 +179,7 @@ class RenderOptions:
     anaglyph: bool = False
     ss_res: int = 5
     overlapping: bool = False
+    cubemap: str = ""  # -c: one of the six cube-face files (CommandLineUI.cpp:41-42)
 
     @classmethod
     def from_cli(cls, args):
@@ -188,6 +192,8 @@ class RenderOptions:
                 o.depth = int(next(it))
             elif a == "-w":
                 o.width = int(next(it))
+            elif a == "-c":
+                o.cubemap = next(it)
             elif a == "-O":
                 prev = next(it)[0]
                 if prev == "a":
@@ -253,7 +259,7 @@ class RenderOptions:
 class HostScene:
     """A parsed + flattened scene (RayTracer::loadScene)."""
 
-    def __init__(self, path: str):
+    def __init__(self, path: str, cubemap: str = ""):
         lib = host_lib()
         h = C.c_void_p()
         rc = lib.rtx_host_load(path.encode(), C.byref(h))
@@ -261,6 +267,13 @@ class HostScene:
             raise RtxError(lib.rtx_host_last_error().decode(errors="replace"))
         self._h = h
         self.path = path
+        self.cubemap_error = None
+        if cubemap:
+            # TraceUI::smartLoadCubemap: a failure is reported on stderr and
+            # the render goes on without a cube map
+            if lib.rtx_host_cubemap(h, cubemap.encode()) != 0:
+                self.cubemap_error = lib.rtx_host_last_error().decode(errors="replace")
+                sys.stderr.write(self.cubemap_error + "\n")
         self.info = RtxHostInfo()
         lib.rtx_host_info(h, C.byref(self.info))
         self.desc = RtxSceneDesc()

@@ -100,7 +100,7 @@ struct DevScene {
   double ambient[3];
   double air_index;      // intensityValue of air's index (material.cpp:17-21)
   int32_t skip_dark;     // shadow queries whose colour factor is exactly 0 may be skipped
-  int32_t pad_;
+  int32_t cube[6];       // cube-map face textures (+x,-x,+y,-y,+z,-z); cube[0] < 0: none
 };
 
 struct Counters {
@@ -275,6 +275,32 @@ __device__ __noinline__ dvec3 tex_lookup(const DevScene& S, int tex, const dvec2
     return (x * (prows[1] - prows[0]) + prows[0]) / 255.0;
   }
   return mk3(0.0, 1.0, 0.0);
+}
+
+// CubeMap::getColor (cubeMap.cpp:12-44): the colour of a ray that hits
+// nothing.  With |x| == |y| == |z| no face branch is taken; the reference then
+// reads an uninitialised face index (decision U24: face 0, d = (0, 0)).
+__device__ __noinline__ dvec3 cube_color(const DevScene& S, const dvec3 rd) {
+  const double ax = fabs(rd.x), ay = fabs(rd.y), az = fabs(rd.z);
+  const bool xy = ax >= ay, yz = ay >= az, zx = az >= ax;
+  int map = 0;
+  double scale = 0.5;
+  dvec2 d = rtm::mk2(0.0, 0.0);
+  if (xy && !zx) {  // x direction
+    scale /= ax;
+    d = rtm::mk2(rd.x > 0 ? rd.z : -rd.z, rd.y);
+    map = rd.x > 0 ? 0 : 1;
+  } else if (yz && !xy) {  // y direction
+    scale /= ay;
+    d = rtm::mk2(rd.x, rd.y > 0 ? rd.z : -rd.z);
+    map = rd.y > 0 ? 2 : 3;
+  } else if (zx && !yz) {  // z direction
+    scale /= az;
+    d = rtm::mk2(rd.z > 0 ? rd.x : -rd.x, rd.y);
+    map = rd.z > 0 ? 4 : 5;
+  }
+  d = rtm::mk2(d.x * scale + 0.5, d.y * scale + 0.5);
+  return tex_lookup(S, S.cube[map], d);
 }
 
 // MaterialParameter::value / intensityValue (material.cpp:140-158)

@@ -511,7 +511,12 @@ __device__ __forceinline__ void advance_lane(LaneRef& LR, const DevScene& S, con
         const int dk = static_cast<int>(b[12 * nlanes]);
         LR.nrays()++;
         const int pdepth = dk >= 0 ? dk / 4 : -((-dk + 3) / 4);
-        if (pdepth < 0) break;  // `depth >= 0 &&` (RayTracer.cpp:116)
+        if (pdepth < 0) {  // `depth >= 0 &&` (RayTracer.cpp:116): no query, the miss colour
+          if (S.cube[0] >= 0)
+            LR.acc() += mk3(b[6 * nlanes], b[7 * nlanes], b[8 * nlanes]) *
+                        cube_color(S, mk3(b[3 * nlanes], b[4 * nlanes], b[5 * nlanes]));
+          break;
+        }
         LR.rp() = mk3(b[0 * nlanes], b[1 * nlanes], b[2 * nlanes]);
         LR.rd() = mk3(b[3 * nlanes], b[4 * nlanes], b[5 * nlanes]);
         LR.W() = mk3(b[6 * nlanes], b[7 * nlanes], b[8 * nlanes]);
@@ -543,7 +548,9 @@ __device__ __forceinline__ void advance_lane(LaneRef& LR, const DevScene& S, con
             }
           }
         }
-        if (!LR.bhave()) {  // miss: no cube map => black
+        if (!LR.bhave()) {  // miss: the cube map's colour, else black (RayTracer.cpp:167-169)
+          // a child's kt^t factor is kt^0 = 1 on a miss (decision U3)
+          if (S.cube[0] >= 0) LR.acc() += LR.W() * cube_color(S, LR.rd());
           LR.st() = ST_POP;
           break;
         }
@@ -1730,6 +1737,14 @@ rtx_status rtx_scene_create(int device, const RtxSceneDesc* d, void** out) {
     UP(tt.tfaces.data(), tt.tfaces.size(), S.tfaces);
     UP(tt.trank.data(), tt.trank.size(), S.trank);
 #undef UP
+  }
+  for (int k = 0; k < 6; ++k) {
+    S.cube[k] = d->cubemap[0] >= 0 ? d->cubemap[k] : -1;
+    if (S.cube[k] >= d->n_textures || (d->cubemap[0] >= 0 && S.cube[k] < 0)) {
+      g_err = "rtx_scene_create: cube-map face names no texture";
+      rtx_scene_destroy(st);
+      return RTX_ERR_INVALID;
+    }
   }
   S.n_snodes = d->n_scene_nodes;
   S.n_objs = d->n_objects;

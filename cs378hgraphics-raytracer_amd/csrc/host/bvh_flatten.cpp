@@ -119,6 +119,7 @@ struct HostScene {
   std::vector<RtxNode> scene_nodes;
   std::vector<RtxObject> objects;
   std::vector<double> obj_params;  // RTX_OBJ_PARAMS per object
+  int32_t cubemap[6] = {-1, -1, -1, -1, -1, -1};
   std::vector<RtxMaterial> materials;
   std::vector<RtxMesh> meshes;
   std::vector<RtxNode> mesh_nodes;
@@ -367,6 +368,31 @@ rtx_status rtx_host_load(const char* ray_path, void** handle) {
   }
 }
 
+rtx_status rtx_host_cubemap(void* handle, const char* one_cubemap_file) {
+  if (!handle || !one_cubemap_file) {
+    g_host_err = "rtx_host_cubemap: null argument";
+    return RTX_ERR_INVALID;
+  }
+  rtxh::HostScene& H = *static_cast<rtxh::HostScene*>(handle);
+  rtxh::Texture faces[6];
+  std::string err;
+  if (!rtxh::load_cubemap(one_cubemap_file, faces, err)) {
+    g_host_err = err;
+    return RTX_ERR_INVALID;
+  }
+  for (int k = 0; k < 6; ++k) {
+    RtxTexture rt;
+    rt.width = faces[k].width;
+    rt.height = faces[k].height;
+    rt.offset = static_cast<int64_t>(H.texels.size());
+    H.texels.insert(H.texels.end(), faces[k].data.begin(), faces[k].data.end());
+    H.cubemap[k] = static_cast<int32_t>(H.textures.size());
+    H.textures.push_back(rt);
+  }
+  H.info.n_textures = static_cast<int>(H.textures.size());
+  return RTX_OK;
+}
+
 rtx_status rtx_host_desc(void* handle, RtxSceneDesc* d) {
   if (!handle || !d) return RTX_ERR_INVALID;
   rtxh::HostScene& H = *static_cast<rtxh::HostScene*>(handle);
@@ -388,6 +414,7 @@ rtx_status rtx_host_desc(void* handle, RtxSceneDesc* d) {
   d->scene_depth = H.info.scene_depth;
   d->mesh_depth = H.info.mesh_depth;
   d->obj_params = H.obj_params.data();
+  for (int k = 0; k < 6; ++k) d->cubemap[k] = H.cubemap[k];
   return RTX_OK;
 }
 

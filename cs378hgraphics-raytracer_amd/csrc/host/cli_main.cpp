@@ -24,6 +24,8 @@ int main(int argc, char** argv) {
     std::cerr << "Unable to load ray file '" << o.ray_name << "'" << std::endl;
     return 1;
   }
+  if (!o.cubemap.empty() && rtx_host_cubemap(hs, o.cubemap.c_str()) != RTX_OK)
+    std::cerr << rtx_host_last_error() << std::endl;  // smartLoadCubemap: render on without one
   RtxHostInfo info;
   rtx_host_info(hs, &info);
   RtxSceneDesc desc;

@@ -210,8 +210,8 @@ inline int cli_parse(int argc, char** argv, CliOptions& o) {
     }
   }
   if (jsonfile) cli_load_json(o, jsonfile);
-  if (!o.cubemap.empty())
-    std::cerr << "Cube maps (-c) are not supported by this build; rendering without one." << std::endl;
+  // -c: the cube map is loaded with the scene (rtx_host_cubemap), where a
+  // failure is reported and the render goes on without one
   if (optind >= argc - 1) {
     std::cerr << "no input and/or output name." << std::endl;
     return 1;

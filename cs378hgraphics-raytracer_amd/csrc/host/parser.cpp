@@ -8,6 +8,7 @@
 //               (addFace degeneracy, generateNormals), camera.cpp, light.h ctors
 // Errors are reported as ParseError carrying the message RayTracer::loadScene
 // would print (RayTracer.cpp:216-234).
+#include <dirent.h>
 #include <cmath>
 #include <cstdlib>
 #include <fstream>
@@ -1127,6 +1128,58 @@ SceneModel load_ray_file(const std::string& path) {  // RayTracer::loadScene (Ra
   size_t slash = path.find_last_of("\\/");
   base = (slash == std::string::npos) ? std::string(".") : path.substr(0, slash);
   return parse_ray_text(ss.str(), base);
+}
+
+// ---------------------------------------------------------------- cube map (-c)
+bool load_cubemap(const std::string& one_cubemap_file, Texture faces[6], std::string& err) {
+  // TraceUI.cc:87-94; note find_first_of: ANY character of "pos" / "neg"
+  static const char* const matcher[6][2] = {{"pos", "x"}, {"neg", "x"}, {"pos", "y"},
+                                            {"neg", "y"}, {"pos", "z"}, {"neg", "z"}};
+  const std::string fN = one_cubemap_file;
+  const std::string pdir = fN.substr(0, fN.find_last_of("/"));
+  DIR* dp = opendir(pdir.data());
+  if (dp == nullptr) {
+    err = "Couldn't open the directory " + pdir;
+    return false;
+  }
+  std::string matched_fn[6];
+  int matched = 0;
+  while (struct dirent* ep = readdir(dp)) {  // directory order, as the reference
+    const std::string fn(ep->d_name);
+    for (int i = 0; i < 6; i++) {
+      const auto pos0 = fn.find_first_of(matcher[i][0]);
+      if (pos0 == std::string::npos) continue;
+      const auto pos1 = fn.find_first_of(matcher[i][1], pos0);
+      if (pos1 == std::string::npos) continue;
+      if (!matched_fn[i].empty()) {
+        closedir(dp);
+        err = std::string(matcher[i][0]) + matcher[i][1] + " matches " + matched_fn[i] + " and " + fn +
+              ", stop smartload to avoid confliction";
+        return false;
+      }
+      matched_fn[i] = fn;
+      matched++;
+      break;
+    }
+    if (matched == 6) break;
+  }
+  closedir(dp);
+  if (matched != 6) {
+    err = "Cannot locate all six cubemap files";
+    return false;
+  }
+  for (int i = 0; i < 6; i++) {  // TextureMap ctor (material.cpp:70-81)
+    const std::string path = pdir + "/" + matched_fn[i];
+    Texture t;
+    t.path = path;
+    t.data = read_image(path, t.width, t.height);
+    if (t.data.empty()) {
+      err = "Unable to load texture map '" + path + "'.";
+      return false;
+    }
+    faces[i] = std::move(t);
+  }
+  return true;
 }
 
 }  // namespace rtxh

@@ -155,6 +155,10 @@ Transform make_transform(const Transform* parent, const Mat4& local);
 
 // Image I/O (image_io.cpp)
 std::vector<uint8_t> read_image(const std::string& path, int& w, int& h);
+// TraceUI::matchCubemapFiles + smartLoadCubemap's TextureMap loads
+// (TraceUI.cc:87-167): fills faces[0..5] (+x,-x,+y,-y,+z,-z) or returns false
+// with the message the reference prints.
+bool load_cubemap(const std::string& one_cubemap_file, Texture faces[6], std::string& err);
 bool write_image(const std::string& path, int w, int h, const uint8_t* rgb, std::string* err);
 
 }  // namespace rtxh

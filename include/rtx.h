@@ -170,6 +170,8 @@ typedef struct RtxSceneDesc {
   int32_t scene_depth;          /* max scene-BVH depth                         */
   int32_t mesh_depth;           /* max mesh-BVH depth over all meshes          */
   const double* obj_params;     /* RTX_OBJ_PARAMS per object (cone shapes)     */
+  int32_t cubemap[6];           /* texture ids of the cube faces +x,-x,+y,-y,+z,-z
+                                   (CubeMap::tMap, cubeMap.h); -1: no cube map   */
 } RtxSceneDesc;
 
 /* ---- render parameters (TraceUI flags, ui/TraceUI.h:34-129) ---- */

@@ -37,6 +37,13 @@ rtx_status rtx_host_load(const char* ray_path, void** handle);
 rtx_status rtx_host_desc(void* handle, RtxSceneDesc* desc);   /* pointers into handle */
 rtx_status rtx_host_info(void* handle, RtxHostInfo* info);
 rtx_status rtx_host_free(void* handle);
+/* -c FILE: TraceUI::smartLoadCubemap (ui/TraceUI.cc:97-167): the six cube
+ * faces are the files of FILE's directory matched by matchCubemapFiles;
+ * they join the scene's textures and RtxSceneDesc.cubemap names them.  On
+ * failure returns RTX_ERR_INVALID with the message the reference prints to
+ * stderr and leaves the scene without a cube map (the reference renders
+ * on without one). */
+rtx_status rtx_host_cubemap(void* handle, const char* one_cubemap_file);
 /* writeImage (fileio/images.cc:59-68): .png / .bmp by extension, RGB8 with
  * buffer row 0 at the bottom. */
 rtx_status rtx_write_image(const char* path, int32_t w, int32_t h, const uint8_t* rgb);

@@ -894,6 +894,35 @@ struct Scene {
   std::unique_ptr<KdTree> kdtree;
   std::vector<int> obj_leaf;
   double aterm_thresh = 0.0;
+  // -c: CubeMap (cubeMap.cpp:12-44), faces +x,-x,+y,-y,+z,-z
+  rtxh::Texture cube_faces[6];
+  bool use_cube = false;
+
+  dvec3 cubeColor(const Ray& r) const {  // CubeMap::getColor
+    const dvec3 rd = r.d;
+    const dvec3 absRD = mk3(std::fabs(rd.x), std::fabs(rd.y), std::fabs(rd.z));
+    const bool xy = absRD[0] >= absRD[1];
+    const bool yz = absRD[1] >= absRD[2];
+    const bool zx = absRD[2] >= absRD[0];
+    int map = 0;  // decision U24: uninitialised when no branch below is taken
+    double scale = 0.5;
+    dvec2 d{0, 0};
+    if (xy && !zx) {
+      scale /= absRD[0];
+      d = rtm::mk2(rd[0] > 0 ? rd[2] : -rd[2], rd[1]);
+      map = rd[0] > 0 ? 0 : 1;
+    } else if (yz && !xy) {
+      scale /= absRD[1];
+      d = rtm::mk2(rd[0], rd[1] > 0 ? rd[2] : -rd[2]);
+      map = rd[1] > 0 ? 2 : 3;
+    } else if (zx && !yz) {
+      scale /= absRD[2];
+      d = rtm::mk2(rd[2] > 0 ? rd[0] : -rd[0], rd[1]);
+      map = rd[2] > 0 ? 4 : 5;
+    }
+    d = rtm::mk2(d.x * scale + 0.5, d.y * scale + 0.5);
+    return Tex{&cube_faces[map]}.getMappedValue(d);
+  }
 
   bool intersect(Ray& r, Isect& i) const {  // scene.cpp:157-180
     bool have_one = false;
@@ -1061,7 +1090,7 @@ struct Tracer {
         }
       }
     }
-    // miss: no cube map in this restatement (-c not supported) => black
+    if (!hit && scene->use_cube) colorC = scene->cubeColor(r);  // RayTracer.cpp:167-169
     return colorC;
   }
 
@@ -1249,10 +1278,17 @@ extern "C" {
 
 const char* oracle_last_error(void) { return orc::g_err.c_str(); }
 
-int oracle_render(const char* ray_path, const RtxRenderParams* params, const OracleRect* rect, uint8_t* rgb8,
-                  double* rgb_f64, RtxHitRecord* hits, RtxStats* stats) {
+int oracle_render(const char* ray_path, const char* cubemap_file, const RtxRenderParams* params,
+                  const OracleRect* rect, uint8_t* rgb8, double* rgb_f64, RtxHitRecord* hits, RtxStats* stats) {
   try {
     std::unique_ptr<orc::Scene> S = orc::build_scene(ray_path);
+    if (cubemap_file && cubemap_file[0]) {  // TraceUI::smartLoadCubemap: failure => stderr, no cube map
+      std::string err;
+      if (rtxh::load_cubemap(cubemap_file, S->cube_faces, err))
+        S->use_cube = true;
+      else
+        std::fprintf(stderr, "%s\n", err.c_str());
+    }
     S->aterm_thresh = params->aterm_thresh;
     orc::Tracer T;
     T.scene = S.get();

@@ -33,9 +33,10 @@ typedef struct OracleRect {
 const char* oracle_last_error(void);
 /* Render `ray_path` with the reference algorithm.  Outputs are full-frame
  * (reference buffer indexing (i + j*w)*3); only pixels inside `rect` are
- * written.  hits: aa-samples-per-pixel records (NULL allowed). */
-int oracle_render(const char* ray_path, const RtxRenderParams* params, const OracleRect* rect,
-                  uint8_t* rgb8, double* rgb_f64, RtxHitRecord* hits, RtxStats* stats);
+ * written.  hits: aa-samples-per-pixel records (NULL allowed).
+ * cubemap_file: -c (NULL or "": none). */
+int oracle_render(const char* ray_path, const char* cubemap_file, const RtxRenderParams* params,
+                  const OracleRect* rect, uint8_t* rgb8, double* rgb_f64, RtxHitRecord* hits, RtxStats* stats);
 /* Structural hashes of the oracle's own KdTree builds (same definition as
  * RtxHostInfo.scene_bvh_hash / mesh_bvh_hash). */
 int oracle_bvh_hash(const char* ray_path, uint64_t* scene_hash, uint64_t* mesh_hash);

@@ -39,8 +39,8 @@ def lib(pkg):
             build()
         L = C.CDLL(LIB)
         L.oracle_last_error.restype = C.c_char_p
-        L.oracle_render.argtypes = [C.c_char_p, C.POINTER(pkg.RtxRenderParams), C.POINTER(OracleRect), C.c_void_p,
-                                    C.c_void_p, C.c_void_p, C.POINTER(pkg.RtxStats)]
+        L.oracle_render.argtypes = [C.c_char_p, C.c_char_p, C.POINTER(pkg.RtxRenderParams), C.POINTER(OracleRect),
+                                    C.c_void_p, C.c_void_p, C.c_void_p, C.POINTER(pkg.RtxStats)]
         L.oracle_bvh_hash.argtypes = [C.c_char_p, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]
         L.oracle_probe.argtypes = [C.c_char_p, C.POINTER(C.c_double), C.POINTER(C.c_double),
                                    C.POINTER(C.c_double), C.POINTER(C.c_double), C.POINTER(C.c_int32),
@@ -90,7 +90,7 @@ def render(pkg, path: str, opts, rect=None, threads: int = 0, want_hits: bool = 
     if rect is not None:
         r.x0, r.y0, r.x1, r.y1 = rect
     st = pkg.RtxStats()
-    rc = L.oracle_render(path.encode(), C.byref(p), C.byref(r), rgb8.ctypes.data, rgb.ctypes.data,
+    rc = L.oracle_render(path.encode(), opts.cubemap.encode(), C.byref(p), C.byref(r), rgb8.ctypes.data, rgb.ctypes.data,
                          hits.ctypes.data if hits is not None else None, C.byref(st))
     if rc != 0:
         raise RuntimeError(L.oracle_last_error().decode())

@@ -33,7 +33,7 @@ int main(int argc, char** argv) {
   OracleRect rect = {0, 0, 0, 0, o.threads};
   RtxStats st;
   auto t0 = std::chrono::steady_clock::now();
-  if (oracle_render(o.ray_name.c_str(), &p, &rect, rgb.data(), f64.data(), hits.empty() ? nullptr : hits.data(),
+  if (oracle_render(o.ray_name.c_str(), o.cubemap.c_str(), &p, &rect, rgb.data(), f64.data(), hits.empty() ? nullptr : hits.data(),
                     &st) != 0) {
     std::cerr << oracle_last_error() << std::endl;
     std::cerr << "Unable to load ray file '" << o.ray_name << "'" << std::endl;

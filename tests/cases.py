@@ -19,4 +19,8 @@ CASES = [
     ("distance_aa3", "distance.ray", "-w 24 -r 2 -O r -A 3"),
     ("cones_r4", "cones.ray", "-w 64 -r 4"),
     ("cones_aa", "cones.ray", "-w 32 -r 3 -O r -A 2"),
+    # -c: relative cube-map paths name files under tests/golden
+    ("cubemap_cones", "cones.ray", "-w 48 -r 3 -c cubemap/posx.bmp"),
+    ("cubemap_spheres_aa", "spheres_overlap.ray", "-w 32 -r 4 -O r -A 2 -c cubemap/negz.bmp"),
+    ("cubemap_r0", "cones.ray", "-w 24 -r 0 -c cubemap/posy.bmp"),
 ]

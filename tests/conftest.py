@@ -46,6 +46,15 @@ def orc():
     return o
 
 
+def cli_opts(pkg, flags):
+    """RenderOptions from reference CLI flags; a relative -c path names a
+    cube-map face under tests/golden (e.g. cubemap/posx.bmp)."""
+    opts = pkg.RenderOptions.from_cli(flags.split())
+    if opts.cubemap and not os.path.isabs(opts.cubemap):
+        opts.cubemap = os.path.join(GOLDEN, opts.cubemap)
+    return opts
+
+
 def scene_path(name):
     for d in (NEWSCENE, SCENES, GOLDEN):
         p = os.path.join(d, name)

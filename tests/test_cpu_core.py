@@ -10,7 +10,7 @@ import subprocess
 import numpy as np
 import pytest
 
-from conftest import GOLDEN, NEWSCENE, ROOT, scene_path
+from conftest import GOLDEN, NEWSCENE, ROOT, cli_opts, scene_path
 
 KAT = os.path.join(GOLDEN, "kat")
 PKG_DIR = os.path.join(ROOT, "cs378hgraphics-raytracer_amd")
@@ -210,7 +210,7 @@ def _golden_files():
 @pytest.mark.parametrize("fname", _golden_files())
 def test_oracle_matches_golden(pkg, orc, fname):
     g = np.load(os.path.join(GOLDEN, fname))
-    opts = pkg.RenderOptions.from_cli(str(g["flags"]).split())
+    opts = cli_opts(pkg, str(g["flags"]))
     r = orc.render(pkg, scene_path(str(g["scene"])), opts, want_hits=True)
     assert np.array_equal(r["rgb8"], g["rgb8"])
     assert np.abs(r["rgb"] - g["rgb"]).max() <= 1e-12

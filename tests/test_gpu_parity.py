@@ -11,7 +11,7 @@ import numpy as np
 import pytest
 
 from cases import CASES
-from conftest import scene_path
+from conftest import cli_opts, scene_path
 
 pytestmark = pytest.mark.gpu
 
@@ -60,8 +60,9 @@ def render_path(request):
 @pytest.mark.parametrize("name,scene,flags", CASES, ids=[c[0] for c in CASES])
 def test_parity(pkg, orc, render_path, name, scene, flags):
     path = scene_path(scene)
-    opts = pkg.RenderOptions.from_cli(flags.split())
-    host = pkg.HostScene(path)
+    opts = cli_opts(pkg, flags)
+    host = pkg.HostScene(path, cubemap=opts.cubemap)
+    assert host.cubemap_error is None
     dev = pkg.DeviceScene(host, 0)
     gpu = dev.render(opts, want_f64=True, want_hits=True, stats=True)
     ref = orc.render(pkg, path, opts, want_hits=True)

@@ -11,7 +11,7 @@ import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "tests"))
-from conftest import load_package, load_oracle, scene_path  # noqa: E402
+from conftest import cli_opts, load_package, load_oracle, scene_path  # noqa: E402
 
 GOLDEN_CASES = [
     ("spheres_overlap", "spheres_overlap.ray", "-w 24 -r 5"),
@@ -22,6 +22,7 @@ GOLDEN_CASES = [
     ("hitchcock", "hitchcock.ray", "-w 24 -r 3 -O r -A 2"),
     ("trimesh2_square", "trimesh2_square.ray", "-w 20 -r 5"),
     ("cones", "cones.ray", "-w 24 -r 4"),
+    ("cubemap_cones", "cones.ray", "-w 24 -r 3 -c cubemap/posx.bmp"),
 ]
 
 
@@ -33,7 +34,7 @@ def main():
     for name, scene, flags in GOLDEN_CASES:
         if only and name not in only:
             continue
-        opts = pkg.RenderOptions.from_cli(flags.split())
+        opts = cli_opts(pkg, flags)
         r = orc.render(pkg, scene_path(scene), opts, want_hits=True)
         np.savez_compressed(os.path.join(out, f"oracle_{name}.npz"), rgb=r["rgb"], rgb8=r["rgb8"],
                             hits=r["hits"], flags=np.array(flags), scene=np.array(scene),
