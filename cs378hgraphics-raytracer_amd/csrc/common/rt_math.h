@@ -72,6 +72,10 @@ RT_HD double distance(const dvec3& p0, const dvec3& p1) { return length(p1 - p0)
 RT_HD double gmin(double x, double y) { return (y < x) ? y : x; }
 RT_HD double gmax(double x, double y) { return (x < y) ? y : x; }
 RT_HD double gclamp(double x, double lo, double hi) { return gmin(gmax(x, lo), hi); }
+// setPixel's (int)(255 * c) (RayTracer.cpp:388-394) for c in [0, 1] or NaN
+// (glm::clamp passes NaN through): x86 cvttsd2si turns NaN into INT_MIN,
+// whose low byte is 0; both paths write that 0 explicitly.
+RT_HD uint8_t to_byte(double c) { return (c != c) ? uint8_t(0) : uint8_t(int(255.0 * c)); }
 RT_HD dvec3 gclamp3(const dvec3& v, double lo, double hi) {
   return mk3(gclamp(v.x, lo, hi), gclamp(v.y, lo, hi), gclamp(v.z, lo, hi));
 }

@@ -253,6 +253,13 @@ __device__ __forceinline__ dvec3 hit_param(const DevScene& S, const HitRef& h, i
   return pval(S, S.mats[h.mat].p[k], h.uv);
 }
 // shininess (material.h:204-209: a texture map is scaled by 128)
+// A parameter's constant value at a hit, what Material::operator+= adds
+// (textured parameters: their _value, 0); per-vertex materials: the
+// interpolated value
+__device__ __forceinline__ dvec3 hit_raw(const DevScene& S, const HitRef& h, int k) {
+  if (h.vm_off >= 0) return hit_param(S, h, k);
+  return ld3(S.mats[h.mat].p[k].v);
+}
 __device__ __forceinline__ double hit_shininess(const DevScene& S, const HitRef& h) {
   if (h.vm_off >= 0) return intensity(hit_param(S, h, RTX_P_SHININESS));
   const RtxParam& shp = S.mats[h.mat].p[RTX_P_SHININESS];
@@ -299,7 +306,9 @@ __device__ __forceinline__ void shadow_bounds(const DevScene& S, const RtxLight&
 }
 
 // ============================================================ lane state machine
-enum { ST_IDLE = 0, ST_CAM, ST_POP, ST_HIT, ST_LIGHT, ST_SRS, ST_WALK };
+enum { ST_IDLE = 0, ST_CAM, ST_POP, ST_HIT, ST_LIGHT, ST_SRS, ST_WALK, ST_RECUR, ST_DISC, ST_WALK2 };
+// discoverMat walks (-O o) return to: 1 ST_RECUR (traceRay), 2 ST_WALK2 (srsAttenuation)
+enum { DISC_NONE = 0, DISC_RECUR = 1, DISC_WALK = 2 };
 
 struct Pending {
   dvec3 p, d, W, ktf;
@@ -314,10 +323,11 @@ struct Pending {
 // fields of its current step, and the traversal's registers are not shared
 // with it.  LaneRef gives a lane's fields as accessors (LR.st(), LR.acc(), ...).
 #define LANE_INT_FIELDS(X) X(st) X(sample_slot) X(rec_on) X(pass) X(camk) X(nrays) X(top) X(rdepth) X(rkind) \
-  X(first_query) X(cam_end) X(sobj) X(ssub) X(m_flags) X(li) X(pick) X(qmode) X(qrp) X(qsq) X(kdone) X(bobj) X(bsub) X(bhave)
-#define LANE_DBL_FIELDS(X) X(sx) X(sy) X(st_t) X(m_sh) X(dattn) X(last_t) X(qtp) X(bt)
+  X(first_query) X(cam_end) X(sobj) X(ssub) X(m_flags) X(li) X(pick) X(qmode) X(qrp) X(qsq) X(kdone) X(bobj) X(bsub) X(bhave) \
+  X(dret) X(dpass) X(dpush) X(dhead) X(dtot) X(dlast) X(dopq) X(mo_trans) X(wobj) X(wsub)
+#define LANE_DBL_FIELDS(X) X(sx) X(sy) X(st_t) X(m_sh) X(dattn) X(last_t) X(qtp) X(bt) X(mo_idx) X(wt) X(wtr)
 #define LANE_VEC_FIELDS(X) X(acc) X(rp) X(rd) X(W) X(N) X(i_out) X(dscomp) X(m_kd) X(m_ks) X(area_sum) X(sdir) \
-  X(wpos) X(sattn)
+  X(wpos) X(sattn) X(dpos) X(ddir) X(dkt) X(didx) X(mo_kt)
 
 enum {
 #define E_(f) LI_##f,
@@ -393,12 +403,171 @@ __device__ __forceinline__ void lane_clear(const LaneMem& m, size_t g) {
   for (int k = 0; k < LV_COUNT; ++k) m.v[size_t(k) * m.n + g] = mk3(0.0, 0.0, 0.0);
 }
 
+// The ray of a lane's pending next-hit query: the shadow walk's (from the
+// backed-up shading point toward the light, bounded by the light, with the
+// opaque-blocker early-out below tblock) or a discoverMat walk's (every hit
+// of the ray, unbounded, no early-out).
+template <bool MEDIA>
+__device__ __forceinline__ void next_query_ray(const DevScene& S, const LaneRef& L, dvec3& qP, dvec3& qD,
+                                               double& qlim, double& qblk) {
+  if (MEDIA && L.dret() != DISC_NONE) {
+    qP = L.dpos();
+    qD = L.ddir();
+    qlim = RTX_INF;
+    qblk = -RTX_INF;
+    return;
+  }
+  qP = rtm::ray_at(L.rp(), L.rd(), L.st_t()) - L.rd() * RTX_EPS_BACKUP;
+  qD = L.sdir();
+  shadow_bounds(S, S.lights[L.li()], qP, L.qrp() < 0, qlim, qblk);
+}
+
+// Scene::discoverMat (scene.cpp:212-237) over the ray (dpos, ddir): its
+// sorted hits as successive next-hit queries from the list start
+__device__ __forceinline__ void disc_query(LaneRef& LR, bool from_start) {
+  LR.qmode() = Q_NEXT;
+  LR.qtp() = from_start ? -RTX_INF : LR.bt();
+  LR.qrp() = from_start ? -1 : LR.bobj();
+  LR.qsq() = from_start ? -1 : LR.bsub();
+}
+__device__ __forceinline__ void disc_start(LaneRef& LR, int ret) {
+  LR.dret() = ret;
+  LR.dpass() = 0;
+  LR.dpush() = 0;
+  LR.dhead() = 0;
+  LR.dlast() = -1;
+  LR.dopq() = 0;
+  LR.dkt() = mk3(1.0, 1.0, 1.0);  // Material(air): kt 1, index 1
+  LR.didx() = mk3(1.0, 1.0, 1.0);
+  LR.st() = ST_DISC;
+  disc_query(LR, true);
+}
+// the shadow walk after a hit's limit check (light.cpp:47-49); m_out = (trans_o, kt_o)
+__device__ __forceinline__ void walk_on(LaneRef& LR, const DevScene& S, double aterm, const HitRef& R, bool is_inside,
+                                        double t, bool trans_o, const dvec3& kt_o, bool& done, dvec3& result) {
+  const bool next_trans = is_inside ? trans_o : ((hit_flags(S, R) & RTX_MF_TRANS) != 0);
+  if (!next_trans || (aterm > 0.0 && rtm::dot(LR.sattn(), LR.sattn()) < aterm * aterm)) {
+    result = mk3(0.0, 0.0, 0.0);
+    done = true;
+  } else {
+    const dvec3 kt = is_inside ? hit_param(S, R, RTX_P_KT) : kt_o;
+    LR.sattn() *= rtm::pow3(kt, t);
+    LR.qmode() = Q_NEXT;
+    LR.qtp() = LR.bt();
+    LR.qrp() = LR.bobj();
+    LR.qsq() = LR.bsub();
+  }
+}
+__device__ __forceinline__ void walk_done(LaneRef& LR, const RtxLight& L, const dvec3& result) {
+  if (LR.pick() < 0) {
+    LR.i_out() += LR.dattn() * result * ld3(L.color) * LR.dscomp();
+    LR.li()++;
+    LR.st() = ST_LIGHT;
+  } else {
+    LR.area_sum() += result;
+    LR.st() = ST_SRS;
+  }
+}
+
+// discoverMat walk steps and the shadow walk's resume after one (-O o).
+// Inlined: an out-of-line call here (function-call ABI inside the state
+// machine) measured 101 vs 91 ms on the headline frame.
+__device__ __forceinline__ void media_step(LaneRef& LR, const DevScene& S, double aterm) {
+  switch (LR.st()) {
+      case ST_DISC: {
+        // one hit of discoverMat's sorted list, or its end.  The object stack
+        // only grows at the back (leaving hits) and loses its FRONT when an
+        // entering hit matches the back's object (the erase(begin) of
+        // scene.cpp:219-224; decision U4: checkObj returns check()), so the
+        // stack is the pushes [dhead, dtot).  Pass 0 finds dhead and sums the
+        // materials of all pushes; when dhead > 0 pass 1 sums again from
+        // push dhead on (the sum is order dependent).
+        if (LR.bhave()) {
+          const HitRef R = resolve_hit(S, LR.dpos(), LR.ddir(), LR.bobj(), LR.bsub(), nullptr, nullptr);
+          const bool leaving = rtm::dot(R.N, LR.ddir()) > 0;
+          if (leaving && LR.dpush() >= LR.dhead()) {
+            if (!(hit_flags(S, R) & RTX_MF_TRANS)) {
+              LR.dopq() = 1;  // vantablack_mat
+            } else {  // Material::operator+= adds the constant values (material.h:178-189)
+              LR.dkt() += hit_raw(S, R, RTX_P_KT);
+              LR.didx() += hit_raw(S, R, RTX_P_INDEX);
+            }
+          }
+          if (LR.dpass() == 0) {
+            if (leaving) {
+              LR.dpush()++;
+              LR.dlast() = LR.bobj();
+            } else if (LR.dpush() > LR.dhead() && LR.bobj() == LR.dlast()) {
+              LR.dhead()++;
+            }
+          } else if (leaving) {
+            LR.dpush()++;
+          }
+          disc_query(LR, false);
+          break;
+        }
+        if (LR.dpass() == 0) {
+          LR.dtot() = LR.dpush();
+          if (LR.dhead() > 0 && LR.dtot() > LR.dhead()) {  // sum again over the surviving pushes only
+            LR.dpass() = 1;
+            LR.dpush() = 0;
+            LR.dopq() = 0;
+            LR.dkt() = mk3(1.0, 1.0, 1.0);
+            LR.didx() = mk3(1.0, 1.0, 1.0);
+            disc_query(LR, true);
+            break;
+          }
+          if (LR.dhead() > 0) {  // every push erased: the empty stack's average
+            LR.dopq() = 0;
+            LR.dkt() = mk3(1.0, 1.0, 1.0);
+            LR.didx() = mk3(1.0, 1.0, 1.0);
+          }
+        }
+        // blank = (1.0 / size) * blank (operator*(double, Material): each
+        // constant value scaled); an empty stack divides by 0
+        if (LR.dopq()) {
+          LR.mo_trans() = 0;
+          LR.mo_kt() = mk3(0.0, 0.0, 0.0);
+          LR.mo_idx() = intensity(mk3(0.0, 0.0, 0.0));
+        } else {
+          const double s = 1.0 / static_cast<double>(LR.dtot() - LR.dhead());
+          LR.mo_trans() = 1;
+          LR.mo_kt() = LR.dkt() * s;
+          LR.mo_idx() = intensity(LR.didx() * s);
+        }
+        LR.st() = LR.dret() == DISC_RECUR ? ST_RECUR : ST_WALK2;
+        LR.dret() = DISC_NONE;
+        break;
+      }
+      case ST_WALK2: {
+        // the shadow walk's hit (wt, wobj, wsub) after its discoverMat
+        const RtxLight& L = S.lights[LR.li()];
+        LR.bt() = LR.wt();
+        LR.bobj() = LR.wobj();
+        LR.bsub() = LR.wsub();
+        const dvec3 pb = rtm::ray_at(LR.rp(), LR.rd(), LR.st_t()) - LR.rd() * RTX_EPS_BACKUP;
+        const HitRef R = resolve_hit(S, pb, LR.sdir(), LR.bobj(), LR.bsub(), nullptr, nullptr);
+        const bool is_inside = rtm::dot(R.N, LR.sdir()) > 0;
+        bool done = false;
+        dvec3 result = LR.sattn();
+        LR.st() = ST_WALK;  // the walk's next hit comes back to ST_WALK
+        walk_on(LR, S, aterm, R, is_inside, LR.wtr(), LR.mo_trans() != 0, LR.mo_kt(), done, result);
+        if (done) walk_done(LR, L, result);
+        break;
+      }
+      default:
+        break;
+  }
+}
+
 // Run one lane's state machine (trace / traceRay / shade / srsAttenuation,
 // RayTracer.cpp:35-174, material.cpp:34-69, light.cpp:16-53) until it needs
 // a traversal query (L.qmode != Q_NONE) or its sample is finished (ST_IDLE).
 // The pending-ray stack lives in HBM: entry e, field f at
 // pbuf[(e * 13 + f) * nlanes + glane].
-template <bool STATS, bool ADAPTIVE>
+// MEDIA: the -O o (overlapping media) states are compiled in; frames
+// without -O o run the instantiation without them (smaller kernels).
+template <bool STATS, bool ADAPTIVE, bool MEDIA>
 __device__ __forceinline__ void advance_lane(LaneRef& LR, const DevScene& S, const FrameParams& F, Counters& C,
                                              double* __restrict__ sbuf, double* __restrict__ colbuf,
                                              RtxHitRecord* __restrict__ hits, int64_t apix_out, int an,
@@ -415,10 +584,49 @@ __device__ __forceinline__ void advance_lane(LaneRef& LR, const DevScene& S, con
     b[12 * nlanes] = static_cast<double>(depth * 4 + kind);
     ++tp;
   };
+  // traceRay's reflection / refraction (RayTracer.cpp:127-164); m_out =
+  // (trans_o, idx_o, kt_o): air, or discoverMat's material under -O o
+  auto recur = [&](bool trans_o, double idx_o, const dvec3& kt_o) {
+    const int depth = LR.rdepth() - 1;
+    const HitRef R = resolve_hit(S, LR.rp(), LR.rd(), LR.sobj(), LR.ssub(), nullptr, nullptr);
+    const bool leaving = rtm::dot(LR.N(), LR.rd()) >= 0;
+    const bool in_trans = (LR.m_flags() & RTX_MF_TRANS) != 0;
+    const bool next_trans = leaving ? trans_o : in_trans;
+    const dvec3 normal = (leaving ? -1.0 : 1.0) * LR.N();
+    const double c = -1 * rtm::dot(normal, LR.rd());
+    const double eta = next_trans ? (leaving ? hit_index(S, R) : idx_o) / (leaving ? idx_o : hit_index(S, R)) : 0;
+    const double radicand = 1 - eta * eta * (1 - c * c);
+    const bool tir = next_trans && radicand < 0;
+    // push refraction first so that reflection is traced first
+    if (next_trans && !tir && LR.top() < pend_cap) {
+      const dvec3 tp = rtm::ray_at(LR.rp(), LR.rd(), LR.st_t() + RTX_RAY_EPS);
+      const dvec3 td = eta * LR.rd() + (eta * c - sqrt(radicand)) * normal;
+      push(LR.top(), tp, td, LR.W(), leaving ? kt_o : hit_param(S, R, RTX_P_KT), depth, 2);
+      if (STATS) C.secondary++;
+    }
+    if (((LR.m_flags() & RTX_MF_REFL) || tir) && LR.top() < pend_cap) {
+      const dvec3 rdir = LR.rd() + 2 * c * normal;
+      const dvec3 rs = rtm::ray_at(LR.rp(), LR.rd(), LR.st_t() - RTX_RAY_EPS);
+      push(LR.top(), rs, rdir, LR.W() * hit_param(S, R, RTX_P_KR), leaving ? hit_param(S, R, RTX_P_KT) : kt_o, depth,
+           1);
+      if (STATS) C.secondary++;
+    }
+  };
   LR.qmode() = Q_NONE;
+#ifdef RTX_WATCHDOG
+  int wd_steps = 0;
+#endif
   while (LR.st() != ST_IDLE && LR.qmode() == Q_NONE) {
     // the lane state is memory: each step re-reads the few fields it uses
     LR.refresh();
+#ifdef RTX_WATCHDOG
+    if (++wd_steps > 1000000) {
+      printf("rtx watchdog: state loop lane %d st %d dret %d top %d li %d\n", int(glane), LR.st(), LR.dret(), LR.top(),
+             LR.li());
+      LR.st() = ST_IDLE;
+      break;
+    }
+#endif
     switch (LR.st()) {
       case ST_CAM: {
         // next camera ray of trace(x, y) (RayTracer.cpp:35-79)
@@ -583,29 +791,13 @@ __device__ __forceinline__ void advance_lane(LaneRef& LR, const DevScene& S, con
           LR.st() = ST_POP;
           if (aterm > 0.0 && rtm::dot(col, col) < aterm) break;
           if ((LR.m_flags() & RTX_MF_RECUR) && depth > 0) {
-            const HitRef R = resolve_hit(S, LR.rp(), LR.rd(), LR.sobj(), LR.ssub(), nullptr, nullptr);
-            const bool leaving = rtm::dot(LR.N(), LR.rd()) >= 0;
-            const bool in_trans = (LR.m_flags() & RTX_MF_TRANS) != 0;
-            const bool next_trans = leaving ? true : in_trans;  // air is transmissive
-            const dvec3 normal = (leaving ? -1.0 : 1.0) * LR.N();
-            const double c = -1 * rtm::dot(normal, LR.rd());
-            const double eta =
-                next_trans ? (leaving ? hit_index(S, R) : S.air_index) / (leaving ? S.air_index : hit_index(S, R)) : 0;
-            const double radicand = 1 - eta * eta * (1 - c * c);
-            const bool tir = next_trans && radicand < 0;
-            // push refraction first so that reflection is traced first
-            if (next_trans && !tir && LR.top() < pend_cap) {
-              const dvec3 tp = rtm::ray_at(LR.rp(), LR.rd(), LR.st_t() + RTX_RAY_EPS);
-              const dvec3 td = eta * LR.rd() + (eta * c - sqrt(radicand)) * normal;
-              push(LR.top(), tp, td, LR.W(), leaving ? mk3(1.0, 1.0, 1.0) : hit_param(S, R, RTX_P_KT), depth, 2);
-              if (STATS) C.secondary++;
-            }
-            if (((LR.m_flags() & RTX_MF_REFL) || tir) && LR.top() < pend_cap) {
-              const dvec3 rdir = LR.rd() + 2 * c * normal;
-              const dvec3 rs = rtm::ray_at(LR.rp(), LR.rd(), LR.st_t() - RTX_RAY_EPS);
-              push(LR.top(), rs, rdir, LR.W() * hit_param(S, R, RTX_P_KR), leaving ? hit_param(S, R, RTX_P_KT) : mk3(1.0, 1.0, 1.0),
-                   depth, 1);
-              if (STATS) C.secondary++;
+            if (MEDIA && P.overlapping) {
+              // m_out = discoverMat(ray(r.at(t - RAY_EPSILON), d)) (RayTracer.cpp:128)
+              LR.dpos() = rtm::ray_at(LR.rp(), LR.rd(), LR.st_t() - RTX_RAY_EPS);
+              LR.ddir() = LR.rd();
+              disc_start(LR, DISC_RECUR);
+            } else {
+              recur(true, S.air_index, mk3(1.0, 1.0, 1.0));  // m_out = air
             }
           }
           break;
@@ -623,7 +815,7 @@ __device__ __forceinline__ void advance_lane(LaneRef& LR, const DevScene& S, con
         LR.dattn() = light_dist_atten(L, X);
         // shadowAttenuation (light.cpp:16-20) / AreaLight (light.cpp:76-87)
         if (L.type == RTX_LIGHT_DIRECTIONAL || L.type == RTX_LIGHT_POINT) {
-          if (S.skip_dark && LR.dscomp().x == 0.0 && LR.dscomp().y == 0.0 && LR.dscomp().z == 0.0) {
+          if (S.skip_dark && !P.overlapping && LR.dscomp().x == 0.0 && LR.dscomp().y == 0.0 && LR.dscomp().z == 0.0) {
             // the light's term is dattn * sattn * color * 0, and sattn is
             // finite in this scene (kt in [0,1]), so it adds +0: the shadow
             // ray still counts (the reference traces it) but is not traced
@@ -687,6 +879,17 @@ __device__ __forceinline__ void advance_lane(LaneRef& LR, const DevScene& S, con
         LR.st() = ST_WALK;
         break;
       }
+      case ST_RECUR: {
+        // after discoverMat (-O o): traceRay's recursion with its material
+        LR.st() = ST_POP;
+        if (MEDIA) recur(LR.mo_trans() != 0, LR.mo_idx(), LR.mo_kt());
+        break;
+      }
+      case ST_DISC:
+      case ST_WALK2:
+        if (MEDIA) media_step(LR, S, aterm);  // -O o only
+        else LR.st() = ST_IDLE;
+        break;
       case ST_WALK: {
         const RtxLight& L = S.lights[LR.li()];
         bool done = false;
@@ -717,31 +920,21 @@ __device__ __forceinline__ void advance_lane(LaneRef& LR, const DevScene& S, con
           }
           if (limit) {
             done = true;
+          } else if (MEDIA && P.overlapping) {
+            // m_out = discoverMat(ray(r2l)) from the moved origin (light.cpp:38-39)
+            LR.wt() = LR.bt();
+            LR.wtr() = t;
+            LR.wobj() = LR.bobj();
+            LR.wsub() = LR.bsub();
+            LR.dpos() = LR.wpos();
+            LR.ddir() = LR.sdir();
+            disc_start(LR, DISC_WALK);
+            break;
           } else {
-            const bool next_trans = is_inside ? true : ((hit_flags(S, R) & RTX_MF_TRANS) != 0);
-            if (!next_trans || (aterm > 0.0 && rtm::dot(LR.sattn(), LR.sattn()) < aterm * aterm)) {
-              result = mk3(0.0, 0.0, 0.0);
-              done = true;
-            } else {
-              const dvec3 kt = is_inside ? hit_param(S, R, RTX_P_KT) : mk3(1.0, 1.0, 1.0);
-              LR.sattn() *= rtm::pow3(kt, t);
-              LR.qmode() = Q_NEXT;
-              LR.qtp() = LR.bt();
-              LR.qrp() = LR.bobj();
-              LR.qsq() = LR.bsub();
-            }
+            walk_on(LR, S, aterm, R, is_inside, t, true, mk3(1.0, 1.0, 1.0), done, result);  // m_out = air
           }
         }
-        if (done) {
-          if (LR.pick() < 0) {
-            LR.i_out() += LR.dattn() * result * ld3(L.color) * LR.dscomp();
-            LR.li()++;
-            LR.st() = ST_LIGHT;
-          } else {
-            LR.area_sum() += result;
-            LR.st() = ST_SRS;
-          }
-        }
+        if (done) walk_done(LR, L, result);
         break;
       }
       default:
@@ -752,7 +945,7 @@ __device__ __forceinline__ void advance_lane(LaneRef& LR, const DevScene& S, con
 
 }
 
-template <bool STATS, bool ADAPTIVE>
+template <bool STATS, bool ADAPTIVE, bool MEDIA>
 __global__ void __launch_bounds__(WG) render_kernel(DevScene S, const DevScene* __restrict__ Sg, const FrameParams* __restrict__ Fp,
                                                      unsigned long long* __restrict__ work,
                                                      double* __restrict__ sbuf, RtxHitRecord* __restrict__ hits,
@@ -784,6 +977,9 @@ __global__ void __launch_bounds__(WG) render_kernel(DevScene S, const DevScene* 
   LR.st() = ST_IDLE;
   LR.sample_slot() = -1;
 
+#ifdef RTX_WATCHDOG
+  int wd_queries = 0;
+#endif
   // ---- wave-uniform scheduler state
   unsigned long long qnext = 0, qend = 0;
   bool exhausted = false;
@@ -935,9 +1131,9 @@ __global__ void __launch_bounds__(WG) render_kernel(DevScene S, const DevScene* 
         if (fsp == 0 && !need_new_pixel) {
           if (lane == 0) {  // setPixel (RayTracer.cpp:388-394)
             if (rgb8) {
-              rgb8[apix_out * 3 + 0] = (uint8_t)(int)(255.0 * LR.acc().x);
-              rgb8[apix_out * 3 + 1] = (uint8_t)(int)(255.0 * LR.acc().y);
-              rgb8[apix_out * 3 + 2] = (uint8_t)(int)(255.0 * LR.acc().z);
+              rgb8[apix_out * 3 + 0] = rtm::to_byte(LR.acc().x);
+              rgb8[apix_out * 3 + 1] = rtm::to_byte(LR.acc().y);
+              rgb8[apix_out * 3 + 2] = rtm::to_byte(LR.acc().z);
             }
             if (rgbf) {
               rgbf[apix_out * 3 + 0] = LR.acc().x;
@@ -1005,7 +1201,7 @@ __global__ void __launch_bounds__(WG) render_kernel(DevScene S, const DevScene* 
     }
 
     // ------------------------------------------------ advance lanes to their next query
-    advance_lane<STATS, ADAPTIVE>(LR, *Sg, F, C, sbuf, colbuf, hits, apix_out, an, pbuf, nlanes, glane, pend_cap);
+    advance_lane<STATS, ADAPTIVE, MEDIA>(LR, *Sg, F, C, sbuf, colbuf, hits, apix_out, an, pbuf, nlanes, glane, pend_cap);
 
     // ------------------------------------------------ exit / traversal
     const unsigned long long busy = __ballot(LR.qmode() != Q_NONE);
@@ -1017,12 +1213,24 @@ __global__ void __launch_bounds__(WG) render_kernel(DevScene S, const DevScene* 
       dvec3 qP = LR.rp(), qD = LR.rd();
       double qlim = RTX_INF;
       if (LR.qmode() == Q_NEXT) {
-        qP = rtm::ray_at(LR.rp(), LR.rd(), LR.st_t()) - LR.rd() * RTX_EPS_BACKUP;
-        qD = LR.sdir();
         double qblk;
-        shadow_bounds(S, S.lights[LR.li()], qP, LR.qrp() < 0, qlim, qblk);
+        next_query_ray<MEDIA>(S, LR, qP, qD, qlim, qblk);
       }
       LR.bhave() = traverse<STATS>(S, LR.qmode(), qP, qD, LR.qtp(), LR.qrp(), LR.qsq(), qlim, LR.bt(), LR.bobj(), LR.bsub(), stk, lane, C);
+#ifdef RTX_WATCHDOG
+      // debugging aid (opt-in): report a lane whose sample runs away
+      if (++wd_queries == 200000) {
+        printf("rtx watchdog: lane %d st %d qm %d dret %d dpass %d dpush %d dhead %d dtot %d bt %.17g bobj %d bsub %d "
+               "qtp %.17g qrp %d qsq %d li %d top %d P (%.17g %.17g %.17g) D (%.17g %.17g %.17g)\n",
+               int(glane), LR.st(), LR.qmode(), LR.dret(), LR.dpass(), LR.dpush(), LR.dhead(), LR.dtot(), LR.bt(),
+               LR.bobj(), LR.bsub(), LR.qtp(), LR.qrp(), LR.qsq(), LR.li(), LR.top(), qP.x, qP.y, qP.z, qD.x, qD.y,
+               qD.z);
+      }
+      if (wd_queries >= 200000 && wd_queries < 200012)
+        printf("rtx watchdog: lane %d step st %d qm %d bt %.17g bobj %d bsub %d have %d\n", int(glane), LR.st(),
+               LR.qmode(), LR.bt(), LR.bobj(), LR.bsub(), LR.bhave());
+      if (wd_queries > 200012) LR.st() = ST_IDLE;
+#endif
     }
   }
   if (STATS) {
@@ -1112,7 +1320,7 @@ __device__ __forceinline__ void claim_sample(LaneRef& L, const FrameParams& F, R
   }
 }
 
-template <bool STATS>
+template <bool STATS, bool MEDIA>
 __global__ void __launch_bounds__(WG, RTX_ADV_WAVES) advance_kernel(DevScene S, const DevScene* __restrict__ Sg, const FrameParams* __restrict__ Fp, LaneMem lm,
                                                       double* __restrict__ sbuf, RtxHitRecord* __restrict__ hits,
                                                       double* __restrict__ pbuf, int pend_cap, QList q0, QList q1,
@@ -1137,7 +1345,7 @@ __global__ void __launch_bounds__(WG, RTX_ADV_WAVES) advance_kernel(DevScene S, 
     for (;;) {
       claim_sample(L, F, hits, slot);
       if (L.st() == ST_IDLE) break;
-      advance_lane<STATS, false>(L, *Sg, F, C, sbuf, nullptr, hits, 0, 0, pbuf, lm.n, static_cast<size_t>(slot),
+      advance_lane<STATS, false, MEDIA>(L, *Sg, F, C, sbuf, nullptr, hits, 0, 0, pbuf, lm.n, static_cast<size_t>(slot),
                                  pend_cap);
       if (L.qmode() != Q_NONE) break;
     }
@@ -1160,9 +1368,7 @@ __global__ void __launch_bounds__(WG, RTX_ADV_WAVES) advance_kernel(DevScene S, 
       dvec3 qP = L.rp(), qD = L.rd();
       double qlim = RTX_INF, qblk = -RTX_INF;
       if (m == Q_NEXT) {
-        qP = rtm::ray_at(L.rp(), L.rd(), L.st_t()) - L.rd() * RTX_EPS_BACKUP;
-        qD = L.sdir();
-        shadow_bounds(S, S.lights[L.li()], qP, L.qrp() < 0, qlim, qblk);
+        next_query_ray<MEDIA>(S, L, qP, qD, qlim, qblk);
       }
       Q.d[8 * cap + k] = qblk;
       Q.slot[k] = slot;
@@ -1207,7 +1413,7 @@ __global__ void __launch_bounds__(WG, RTX_ADV_WAVES) advance_kernel(DevScene S, 
 // lane state).  In the batched iterations every launch waits for its slowest
 // query (grazing rays take up to ~1700 steps), so a frame's tail costs
 // (iterations) x (worst query); here each lane only waits for its own.
-template <bool STATS>
+template <bool STATS, bool MEDIA>
 __global__ void __launch_bounds__(WG) tail_kernel(DevScene S, const DevScene* __restrict__ Sg,
                                                    const FrameParams* __restrict__ Fp, LaneMem lm,
                                                    double* __restrict__ sbuf, RtxHitRecord* __restrict__ hits,
@@ -1237,17 +1443,15 @@ __global__ void __launch_bounds__(WG) tail_kernel(DevScene S, const DevScene* __
       L.qmode() = Q_NONE;
       claim_sample(L, F, hits, slot);
       if (L.st() == ST_IDLE) break;
-      advance_lane<STATS, false>(L, *Sg, F, C, sbuf, nullptr, hits, 0, 0, pbuf, lm.n, static_cast<size_t>(slot),
+      advance_lane<STATS, false, MEDIA>(L, *Sg, F, C, sbuf, nullptr, hits, 0, 0, pbuf, lm.n, static_cast<size_t>(slot),
                                  pend_cap);
       const int qm = L.qmode();
       if (qm == Q_NONE) continue;
       dvec3 qP = L.rp(), qD = L.rd();
       double qlim = RTX_INF;
       if (qm == Q_NEXT) {
-        qP = rtm::ray_at(L.rp(), L.rd(), L.st_t()) - L.rd() * RTX_EPS_BACKUP;
-        qD = L.sdir();
         double qblk;
-        shadow_bounds(S, S.lights[L.li()], qP, L.qrp() < 0, qlim, qblk);
+        next_query_ray<MEDIA>(S, L, qP, qD, qlim, qblk);
       }
       double bt;
       int bobj, bsub;
@@ -1284,17 +1488,15 @@ __global__ void __launch_bounds__(WG) tail_kernel(DevScene S, const DevScene* __
           valid = false;
           break;
         }
-        advance_lane<STATS, false>(L, *Sg, F, C, sbuf, nullptr, hits, 0, 0, pbuf, lm.n, static_cast<size_t>(slot),
+        advance_lane<STATS, false, MEDIA>(L, *Sg, F, C, sbuf, nullptr, hits, 0, 0, pbuf, lm.n, static_cast<size_t>(slot),
                                    pend_cap);
         qm = L.qmode();
         if (qm == Q_NONE) continue;
         dvec3 qP = L.rp(), qD = L.rd();
         double qlim = RTX_INF;
         if (qm == Q_NEXT) {
-          qP = rtm::ray_at(L.rp(), L.rd(), L.st_t()) - L.rd() * RTX_EPS_BACKUP;
-          qD = L.sdir();
           double qblk;
-          shadow_bounds(S, S.lights[L.li()], qP, L.qrp() < 0, qlim, qblk);
+          next_query_ray<MEDIA>(S, L, qP, qD, qlim, qblk);
         }
         if (STATS) queries++;
         has_q = qm == Q_CLOSEST
@@ -1536,9 +1738,9 @@ __global__ void __launch_bounds__(WG) reduce_kernel(const FrameParams* __restric
   }
   if (F.P.aa_mode != RTX_AA_NONE) acc = acc / double(F.s * F.s);
   if (rgb8) {
-    rgb8[o * 3 + 0] = (uint8_t)(int)(255.0 * acc.x);
-    rgb8[o * 3 + 1] = (uint8_t)(int)(255.0 * acc.y);
-    rgb8[o * 3 + 2] = (uint8_t)(int)(255.0 * acc.z);
+    rgb8[o * 3 + 0] = rtm::to_byte(acc.x);
+    rgb8[o * 3 + 1] = rtm::to_byte(acc.y);
+    rgb8[o * 3 + 2] = rtm::to_byte(acc.z);
   }
   if (rgbf) {
     rgbf[o * 3 + 0] = acc.x;
@@ -1660,6 +1862,18 @@ int isqrt_floor(int v) {
 }
 
 }  // namespace
+
+// compile-time dispatch of runtime flags to kernel template arguments
+template <class Fn>
+void dispatch2(bool a, bool b, Fn&& f) {
+  if (a) {
+    if (b) f(std::true_type{}, std::true_type{});
+    else f(std::true_type{}, std::false_type{});
+  } else {
+    if (b) f(std::false_type{}, std::true_type{});
+    else f(std::false_type{}, std::false_type{});
+  }
+}
 
 extern "C" {
 
@@ -1821,10 +2035,6 @@ static rtx_status build_frame(const SceneState* st, const RtxRenderParams* p, Fr
     g_err = "rtx_render: width/height must be positive";
     return RTX_ERR_INVALID;
   }
-  if (p->overlapping) {
-    g_err = "rtx_render: -O o (overlapping objects) is not supported on the GPU path";
-    return RTX_ERR_INVALID;
-  }
   if (p->depth > MAX_DEPTH) {
     g_err = "rtx_render: recursion depth above 16 is not supported by this build";
     return RTX_ERR_CAPACITY;
@@ -1967,6 +2177,7 @@ rtx_status rtx_render(void* scene, const RtxRenderParams* params, uint8_t* rgb8,
     }
   }
   const bool adaptive = params->aa_mode == RTX_AA_ADAPTIVE;
+  const bool media = params->overlapping != 0;  // -O o: the kernels with the discoverMat states
   // wavefront path by default; adaptive AA (per-pixel sample frames) and
   // RTX_MEGAKERNEL=1 use the persistent megakernel (kernels)
   const char* mk_env = getenv("RTX_MEGAKERNEL");
@@ -2030,10 +2241,11 @@ rtx_status rtx_render(void* scene, const RtxRenderParams* params, uint8_t* rgb8,
       return RTX_ERR_CAPACITY;
     }
     // persistent grid: as many resident workgroups as the occupancy allows
-    const void* kfn = stats ? (adaptive ? reinterpret_cast<const void*>(render_kernel<true, true>)
-                                        : reinterpret_cast<const void*>(render_kernel<true, false>))
-                            : (adaptive ? reinterpret_cast<const void*>(render_kernel<false, true>)
-                                        : reinterpret_cast<const void*>(render_kernel<false, false>));
+    const void* kfn = nullptr;
+    dispatch2(stats, adaptive, [&](auto st_, auto ad_) {
+      kfn = media ? reinterpret_cast<const void*>(render_kernel<decltype(st_)::value, decltype(ad_)::value, true>)
+                  : reinterpret_cast<const void*>(render_kernel<decltype(st_)::value, decltype(ad_)::value, false>);
+    });
     int per_cu = 0;
     HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kfn, WG, lds));
     if (per_cu < 1) per_cu = 1;
@@ -2061,24 +2273,17 @@ rtx_status rtx_render(void* scene, const RtxRenderParams* params, uint8_t* rgb8,
     hipEvent_t e0, e1;
     if ((rc = get_event(&e0)) != RTX_OK || (rc = get_event(&e1)) != RTX_OK) return rc;
     HIP_TRY(hipEventRecord(e0, stream));
-    if (stats) {
-      if (adaptive)
-        hipLaunchKernelGGL((render_kernel<true, true>), dim3(grid), dim3(WG), lds, stream, st->S_launch, st->d_scene, st->d_frame,
-                           st->d_work, sb, d_hits, d_rgb8, d_rgbf, st->d_stats, st->stack_cap, st->d_pbuf, pend_cap, lm);
-      else
-        hipLaunchKernelGGL((render_kernel<true, false>), dim3(grid), dim3(WG), lds, stream, st->S_launch, st->d_scene,
-                           st->d_frame, st->d_work, sb, d_hits, d_rgb8, d_rgbf, st->d_stats, st->stack_cap,
-                           st->d_pbuf, pend_cap, lm);
-    } else {
-      if (adaptive)
-        hipLaunchKernelGGL((render_kernel<false, true>), dim3(grid), dim3(WG), lds, stream, st->S_launch, st->d_scene,
-                           st->d_frame, st->d_work, sb, d_hits, d_rgb8, d_rgbf, st->d_stats, st->stack_cap,
+    dispatch2(stats, adaptive, [&](auto st_, auto ad_) {
+      constexpr bool ST_ = decltype(st_)::value, AD_ = decltype(ad_)::value;
+      if (media)
+        hipLaunchKernelGGL((render_kernel<ST_, AD_, true>), dim3(grid), dim3(WG), lds, stream, st->S_launch,
+                           st->d_scene, st->d_frame, st->d_work, sb, d_hits, d_rgb8, d_rgbf, st->d_stats, st->stack_cap,
                            st->d_pbuf, pend_cap, lm);
       else
-        hipLaunchKernelGGL((render_kernel<false, false>), dim3(grid), dim3(WG), lds, stream, st->S_launch, st->d_scene,
-                           st->d_frame, st->d_work, sb, d_hits, d_rgb8, d_rgbf, st->d_stats, st->stack_cap,
+        hipLaunchKernelGGL((render_kernel<ST_, AD_, false>), dim3(grid), dim3(WG), lds, stream, st->S_launch,
+                           st->d_scene, st->d_frame, st->d_work, sb, d_hits, d_rgb8, d_rgbf, st->d_stats, st->stack_cap,
                            st->d_pbuf, pend_cap, lm);
-    }
+    });
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipEventRecord(e1, stream));
     frame_events.push_back({e0, e1});
@@ -2157,8 +2362,10 @@ rtx_status rtx_render(void* scene, const RtxRenderParams* params, uint8_t* rgb8,
     if (tail_env) tail_slots = atoll(tail_env);
     F.qchunk = 64;
     HIP_TRY(hipMemcpyAsync(st->d_frame, &F, sizeof(FrameParams), hipMemcpyHostToDevice, stream));
-    // every slot ST_IDLE, kdone = 0, no pending query
-    HIP_TRY(hipMemsetAsync(A.i, 0, ns * LI_COUNT * sizeof(int), stream));
+    // every slot ST_IDLE, kdone = 0, outside a discoverMat walk (every other
+    // field is written before it is read; the int rows are field-major)
+    for (int f : {int(LI_st), int(LI_kdone), int(LI_dret)})
+      HIP_TRY(hipMemsetAsync(A.i + size_t(f) * ns, 0, ns * sizeof(int), stream));
     HIP_TRY(hipMemsetAsync(st->d_counters, 0, 16 * CNT_PER_GROUP * sizeof(unsigned int), stream));
     const size_t lds_stacks = size_t(st->stack_cap) * 64 * sizeof(int) * WAVES_PER_WG;
 #ifdef RTX_LDS_STAGE
@@ -2202,12 +2409,11 @@ rtx_status rtx_render(void* scene, const RtxRenderParams* params, uint8_t* rgb8,
           const int* live_in = live[size_t(g) * 2 + (odd ? 0 : 1)];
           const int64_t lb = live_bound[size_t(g)];
           const int64_t grid = std::max<int64_t>(1, (lb + WG - 1) / WG);
-          if (stats)
-            hipLaunchKernelGGL((tail_kernel<true>), dim3(grid), dim3(WG), lds, sg, S, st->d_scene, st->d_frame, A, sb,
-                               d_hits, st->d_pbuf, pend_cap, cnt, live_in, in_cnt, st->stack_cap, st->d_stats);
-          else
-            hipLaunchKernelGGL((tail_kernel<false>), dim3(grid), dim3(WG), lds, sg, S, st->d_scene, st->d_frame, A, sb,
-                               d_hits, st->d_pbuf, pend_cap, cnt, live_in, in_cnt, st->stack_cap, st->d_stats);
+          dispatch2(stats, media, [&](auto st_, auto md_) {
+            hipLaunchKernelGGL((tail_kernel<decltype(st_)::value, decltype(md_)::value>), dim3(grid), dim3(WG), lds, sg,
+                               S, st->d_scene, st->d_frame, A, sb, d_hits, st->d_pbuf, pend_cap, cnt, live_in, in_cnt,
+                               st->stack_cap, st->d_stats);
+          });
           HIP_TRY(hipGetLastError());
           done[size_t(g)] = 1;
           ++ndone;
@@ -2224,14 +2430,11 @@ rtx_status rtx_render(void* scene, const RtxRenderParams* params, uint8_t* rgb8,
         const int64_t lb = live_bound[size_t(g)];
         const int64_t agrid = first ? per : std::max<int64_t>(1, std::min<int64_t>(per, (lb + WG - 1) / WG));
         const int64_t tg = std::max<int64_t>(1, std::min<int64_t>(tgrid, (lb + WG - 1) / WG));
-        if (stats)
-          hipLaunchKernelGGL((advance_kernel<true>), dim3(agrid), dim3(WG), 0, sg, S, st->d_scene, st->d_frame, A, sb,
-                             d_hits, st->d_pbuf, pend_cap, q0, q1, cnt, st->d_stats, static_cast<int>(g * gslots),
-                             live_in, live_out, first, in_cnt, out_cnt);
-        else
-          hipLaunchKernelGGL((advance_kernel<false>), dim3(agrid), dim3(WG), 0, sg, S, st->d_scene, st->d_frame, A, sb,
-                             d_hits, st->d_pbuf, pend_cap, q0, q1, cnt, st->d_stats, static_cast<int>(g * gslots),
-                             live_in, live_out, first, in_cnt, out_cnt);
+        dispatch2(stats, media, [&](auto st_, auto md_) {
+          hipLaunchKernelGGL((advance_kernel<decltype(st_)::value, decltype(md_)::value>), dim3(agrid), dim3(WG), 0, sg,
+                             S, st->d_scene, st->d_frame, A, sb, d_hits, st->d_pbuf, pend_cap, q0, q1, cnt,
+                             st->d_stats, static_cast<int>(g * gslots), live_in, live_out, first, in_cnt, out_cnt);
+        });
         if (stats) {
           hipLaunchKernelGGL((trace_kernel<true, Q_CLOSEST>), dim3(tg), dim3(WG), lds, sg, S, st->d_scene, q0,
                              cnt, A, st->stack_cap, st->d_stats);

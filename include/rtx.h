@@ -187,7 +187,7 @@ typedef struct RtxRenderParams {
   int32_t dof_div;              /* -B for d                                    */
   int32_t anaglyph;             /* -O g                                        */
   int32_t ss_res;               /* -O s -A n (soft-shadow rays)                */
-  int32_t overlapping;          /* -O o (unsupported on the GPU path: error)   */
+  int32_t overlapping;          /* -O o (Scene::discoverMat media)             */
   double aa_thresh;             /* -B for a                                    */
   double aterm_thresh;          /* -O c -A x                                   */
   double dof_fd;                /* -A for d                                    */

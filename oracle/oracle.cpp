@@ -113,6 +113,14 @@ rtxh::Material make_air() {
   return a;
 }
 const rtxh::Material g_air = make_air();
+// vantablack_mat (material.cpp:22-26): all zero, index 0, setBools => no flags
+rtxh::Material make_vantablack() {
+  rtxh::Material a;
+  a.p[rtxh::P_INDEX].v = mk3(0.0, 0.0, 0.0);
+  a.setBools();
+  return a;
+}
+const rtxh::Material g_vantablack = make_vantablack();
 
 // ---------------------------------------------------------------- bbox (bbox.cc)
 struct BBox {
@@ -811,6 +819,7 @@ dvec2 hammersley(int n, int N) {
 }
 
 thread_local int tl_ss_res = 5;
+thread_local bool tl_overlapping = false;  // -O o
 
 struct AreaLight : PointLight {  // light.cpp:76-104
   virtual bool validImpact(const Ray&, const dvec3&) const { return true; }
@@ -952,6 +961,44 @@ struct Scene {
     }
     return iv;
   }
+
+  // Scene::discoverMat (scene.cpp:212-237).  isect::checkObj has no return
+  // statement (ray.cpp:43-45); decision U4: it returns a.obj->check(b.obj),
+  // i.e. the same primitive (a mesh for all of its faces, trimesh.h:139).
+  rtxh::Material discoverMat(Ray r) const {
+    std::vector<Isect> iv = intersectList(r);
+    std::sort(iv.begin(), iv.end(), [](const Isect& a, const Isect& b) { return a.t < b.t; });
+    std::vector<Isect> obj_stk;
+    for (const Isect& iv_it : iv) {
+      const bool leaving = rtm::dot(iv_it.N, r.d) > 0;
+      if (leaving) {
+        obj_stk.push_back(iv_it);
+      } else {
+        // the loop tests the BACK every time and erases the element at `it`
+        for (auto it = obj_stk.begin(); it != obj_stk.end(); ++it) {
+          if (iv_it.obj == obj_stk.back().obj) {
+            obj_stk.erase(it);
+            break;
+          }
+        }
+      }
+    }
+    rtxh::Material blank = g_air;
+    for (const Isect& os_it : obj_stk) {
+      const rtxh::Material& m = os_it.getMaterial();
+      if (!m.trans) return g_vantablack;
+      // Material::operator+= (material.h:178-189): constant values, no bump
+      for (int k : {rtxh::P_KE, rtxh::P_KA, rtxh::P_KS, rtxh::P_KD, rtxh::P_KR, rtxh::P_KT, rtxh::P_INDEX,
+                    rtxh::P_SHININESS, rtxh::P_GLOSS})
+        blank.p[k].v += m.p[k].v;
+    }
+    // blank = (1.0 / size) * blank (operator*(double, Material), material.h:277-290)
+    const double d = 1.0 / (double)obj_stk.size();
+    for (int k : {rtxh::P_KE, rtxh::P_KA, rtxh::P_KS, rtxh::P_KD, rtxh::P_KR, rtxh::P_KT, rtxh::P_INDEX,
+                  rtxh::P_SHININESS, rtxh::P_GLOSS})
+      blank.p[k].v = mk3(blank.p[k].v.x * d, blank.p[k].v.y * d, blank.p[k].v.z * d);
+    return blank;
+  }
 };
 
 dvec3 pvalue(const rtxh::MatParam& q, const Isect& is) {
@@ -974,7 +1021,9 @@ dvec3 Light::srsAttenuation(const dvec3& pos, const dvec3& dir) const {
     const rtxh::Material& m_in = iv_it.getMaterial();
     const bool is_inside = rtm::dot(iv_it.N, r2l.d) > 0;
     r2l.p = r2l.at(iv_it.t);
-    const rtxh::Material& m_out = g_air;  // -O o (overlapping media) not restated
+    rtxh::Material m_disc;
+    if (tl_overlapping) m_disc = tl_scene->discoverMat(r2l);  // light.cpp:39
+    const rtxh::Material& m_out = tl_overlapping ? m_disc : g_air;
     const rtxh::Material& curr_m = is_inside ? m_in : m_out;
     const rtxh::Material& next_m = is_inside ? m_out : m_in;
     if (sattnLimitCheck(r2l, iv_it)) return sattn;
@@ -1060,7 +1109,9 @@ struct Tracer {
       colorC = shade(m_in, scene, r, i);
       if (thresh > 0.0 && rtm::dot(colorC, colorC) < thresh) return colorC;
       if (m_in.recur && depth > 0) {
-        const rtxh::Material& m_out = g_air;
+        rtxh::Material m_disc;  // RayTracer.cpp:128
+        if (P.overlapping) m_disc = scene->discoverMat(Ray(r.at(i.t - RAY_EPSILON), r.d));
+        const rtxh::Material& m_out = P.overlapping ? m_disc : g_air;
         bool leaving = rtm::dot(i.N, r.d) >= 0;
         const rtxh::Material& curr_m = leaving ? m_in : m_out;
         const rtxh::Material& next_m = leaving ? m_out : m_in;
@@ -1295,7 +1346,6 @@ int oracle_render(const char* ray_path, const char* cubemap_file, const RtxRende
     T.P = *params;
     T.buffer_width = params->width;
     T.buffer_height = params->height;
-    if (params->overlapping) throw rtxh::ParseError("-O o (overlapping objects) is not restated");
     const int w = params->width, h = params->height;
     int x0 = 0, y0 = 0, x1 = w, y1 = h;
     if (rect && rect->x1 > 0) {
@@ -1311,6 +1361,7 @@ int oracle_render(const char* ray_path, const char* cubemap_file, const RtxRende
     {
       orc::tl_scene = S.get();
       orc::tl_ss_res = ss_res;
+      orc::tl_overlapping = params->overlapping != 0;
       orc::tl = orc::Counters();
 #pragma omp for collapse(2) schedule(dynamic, 4)
       for (int i = x0; i < x1; i++) {
@@ -1356,9 +1407,9 @@ int oracle_render(const char* ray_path, const char* cubemap_file, const RtxRende
           // RayTracer::setPixel (RayTracer.cpp:388-394)
           if (rgb8) {
             uint8_t* pixel = rgb8 + pix * 3;
-            pixel[0] = (int)(255.0 * col.x);
-            pixel[1] = (int)(255.0 * col.y);
-            pixel[2] = (int)(255.0 * col.z);
+            pixel[0] = rtm::to_byte(col.x);
+            pixel[1] = rtm::to_byte(col.y);
+            pixel[2] = rtm::to_byte(col.z);
           }
           if (rgb_f64) {
             rgb_f64[pix * 3 + 0] = col.x;

@@ -23,4 +23,10 @@ CASES = [
     ("cubemap_cones", "cones.ray", "-w 48 -r 3 -c cubemap/posx.bmp"),
     ("cubemap_spheres_aa", "spheres_overlap.ray", "-w 32 -r 4 -O r -A 2 -c cubemap/negz.bmp"),
     ("cubemap_r0", "cones.ray", "-w 24 -r 0 -c cubemap/posy.bmp"),
+    # -O o: discoverMat media on refraction and along shadow walks
+    ("overlap_spheres", "spheres_overlap.ray", "-w 48 -r 5 -O o"),
+    ("overlap_cones", "cones.ray", "-w 40 -r 4 -O o"),
+    ("overlap_hitchcock", "hitchcock.ray", "-w 40 -r 3 -O o"),
+    ("overlap_trimesh_aa", "trimesh2_square.ray", "-w 24 -r 3 -O o -O r -A 2"),
+    ("overlap_area_cube", "lava_box.ray", "-w 32 -r 3 -O o -O s -A 4 -c cubemap/posz.bmp"),
 ]

@@ -213,7 +213,7 @@ def test_oracle_matches_golden(pkg, orc, fname):
     opts = cli_opts(pkg, str(g["flags"]))
     r = orc.render(pkg, scene_path(str(g["scene"])), opts, want_hits=True)
     assert np.array_equal(r["rgb8"], g["rgb8"])
-    assert np.abs(r["rgb"] - g["rgb"]).max() <= 1e-12
+    np.testing.assert_allclose(r["rgb"], g["rgb"], rtol=0, atol=1e-12, equal_nan=True)  # -O o can give NaN
     for f in ("object", "face", "scene_leaf", "mesh_leaf", "nrays"):
         assert np.array_equal(r["hits"][f], g["hits"][f]), f
     assert r["stats"]["rays"] == int(g["rays"])

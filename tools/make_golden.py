@@ -23,6 +23,7 @@ GOLDEN_CASES = [
     ("trimesh2_square", "trimesh2_square.ray", "-w 20 -r 5"),
     ("cones", "cones.ray", "-w 24 -r 4"),
     ("cubemap_cones", "cones.ray", "-w 24 -r 3 -c cubemap/posx.bmp"),
+    ("overlap_spheres", "spheres_overlap.ray", "-w 24 -r 5 -O o"),
 ]
 
 
