@@ -75,6 +75,18 @@ struct FrameParams {
   int wf_nslot;              // wavefront path: path slots (samples dealt slot + k * wf_nslot)
   int ncam;                  // camera rays per sample (1, or divs + 1 with DoF)
   int cam_split;             // 1: each DoF camera ray is its own work unit (wavefront path)
+  // wavefront slot layout: G groups of wf_gs slots; the first wf_gsamp slots
+  // of a group take samples (sample slot g * wf_gsamp + l, samples dealt
+  // sample slot + k * wf_nslot), the rest are fork slots
+  int wf_gs, wf_gsamp;
+  // ray-tree forking (wavefront path, frames with fewer samples than slots):
+  // a reflection / refraction ray at heap position 2 .. fork_npos + 1 of its
+  // sample's ray tree (root 1, children 2p and 2p + 1) may run its sub-tree
+  // on a fork slot; the sub-tree's colour sum goes to fbuf[sample][pos - 2]
+  // and its bit to fmask[sample], reduce_kernel adds them before the clamp
+  int fork_on, fork_npos;
+  double* fbuf;
+  unsigned int* fmask;
 };
 
 // Work item -> pixel; out_index is the output slot (packed tile order or
@@ -324,7 +336,7 @@ struct Pending {
 // with it.  LaneRef gives a lane's fields as accessors (LR.st(), LR.acc(), ...).
 #define LANE_INT_FIELDS(X) X(st) X(sample_slot) X(rec_on) X(pass) X(camk) X(nrays) X(top) X(rdepth) X(rkind) \
   X(first_query) X(cam_end) X(sobj) X(ssub) X(m_flags) X(li) X(pick) X(qmode) X(qrp) X(qsq) X(kdone) X(bobj) X(bsub) X(bhave) \
-  X(dret) X(dpass) X(dpush) X(dhead) X(dtot) X(dlast) X(dopq) X(mo_trans) X(wobj) X(wsub)
+  X(dret) X(dpass) X(dpush) X(dhead) X(dtot) X(dlast) X(dopq) X(mo_trans) X(wobj) X(wsub) X(fpos) X(rpos)
 #define LANE_DBL_FIELDS(X) X(sx) X(sy) X(st_t) X(m_sh) X(dattn) X(last_t) X(qtp) X(bt) X(mo_idx) X(wt) X(wtr)
 #define LANE_VEC_FIELDS(X) X(acc) X(rp) X(rd) X(W) X(N) X(i_out) X(dscomp) X(m_kd) X(m_ks) X(area_sum) X(sdir) \
   X(wpos) X(sattn) X(dpos) X(ddir) X(dkt) X(didx) X(mo_kt)
@@ -560,6 +572,23 @@ __device__ __forceinline__ void media_step(LaneRef& LR, const DevScene& S, doubl
   }
 }
 
+// Fork slots of the calling advance_kernel's group (FORK instantiations):
+// a forked ray's sub-tree starts on slot spare_base + atomicAdd(fcnt) while
+// fewer than spare_n were taken, and joins this iteration's live list.
+struct ForkCtx {
+  unsigned int* fcnt;
+  int spare_base;
+  unsigned int spare_n;
+  int* live_out;
+  unsigned int* live_cnt;
+};
+
+// pending-ray entry field 12: heap position (0: past the fork depth), depth
+// and kind (0 camera, 1 reflection, 2 refraction), exact in a double
+__device__ __forceinline__ double pend_code(int pos, int depth, int kind) {
+  return static_cast<double>((static_cast<int64_t>(pos) << 40) + (int64_t(1) << 39) + depth * 4 + kind);
+}
+
 // Run one lane's state machine (trace / traceRay / shade / srsAttenuation,
 // RayTracer.cpp:35-174, material.cpp:34-69, light.cpp:16-53) until it needs
 // a traversal query (L.qmode != Q_NONE) or its sample is finished (ST_IDLE).
@@ -567,22 +596,54 @@ __device__ __forceinline__ void media_step(LaneRef& LR, const DevScene& S, doubl
 // pbuf[(e * 13 + f) * nlanes + glane].
 // MEDIA: the -O o (overlapping media) states are compiled in; frames
 // without -O o run the instantiation without them (smaller kernels).
-template <bool STATS, bool ADAPTIVE, bool MEDIA>
+template <bool STATS, bool ADAPTIVE, bool MEDIA, bool FORK = false>
 __device__ __forceinline__ void advance_lane(LaneRef& LR, const DevScene& S, const FrameParams& F, Counters& C,
                                              double* __restrict__ sbuf, double* __restrict__ colbuf,
                                              RtxHitRecord* __restrict__ hits, int64_t apix_out, int an,
-                                             double* __restrict__ pbuf, size_t nlanes, size_t glane, int pend_cap) {
+                                             double* __restrict__ pbuf, size_t nlanes, size_t glane, int pend_cap,
+                                             const ForkCtx* fk = nullptr) {
   const RtxRenderParams& P = F.P;
   const double aterm = P.aterm_thresh;
   const int ncam = P.dof ? P.dof_div + 1 : 1;
-  auto push = [&](int& tp, const dvec3& p, const dvec3& d, const dvec3& w, const dvec3& k, int depth, int kind) {
-    double* b = pbuf + static_cast<size_t>(tp) * 13 * nlanes + LR.g;
+  auto put_entry = [&](double* b, const dvec3& p, const dvec3& d, const dvec3& w, const dvec3& k, int depth, int kind,
+                       int pos) {
     b[0 * nlanes] = p.x; b[1 * nlanes] = p.y; b[2 * nlanes] = p.z;
     b[3 * nlanes] = d.x; b[4 * nlanes] = d.y; b[5 * nlanes] = d.z;
     b[6 * nlanes] = w.x; b[7 * nlanes] = w.y; b[8 * nlanes] = w.z;
     b[9 * nlanes] = k.x; b[10 * nlanes] = k.y; b[11 * nlanes] = k.z;
-    b[12 * nlanes] = static_cast<double>(depth * 4 + kind);
+    b[12 * nlanes] = pend_code(pos, depth, kind);
+  };
+  auto push = [&](int& tp, const dvec3& p, const dvec3& d, const dvec3& w, const dvec3& k, int depth, int kind,
+                  int pos) {
+    put_entry(pbuf + static_cast<size_t>(tp) * 13 * nlanes + LR.g, p, d, w, k, depth, kind, pos);
     ++tp;
+  };
+  // child ray at heap position cpos: its sub-tree on a fork slot, if one is
+  // free (same result as the own stack: the sub-tree's sum joins the
+  // sample's in reduce_kernel); false leaves it to the own stack
+  auto fork_child = [&](const dvec3& p, const dvec3& d, const dvec3& w, const dvec3& k, int depth, int kind,
+                        int cpos) -> bool {
+    if (!FORK || cpos == 0 || fk->spare_n == 0) return false;
+    const unsigned int idx = atomicAdd(fk->fcnt, 1u);
+    if (idx >= fk->spare_n) return false;
+    const int T = fk->spare_base + static_cast<int>(idx);
+    LaneRef LT(LR.m, static_cast<size_t>(T));
+    put_entry(pbuf + static_cast<size_t>(T), p, d, w, k, depth, kind, cpos);
+    LT.top() = 1;
+    LT.acc() = mk3(0.0, 0.0, 0.0);
+    LT.nrays() = 0;
+    LT.camk() = 1;
+    LT.cam_end() = 1;
+    LT.pass() = 0;
+    LT.first_query() = 0;
+    LT.rec_on() = LR.rec_on();
+    LT.sample_slot() = LR.sample_slot();
+    LT.fpos() = cpos;
+    LT.dret() = DISC_NONE;
+    LT.st() = ST_POP;
+    atomicOr(&F.fmask[LR.sample_slot()], 1u << (cpos - 2));
+    fk->live_out[atomicAdd(fk->live_cnt, 1u)] = T;
+    return true;
   };
   // traceRay's reflection / refraction (RayTracer.cpp:127-164); m_out =
   // (trans_o, idx_o, kt_o): air, or discoverMat's material under -O o
@@ -597,18 +658,24 @@ __device__ __forceinline__ void advance_lane(LaneRef& LR, const DevScene& S, con
     const double eta = next_trans ? (leaving ? hit_index(S, R) : idx_o) / (leaving ? idx_o : hit_index(S, R)) : 0;
     const double radicand = 1 - eta * eta * (1 - c * c);
     const bool tir = next_trans && radicand < 0;
+    // heap positions of the children (0 past the fork depth)
+    const int ppos = LR.rpos();
+    const int pos_refl = ppos > 0 && 2 * ppos < F.fork_npos + 2 ? 2 * ppos : 0;
+    const int pos_refr = ppos > 0 && 2 * ppos + 1 < F.fork_npos + 2 ? 2 * ppos + 1 : 0;
     // push refraction first so that reflection is traced first
     if (next_trans && !tir && LR.top() < pend_cap) {
       const dvec3 tp = rtm::ray_at(LR.rp(), LR.rd(), LR.st_t() + RTX_RAY_EPS);
       const dvec3 td = eta * LR.rd() + (eta * c - sqrt(radicand)) * normal;
-      push(LR.top(), tp, td, LR.W(), leaving ? kt_o : hit_param(S, R, RTX_P_KT), depth, 2);
+      const dvec3 kf = leaving ? kt_o : hit_param(S, R, RTX_P_KT);
+      if (!fork_child(tp, td, LR.W(), kf, depth, 2, pos_refr)) push(LR.top(), tp, td, LR.W(), kf, depth, 2, pos_refr);
       if (STATS) C.secondary++;
     }
     if (((LR.m_flags() & RTX_MF_REFL) || tir) && LR.top() < pend_cap) {
       const dvec3 rdir = LR.rd() + 2 * c * normal;
       const dvec3 rs = rtm::ray_at(LR.rp(), LR.rd(), LR.st_t() - RTX_RAY_EPS);
-      push(LR.top(), rs, rdir, LR.W() * hit_param(S, R, RTX_P_KR), leaving ? hit_param(S, R, RTX_P_KT) : kt_o, depth,
-           1);
+      const dvec3 wr = LR.W() * hit_param(S, R, RTX_P_KR);
+      const dvec3 kf = leaving ? hit_param(S, R, RTX_P_KT) : kt_o;
+      if (!fork_child(rs, rdir, wr, kf, depth, 1, pos_refl)) push(LR.top(), rs, rdir, wr, kf, depth, 1, pos_refl);
       if (STATS) C.secondary++;
     }
   };
@@ -631,6 +698,29 @@ __device__ __forceinline__ void advance_lane(LaneRef& LR, const DevScene& S, con
       case ST_CAM: {
         // next camera ray of trace(x, y) (RayTracer.cpp:35-79)
         if (LR.camk() == LR.cam_end()) {
+          if (LR.fpos() != 0) {
+            // a forked sub-tree: its sum and its rays join the sample's
+            double* fo = F.fbuf + (static_cast<int64_t>(LR.sample_slot()) * F.fork_npos + (LR.fpos() - 2)) * 3;
+            fo[0] = LR.acc().x;
+            fo[1] = LR.acc().y;
+            fo[2] = LR.acc().z;
+            if (LR.rec_on()) atomicAdd(&hits[LR.sample_slot()].nrays, LR.nrays());
+            LR.fpos() = 0;
+            LR.st() = ST_IDLE;
+            break;
+          }
+          if (F.fork_on) {
+            // the root's sum; reduce_kernel adds the forked sub-trees' sums,
+            // then clamps (no DoF / anaglyph with forking); the record's ray
+            // count starts at -1 (0xff fill)
+            double* out = sbuf + static_cast<int64_t>(LR.sample_slot()) * 3;
+            out[0] = LR.acc().x;
+            out[1] = LR.acc().y;
+            out[2] = LR.acc().z;
+            if (LR.rec_on()) atomicAdd(&hits[LR.sample_slot()].nrays, LR.nrays() + 1);
+            LR.st() = ST_IDLE;
+            break;
+          }
           if (F.cam_split) {
             // one camera ray of a DoF sample (RayTracer.cpp:47-75): its own
             // sum; reduce_kernel adds the sample's rays in order, scales and
@@ -705,7 +795,7 @@ __device__ __forceinline__ void advance_lane(LaneRef& LR, const DevScene& S, con
         LR.camk()++;
         if (STATS) C.camera++;
         LR.top() = 0;
-        push(LR.top(), LR.rp(), LR.rd(), mk3(1, 1, 1), mk3(1, 1, 1), P.depth, 0);
+        push(LR.top(), LR.rp(), LR.rd(), mk3(1, 1, 1), mk3(1, 1, 1), P.depth, 0, F.fork_on ? 1 : 0);
         LR.st() = ST_POP;
         break;
       }
@@ -716,7 +806,9 @@ __device__ __forceinline__ void advance_lane(LaneRef& LR, const DevScene& S, con
         }
         --LR.top();
         const double* b = pbuf + static_cast<size_t>(LR.top()) * 13 * nlanes + LR.g;
-        const int dk = static_cast<int>(b[12 * nlanes]);
+        const int64_t code = static_cast<int64_t>(b[12 * nlanes]);
+        const int dk = static_cast<int>((code & ((int64_t(1) << 40) - 1)) - (int64_t(1) << 39));
+        LR.rpos() = static_cast<int>(code >> 40);
         LR.nrays()++;
         const int pdepth = dk >= 0 ? dk / 4 : -((-dk + 3) / 4);
         if (pdepth < 0) {  // `depth >= 0 &&` (RayTracer.cpp:116): no query, the miss colour
@@ -1275,11 +1367,21 @@ struct QList {
 #define CNT_Q (1 * CNT_LINE)
 #define CNT_CLAIM (3 * CNT_LINE)
 #define CNT_ALIVE_B (5 * CNT_LINE)
-#define CNT_PER_GROUP (6 * CNT_LINE)
+#define CNT_FORK (6 * CNT_LINE)  // fork slots taken this frame (not cleared per iteration)
+#define CNT_PER_GROUP (7 * CNT_LINE)
 
 __device__ __forceinline__ unsigned int lane_prefix(unsigned long long mask) {
   return __builtin_amdgcn_mbcnt_hi(static_cast<unsigned int>(mask >> 32),
                                    __builtin_amdgcn_mbcnt_lo(static_cast<unsigned int>(mask), 0u));
+}
+
+// A slot's next statically dealt work unit (sample slot + k * wf_nslot), or
+// -1: none left, or a fork slot
+__device__ __forceinline__ int64_t slot_unit(const FrameParams& F, int slot, int kdone) {
+  const int g = slot / F.wf_gs, l = slot - g * F.wf_gs;
+  if (l >= F.wf_gsamp) return -1;
+  const int64_t unit = static_cast<int64_t>(g) * F.wf_gsamp + l + static_cast<int64_t>(kdone) * F.wf_nslot;
+  return unit < F.n_samples ? unit : -1;
 }
 
 // Claim the next statically dealt sample for an idle slot (what the
@@ -1287,8 +1389,8 @@ __device__ __forceinline__ unsigned int lane_prefix(unsigned long long mask) {
 __device__ __forceinline__ void claim_sample(LaneRef& L, const FrameParams& F, RtxHitRecord* hits, int slot) {
   const RtxRenderParams& P = F.P;
   while (L.st() == ST_IDLE) {
-    const int64_t unit = static_cast<int64_t>(slot) + static_cast<int64_t>(L.kdone()) * F.wf_nslot;
-    if (unit >= F.n_samples) return;
+    const int64_t unit = slot_unit(F, slot, L.kdone());
+    if (unit < 0) return;
     L.kdone()++;
     // work unit -> sample (and, with cam_split, which of its camera rays)
     const int64_t sid = F.cam_split ? unit / F.ncam : unit;
@@ -1316,11 +1418,12 @@ __device__ __forceinline__ void claim_sample(LaneRef& L, const FrameParams& F, R
     L.cam_end() = F.cam_split ? cam0 + 1 : F.ncam;
     L.nrays() = 0;
     L.acc() = mk3(0, 0, 0);
+    L.fpos() = 0;
     L.st() = ST_CAM;
   }
 }
 
-template <bool STATS, bool MEDIA>
+template <bool STATS, bool MEDIA, bool FORK>
 __global__ void __launch_bounds__(WG, RTX_ADV_WAVES) advance_kernel(DevScene S, const DevScene* __restrict__ Sg, const FrameParams* __restrict__ Fp, LaneMem lm,
                                                       double* __restrict__ sbuf, RtxHitRecord* __restrict__ hits,
                                                       double* __restrict__ pbuf, int pend_cap, QList q0, QList q1,
@@ -1338,15 +1441,18 @@ __global__ void __launch_bounds__(WG, RTX_ADV_WAVES) advance_kernel(DevScene S, 
   Counters C = {0, 0, 0, 0, 0, 0, 0};
   LaneRef L(lm, static_cast<size_t>(slot));
   int qm = Q_NONE;
-  if (valid && (L.st() != ST_IDLE ||
-                static_cast<int64_t>(slot) + static_cast<int64_t>(L.kdone()) * F.wf_nslot < F.n_samples)) {
+  // fork slots: the group's slots past its sample slots (none in the
+  // first iteration, which only starts camera rays)
+  const ForkCtx fk = {counters + CNT_FORK, slot_off + F.wf_gsamp,
+                      first ? 0u : static_cast<unsigned int>(F.wf_gs - F.wf_gsamp), live_out, counters + out_cnt};
+  if (valid && (L.st() != ST_IDLE || slot_unit(F, slot, L.kdone()) >= 0)) {
     // the previous iteration's query result is already in L.bt()/bobj/bsub/bhave
     L.qmode() = Q_NONE;
     for (;;) {
       claim_sample(L, F, hits, slot);
       if (L.st() == ST_IDLE) break;
-      advance_lane<STATS, false, MEDIA>(L, *Sg, F, C, sbuf, nullptr, hits, 0, 0, pbuf, lm.n, static_cast<size_t>(slot),
-                                 pend_cap);
+      advance_lane<STATS, false, MEDIA, FORK>(L, *Sg, F, C, sbuf, nullptr, hits, 0, 0, pbuf, lm.n,
+                                              static_cast<size_t>(slot), pend_cap, &fk);
       if (L.qmode() != Q_NONE) break;
     }
     qm = L.qmode();
@@ -1732,6 +1838,22 @@ __global__ void __launch_bounds__(WG) reduce_kernel(const FrameParams* __restric
       ret *= (1.0 / (F.P.dof_div + 1.0));
       acc += rtm::gclamp3(ret, 0.0, 1.0);
     }
+  } else if (F.fork_on) {
+    // forked ray trees: the root's sum plus the forked sub-trees' sums in
+    // heap order, then trace()'s clamp (RayTracer.cpp:77)
+    const double* s = sbuf + o * F.spp * 3;
+    for (int q = 0; q < F.spp; ++q) {
+      dvec3 ret = mk3(s[q * 3 + 0], s[q * 3 + 1], s[q * 3 + 2]);
+      const int64_t sid = o * F.spp + q;
+      unsigned int m = F.fmask[sid];
+      while (m) {
+        const int b = __builtin_ctz(m);
+        m &= m - 1;
+        const double* f = F.fbuf + (sid * F.fork_npos + b) * 3;
+        ret += mk3(f[0], f[1], f[2]);
+      }
+      acc += rtm::gclamp3(ret, 0.0, 1.0);
+    }
   } else {
     const double* s = sbuf + o * F.spp * 3;
     for (int q = 0; q < F.spp; ++q) acc += mk3(s[q * 3 + 0], s[q * 3 + 1], s[q * 3 + 2]);
@@ -1782,6 +1904,10 @@ struct SceneState {
   size_t sbuf_bytes = 0;
   double* d_pbuf = nullptr;     // per-lane pending-ray stacks (HBM)
   size_t pbuf_bytes = 0;
+  double* d_fbuf = nullptr;     // forked sub-tree sums
+  size_t fbuf_bytes = 0;
+  unsigned int* d_fmask = nullptr;  // forked positions per sample
+  size_t fmask_bytes = 0;
   // wavefront path: slot state, query lists, counters
   void* d_wf = nullptr;
   size_t wf_bytes = 0;
@@ -1873,6 +1999,14 @@ void dispatch2(bool a, bool b, Fn&& f) {
     if (b) f(std::false_type{}, std::true_type{});
     else f(std::false_type{}, std::false_type{});
   }
+}
+
+template <class Fn>
+void dispatch3(bool a, bool b, bool c, Fn&& f) {
+  dispatch2(a, b, [&](auto x, auto y) {
+    if (c) f(x, y, std::true_type{});
+    else f(x, y, std::false_type{});
+  });
 }
 
 extern "C" {
@@ -2011,6 +2145,8 @@ rtx_status rtx_scene_destroy(void* scene) {
   if (st->d_picks) (void)hipFree(st->d_picks);
   if (st->d_sbuf) (void)hipFree(st->d_sbuf);
   if (st->d_pbuf) (void)hipFree(st->d_pbuf);
+  if (st->d_fbuf) (void)hipFree(st->d_fbuf);
+  if (st->d_fmask) (void)hipFree(st->d_fmask);
   if (st->d_wf) (void)hipFree(st->d_wf);
   if (st->d_lane) (void)hipFree(st->d_lane);
   for (auto e : st->wf_join) (void)hipEventDestroy(e);
@@ -2299,11 +2435,45 @@ rtx_status rtx_render(void* scene, const RtxRenderParams* params, uint8_t* rgb8,
     const char* g_env = getenv("RTX_GROUPS");
     if (g_env && atoi(g_env) > 0) G = atoi(g_env);
     if (G > 16) G = 16;
-    if (nslot64 > F.n_samples) nslot64 = F.n_samples;
-    const int64_t per = (nslot64 + G * WG - 1) / (G * WG);  // workgroups per group
+    // ray-tree forking when the frame has fewer samples than 3/4 of the
+    // slots (a shard of a multi-GPU frame): the spare slots run forked
+    // reflection / refraction sub-trees, so a sample's critical path is its
+    // deepest sub-tree instead of its whole tree (RTX_FORK=0: off;
+    // RTX_FORK_DEPTH: heap depth of the deepest forked ray, 1..4)
+    const char* fork_env = getenv("RTX_FORK");
+    int fork_depth = 3;
+    const char* fd_env = getenv("RTX_FORK_DEPTH");
+    if (fd_env && atoi(fd_env) > 0) fork_depth = std::min(4, atoi(fd_env));
+    const bool fork = !(fork_env && atoi(fork_env) == 0) && !F.cam_split && !params->dof && !params->anaglyph &&
+                      F.n_samples * 4 <= nslot64 * 3;
+    int64_t gsamp = (F.n_samples + G - 1) / G;  // sample slots per group
+    if (gsamp > (nslot64 + G - 1) / G) gsamp = (nslot64 + G - 1) / G;
+    int64_t gspare = 0;
+    if (fork) gspare = std::min<int64_t>(gsamp / 2 + WG, nslot64 / G - gsamp);
+    const int64_t per = (gsamp + gspare + WG - 1) / WG;  // workgroups per group
     const int64_t gslots = per * WG;
+    if (!fork) gsamp = gslots;
     nslot64 = gslots * G;
-    F.wf_nslot = static_cast<int>(nslot64);
+    F.wf_nslot = static_cast<int>(gsamp * G);
+    F.wf_gs = static_cast<int>(gslots);
+    F.wf_gsamp = static_cast<int>(gsamp);
+    F.fork_on = fork ? 1 : 0;
+    F.fork_npos = fork ? (1 << (fork_depth + 1)) - 2 : 0;
+    F.fbuf = nullptr;
+    F.fmask = nullptr;
+    if (fork) {
+      const size_t nsamp_out = size_t(npix) * F.spp;
+      if ((rc = ensure(reinterpret_cast<void**>(&st->d_fbuf), &st->fbuf_bytes,
+                       nsamp_out * F.fork_npos * 3 * sizeof(double))) != RTX_OK)
+        return rc;
+      if ((rc = ensure(reinterpret_cast<void**>(&st->d_fmask), &st->fmask_bytes, nsamp_out * sizeof(unsigned int))) !=
+          RTX_OK)
+        return rc;
+      F.fbuf = st->d_fbuf;
+      F.fmask = st->d_fmask;
+      HIP_TRY(hipMemsetAsync(st->d_fmask, 0, nsamp_out * sizeof(unsigned int), stream));
+      if (hits) HIP_TRY(hipMemsetAsync(d_hits, 0xff, nsamp_out * sizeof(RtxHitRecord), stream));
+    }
     const size_t ns = static_cast<size_t>(nslot64);
     const size_t gs = static_cast<size_t>(gslots);
     const size_t bytes_q = gs * (sizeof(int) + QL_D * sizeof(double) + 2 * sizeof(int)) + 1024;
@@ -2354,6 +2524,9 @@ rtx_status rtx_render(void* scene, const RtxRenderParams* params, uint8_t* rgb8,
     // upper bound of each group's live slots (counts only fall; read back by
     // the pipelined checks): sizes the tail iterations' grids
     std::vector<int64_t> live_bound(size_t(G), gslots);
+    // upper bound of the live slots an iteration can see (live_bound plus
+    // the forks that can still start): sizes the grids
+    std::vector<int64_t> grid_bound(size_t(G), gslots);
     // tail switch: a group whose live slots fall to this many finishes in
     // tail_kernel (RTX_TAIL; headline frame 92.6 / 91.0 / 99.5 ms and an
     // 8-way shard 32.3 / 25.0 / 24.9 ms at 65k / 200k / 400k)
@@ -2407,7 +2580,7 @@ rtx_status rtx_render(void* scene, const RtxRenderParams* params, uint8_t* rgb8,
           const bool odd = (it & 1) != 0;  // this iteration would read the list the last one wrote
           const int in_cnt = odd ? CNT_ALIVE_A : CNT_ALIVE_B;
           const int* live_in = live[size_t(g) * 2 + (odd ? 0 : 1)];
-          const int64_t lb = live_bound[size_t(g)];
+          const int64_t lb = grid_bound[size_t(g)];
           const int64_t grid = std::max<int64_t>(1, (lb + WG - 1) / WG);
           dispatch2(stats, media, [&](auto st_, auto md_) {
             hipLaunchKernelGGL((tail_kernel<decltype(st_)::value, decltype(md_)::value>), dim3(grid), dim3(WG), lds, sg,
@@ -2427,11 +2600,12 @@ rtx_status rtx_render(void* scene, const RtxRenderParams* params, uint8_t* rgb8,
         const int* live_in = live[size_t(g) * 2 + (odd ? 0 : 1)];
         HIP_TRY(hipMemsetAsync(cnt + (odd ? CNT_LINE : 0), 0, 5 * CNT_LINE * sizeof(unsigned int), sg));
         const int first = it == 0 ? 1 : 0;
-        const int64_t lb = live_bound[size_t(g)];
+        const int64_t lb = grid_bound[size_t(g)];
         const int64_t agrid = first ? per : std::max<int64_t>(1, std::min<int64_t>(per, (lb + WG - 1) / WG));
         const int64_t tg = std::max<int64_t>(1, std::min<int64_t>(tgrid, (lb + WG - 1) / WG));
-        dispatch2(stats, media, [&](auto st_, auto md_) {
-          hipLaunchKernelGGL((advance_kernel<decltype(st_)::value, decltype(md_)::value>), dim3(agrid), dim3(WG), 0, sg,
+        dispatch3(stats, media, fork, [&](auto st_, auto md_, auto fk_) {
+          hipLaunchKernelGGL((advance_kernel<decltype(st_)::value, decltype(md_)::value, decltype(fk_)::value>),
+                             dim3(agrid), dim3(WG), 0, sg,
                              S, st->d_scene, st->d_frame, A, sb, d_hits, st->d_pbuf, pend_cap, q0, q1, cnt,
                              st->d_stats, static_cast<int>(g * gslots), live_in, live_out, first, in_cnt, out_cnt);
         });
@@ -2456,6 +2630,10 @@ rtx_status rtx_render(void* scene, const RtxRenderParams* params, uint8_t* rgb8,
             const unsigned int* hc = st->h_counters + CNT_PER_GROUP * g;
             const unsigned int alive = hc[(pending_check[size_t(g)] & 1) ? CNT_ALIVE_B : CNT_ALIVE_A];
             live_bound[size_t(g)] = alive;
+            // forks add live slots: bound by the fork slots still free
+            const int64_t forks_left =
+                fork ? std::max<int64_t>(0, (gslots - gsamp) - static_cast<int64_t>(hc[CNT_FORK])) : 0;
+            grid_bound[size_t(g)] = std::min<int64_t>(gslots, alive + forks_left);
             if (dbg)
               fprintf(stderr, "rtx group %d iter %d: alive %u (closest %u next %u)\n", g, pending_check[size_t(g)],
                       alive, hc[CNT_Q], hc[CNT_Q + CNT_LINE]);

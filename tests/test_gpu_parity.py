@@ -40,16 +40,21 @@ def _compare(gpu, ref, spp):
 # render paths (DESIGN.md "Kernels"): the wavefront advance/trace pipeline
 # (default, 3 slot groups on 3 streams), the persistent megakernel, one slot
 # group, a tiny slot pool so every slot walks many samples (claim_sample's
-# static deal), and the tail kernel finishing almost everything
+# static deal), and the tail kernel finishing almost everything.  The small
+# parity frames have fewer samples than slots, so "wavefront" forks ray
+# sub-trees onto spare slots (heap depth 3); "wavefront_nofork" does not,
+# "wavefront_fork4" forks down to depth 4
 PATHS = {"wavefront": {}, "mega": {"RTX_MEGAKERNEL": "1"}, "wavefront_1g": {"RTX_GROUPS": "1"},
          "wavefront_256": {"RTX_SLOTS": "256"},
+         "wavefront_nofork": {"RTX_FORK": "0"}, "wavefront_fork4": {"RTX_FORK_DEPTH": "4"},
          # tail_kernel takes over right after the first batched iteration
          "wavefront_tail": {"RTX_TAIL": "1000000000"}}
 
 
 @pytest.fixture(params=list(PATHS), ids=list(PATHS))
 def render_path(request):
-    saved = {k: os.environ.get(k) for k in ("RTX_MEGAKERNEL", "RTX_SLOTS", "RTX_GROUPS", "RTX_TAIL")}
+    saved = {k: os.environ.get(k) for k in ("RTX_MEGAKERNEL", "RTX_SLOTS", "RTX_GROUPS", "RTX_TAIL", "RTX_FORK",
+                                     "RTX_FORK_DEPTH")}
     for k in saved:
         os.environ.pop(k, None)
     os.environ.update(PATHS[request.param])
