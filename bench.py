@@ -4,7 +4,8 @@ trimesh2.ray (stand-in, tools/gen_scenes.py) at 1920x1080, depth 5, 4x4
 regular AA (`ray -w 1920 -r 5 -O r -A 4`).
 
 One step = one frame.  On N GPUs (one process per GPU, torch.distributed over
-RCCL) the frame is cut into 32x32 tiles dealt round-robin (tile % N == rank),
+RCCL) the frame is cut into 32x32 tiles dealt round-robin along rotated rows
+(diagonal stripes, deal index % N == rank),
 each rank renders its tiles into a packed HBM buffer and rank 0 gathers them
 over xGMI (dist.gather) — total work is fixed, so scaling is strong.
 

@@ -378,10 +378,17 @@ def shard_pixels(opts: RenderOptions, height: int, tile: int, shard: int, nshard
 
 
 def owned_tiles(width: int, height: int, tile: int, shard: int, nshards: int):
-    """Tile ids (row-major from the bottom-left) a shard renders (tile % n == shard)."""
+    """Tile ids (row-major from the bottom-left) a shard renders, in its packed
+    order: deal indices d = shard, shard + n, ... where deal index d is tile
+    row d // tx, column (d % tx + row) % tx (rows rotated by their index:
+    diagonal stripes, deal_tile in rtx_render.hip)."""
     tx = (width + tile - 1) // tile
     ty = (height + tile - 1) // tile
-    return [t for t in range(tx * ty) if t % nshards == shard]
+    out = []
+    for d in range(shard, tx * ty, nshards):
+        row = d // tx
+        out.append(row * tx + (d % tx + row) % tx)
+    return out
 
 
 def unpack_tiles(packed: np.ndarray, width: int, height: int, tile: int, shard: int, nshards: int,

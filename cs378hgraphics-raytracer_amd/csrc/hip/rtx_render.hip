@@ -78,7 +78,7 @@ struct FrameParams {
   // wavefront slot layout: G groups of wf_gs slots; the first wf_gsamp slots
   // of a group take samples (sample slot g * wf_gsamp + l, samples dealt
   // sample slot + k * wf_nslot), the rest are fork slots
-  int wf_gs, wf_gsamp;
+  int wf_gs, wf_gsamp, wf_groups;
   // ray-tree forking (wavefront path, frames with fewer samples than slots):
   // a reflection / refraction ray at heap position 2 .. fork_npos + 1 of its
   // sample's ray tree (root 1, children 2p and 2p + 1) may run its sub-tree
@@ -89,14 +89,30 @@ struct FrameParams {
   unsigned int* fmask;
 };
 
+// Tile deal: deal index d = shard + k * nshards is tile row d / tiles_x,
+// column (d % tiles_x + row) % tiles_x — row-major with each row rotated by
+// its index, so shards own diagonal stripes of tiles rather than columns
+// when nshards divides tiles_x (render cost is correlated along columns:
+// 2-way shards of the headline frame 49.5 / 42.0 ms with column stripes).
+#ifndef RTX_DEAL_SKEW
+#define RTX_DEAL_SKEW 1
+#endif
+__host__ __device__ __forceinline__ void deal_tile(int d, int tiles_x, int& tx, int& ty) {
+  ty = d / tiles_x;
+  tx = (d % tiles_x + RTX_DEAL_SKEW * ty) % tiles_x;
+}
+__host__ __device__ __forceinline__ int tile_deal(int tx, int ty, int tiles_x) {
+  return ty * tiles_x + ((tx - RTX_DEAL_SKEW * ty) % tiles_x + tiles_x) % tiles_x;
+}
+
 // Work item -> pixel; out_index is the output slot (packed tile order or
 // (i + j*w) reference order).
 __device__ __forceinline__ bool item_pixel(const FrameParams& F, int64_t item, int pix_in_item, int& i, int& j,
                                            int64_t& out_index) {
   const int k = static_cast<int>(item / F.items_per_tile);
   const int b = static_cast<int>(item % F.items_per_tile);
-  const int tile_id = F.P.tile > 0 ? F.P.shard + k * F.P.nshards : 0;
-  const int tx = tile_id % F.tiles_x, ty = tile_id / F.tiles_x;
+  int tx, ty;
+  deal_tile(F.P.tile > 0 ? F.P.shard + k * F.P.nshards : 0, F.tiles_x, tx, ty);
   const int bx = b % F.bx_per_tile, by = b / F.bx_per_tile;
   const int lx = bx * F.bw + pix_in_item % F.bw;
   const int ly = by * F.bh + pix_in_item / F.bw;
@@ -1375,12 +1391,16 @@ __device__ __forceinline__ unsigned int lane_prefix(unsigned long long mask) {
                                    __builtin_amdgcn_mbcnt_lo(static_cast<unsigned int>(mask), 0u));
 }
 
-// A slot's next statically dealt work unit (sample slot + k * wf_nslot), or
-// -1: none left, or a fork slot
+// A slot's next statically dealt work unit, or -1: none left, or a fork
+// slot.  Runs of 64 consecutive units (one wave's worth of neighbouring
+// samples) are dealt to the groups round-robin, so every group gets a share
+// of every image region: contiguous thirds left the bottom third's group
+// idle after 3 iterations while the other two carried the costly rows.
 __device__ __forceinline__ int64_t slot_unit(const FrameParams& F, int slot, int kdone) {
   const int g = slot / F.wf_gs, l = slot - g * F.wf_gs;
   if (l >= F.wf_gsamp) return -1;
-  const int64_t unit = static_cast<int64_t>(g) * F.wf_gsamp + l + static_cast<int64_t>(kdone) * F.wf_nslot;
+  const int64_t unit = ((static_cast<int64_t>(l >> 6) * F.wf_groups + g) << 6) + (l & 63) +
+                       static_cast<int64_t>(kdone) * F.wf_nslot;
   return unit < F.n_samples ? unit : -1;
 }
 
@@ -1815,14 +1835,14 @@ __global__ void __launch_bounds__(WG) reduce_kernel(const FrameParams* __restric
   if (F.P.packed && F.P.tile > 0) {
     const int64_t k = o / (int64_t(F.tw) * F.th);
     const int r = static_cast<int>(o % (int64_t(F.tw) * F.th));
-    const int tile_id = F.P.shard + static_cast<int>(k) * F.P.nshards;
-    const int i = (tile_id % F.tiles_x) * F.tw + r % F.tw;
-    const int j = (tile_id / F.tiles_x) * F.th + r / F.tw;
+    int tx, ty;
+    deal_tile(F.P.shard + static_cast<int>(k) * F.P.nshards, F.tiles_x, tx, ty);
+    const int i = tx * F.tw + r % F.tw;
+    const int j = ty * F.th + r / F.tw;
     if (i >= F.P.width || j >= F.P.height) return;
   } else if (F.P.tile > 0) {  // full frame, sharded: only this shard's tiles
     const int i = static_cast<int>(o % F.P.width), j = static_cast<int>(o / F.P.width);
-    const int tile_id = (j / F.th) * F.tiles_x + (i / F.tw);
-    if (tile_id % F.P.nshards != F.P.shard) return;
+    if (tile_deal(i / F.tw, j / F.th, F.tiles_x) % F.P.nshards != F.P.shard) return;
   }
   dvec3 acc = mk3(0.0, 0.0, 0.0);
   if (F.cam_split) {
@@ -2444,10 +2464,21 @@ rtx_status rtx_render(void* scene, const RtxRenderParams* params, uint8_t* rgb8,
     int fork_depth = 3;
     const char* fd_env = getenv("RTX_FORK_DEPTH");
     if (fd_env && atoi(fd_env) > 0) fork_depth = std::min(4, atoi(fd_env));
-    const bool fork = !(fork_env && atoi(fork_env) == 0) && !F.cam_split && !params->dof && !params->anaglyph &&
-                      F.n_samples * 4 <= nslot64 * 3;
+    const bool fork_ok = !(fork_env && atoi(fork_env) == 0) && !F.cam_split && !params->dof && !params->anaglyph;
+    if (fork_ok && !(ns_env && atoll(ns_env) > 0)) {
+      // one slot per sample plus half as many fork slots, within a memory
+      // budget for the slot state + pending-ray stacks (headline frame:
+      // 50 M slots, 89 -> 84 ms; 2-way shard 58 -> 50 ms)
+      const size_t per_slot = lane_mem_bytes(1) + size_t(pend_cap) * 13 * sizeof(double) +
+                              2 * (3 * sizeof(int) + QL_D * sizeof(double)) + 2 * sizeof(int);
+      const int64_t cap = static_cast<int64_t>((size_t(96) << 30) / per_slot);
+      const int64_t want = std::min<int64_t>(cap, F.n_samples + F.n_samples / 2 + int64_t(G) * 2 * WG);
+      if (want > nslot64) nslot64 = want;
+    }
+    const bool fork = fork_ok && F.n_samples * 4 <= nslot64 * 3;
     int64_t gsamp = (F.n_samples + G - 1) / G;  // sample slots per group
     if (gsamp > (nslot64 + G - 1) / G) gsamp = (nslot64 + G - 1) / G;
+    gsamp = (gsamp + 63) / 64 * 64;  // whole 64-unit runs (slot_unit)
     int64_t gspare = 0;
     if (fork) gspare = std::min<int64_t>(gsamp / 2 + WG, nslot64 / G - gsamp);
     const int64_t per = (gsamp + gspare + WG - 1) / WG;  // workgroups per group
@@ -2457,6 +2488,7 @@ rtx_status rtx_render(void* scene, const RtxRenderParams* params, uint8_t* rgb8,
     F.wf_nslot = static_cast<int>(gsamp * G);
     F.wf_gs = static_cast<int>(gslots);
     F.wf_gsamp = static_cast<int>(gsamp);
+    F.wf_groups = G;
     F.fork_on = fork ? 1 : 0;
     F.fork_npos = fork ? (1 << (fork_depth + 1)) - 2 : 0;
     F.fbuf = nullptr;

@@ -193,8 +193,10 @@ typedef struct RtxRenderParams {
   double dof_fd;                /* -A for d                                    */
   double dof_apsz;              /* -C for d                                    */
   /* Tile sharding: the image is cut into tile x tile squares, numbered
-   * row-major from the bottom-left; this call renders tiles
-   * t with t % nshards == shard.  tile == 0 renders the whole image. */
+   * row-major from the bottom-left, and dealt to shards diagonally: deal
+   * index d is tile row d / tiles_x, column (d % tiles_x + row) % tiles_x,
+   * and this call renders deal indices d with d % nshards == shard (packed
+   * in increasing d).  tile == 0 renders the whole image. */
   int32_t tile;
   int32_t shard, nshards;
   int32_t packed;               /* 1: outputs packed per owned tile (tile*tile

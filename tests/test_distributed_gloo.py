@@ -71,3 +71,16 @@ def test_tiles_partition_the_frame():
         for r in range(n):
             seen += pkg.owned_tiles(1920, 1080, 32, r, n)
         assert sorted(seen) == list(range(60 * 34))
+
+
+def test_tile_deal_is_diagonal():
+    # rows are rotated by their index, so when N divides the 60 tile columns
+    # a shard still owns tiles in every column (not column stripes)
+    pkg = load_package()
+    for n in (2, 4):
+        for r in range(n):
+            cols = {t % 60 for t in pkg.owned_tiles(1920, 1080, 32, r, n)}
+            assert cols == set(range(60))
+    # deal index d = shard + k * n -> tile (row d // 60, column (d % 60 + row) % 60)
+    assert pkg.owned_tiles(1920, 1080, 32, 1, 2)[:3] == [1, 3, 5]
+    assert pkg.owned_tiles(1920, 1080, 32, 0, 2)[30:32] == [61, 63]

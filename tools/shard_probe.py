@@ -37,8 +37,6 @@ def main():
                 dev.render_device(opts, out.data_ptr(), 0, stream, tile=tile, shard=r, nshards=n, packed=n > 1)
             torch.cuda.synchronize()
             times.append((time.perf_counter() - t0) / 3 * 1e3)
-            if n == 8 and r >= 1:  # shards of 8 are alike; two are enough
-                break
         full = 1e3 if n == 1 else None
         print(json.dumps({"n": n, "shard_ms": [round(t, 2) for t in times], "max_ms": round(max(times), 2)}),
               flush=True)
