@@ -124,6 +124,12 @@ def host_lib():
         lib.rtx_write_image.argtypes = [C.c_char_p, C.c_int32, C.c_int32, C.c_void_p]
         lib.rtx_image_height.argtypes = [C.c_int32, C.c_double]
         lib.rtx_image_height.restype = C.c_int32
+        lib.rtx_read_image.argtypes = [C.c_char_p, C.POINTER(C.c_int32), C.POINTER(C.c_int32),
+                                       C.POINTER(C.c_int32), C.c_void_p, C.c_int64]
+        lib.rtx_shard_tiles.argtypes = [C.c_int32, C.c_int32, C.c_int32, C.c_int32, C.c_int32, C.c_void_p,
+                                        C.c_int32, C.POINTER(C.c_int32)]
+        lib.rtx_unpack_tiles.argtypes = [C.c_void_p, C.c_int32, C.c_int32, C.c_int32, C.c_int32, C.c_int32,
+                                         C.c_int32, C.c_void_p]
         _host = lib
     return _host
 
@@ -154,7 +160,13 @@ def hip_lib():
 HIP_SYMBOLS = ["rtx_last_error", "rtx_device_count", "rtx_scene_create", "rtx_scene_destroy", "rtx_render",
                "rtx_shard_pixels", "rtx_kernel_time"]
 HOST_SYMBOLS = ["rtx_host_last_error", "rtx_host_load", "rtx_host_desc", "rtx_host_info", "rtx_host_free",
-                "rtx_host_cubemap", "rtx_write_image", "rtx_image_height"]
+                "rtx_host_cubemap", "rtx_write_image", "rtx_image_height", "rtx_read_image", "rtx_shard_tiles",
+                "rtx_unpack_tiles"]
+
+
+def _check_host(rc, what):
+    if rc != 0:
+        raise RtxError(f"{what}: {host_lib().rtx_host_last_error().decode(errors='replace')} (status {rc})")
 
 
 def _check(rc, lib, what):
@@ -379,29 +391,38 @@ def shard_pixels(opts: RenderOptions, height: int, tile: int, shard: int, nshard
 
 def owned_tiles(width: int, height: int, tile: int, shard: int, nshards: int):
     """Tile ids (row-major from the bottom-left) a shard renders, in its packed
-    order: deal indices d = shard, shard + n, ... where deal index d is tile
-    row d // tx, column (d % tx + row) % tx (rows rotated by their index:
-    diagonal stripes, deal_tile in rtx_render.hip)."""
-    tx = (width + tile - 1) // tile
-    ty = (height + tile - 1) // tile
-    out = []
-    for d in range(shard, tx * ty, nshards):
-        row = d // tx
-        out.append(row * tx + (d % tx + row) % tx)
-    return out
+    order (rtx_shard_tiles: the deal of rtx_render.hip's deal_tile — deal
+    index d = shard + k * nshards is tile row d // tx, column
+    (d % tx + row) % tx, i.e. diagonal stripes)."""
+    lib = host_lib()
+    n = C.c_int32()
+    _check_host(lib.rtx_shard_tiles(width, height, tile, shard, nshards, None, 0, C.byref(n)), "rtx_shard_tiles")
+    ids = np.zeros(n.value, np.int32)
+    _check_host(lib.rtx_shard_tiles(width, height, tile, shard, nshards, ids.ctypes.data, n.value, C.byref(n)),
+                "rtx_shard_tiles")
+    return [int(t) for t in ids]
 
 
 def unpack_tiles(packed: np.ndarray, width: int, height: int, tile: int, shard: int, nshards: int,
                  out: np.ndarray, channels: int = 3):
-    """Scatter a shard's packed tiles into a full (height, width, c) frame."""
-    tx = (width + tile - 1) // tile
-    tiles = owned_tiles(width, height, tile, shard, nshards)
-    blk = packed.reshape(len(tiles), tile, tile, channels)
-    for k, t in enumerate(tiles):
-        x0, y0 = (t % tx) * tile, (t // tx) * tile
-        w = min(tile, width - x0)
-        h = min(tile, height - y0)
-        out[y0:y0 + h, x0:x0 + w] = blk[k, :h, :w]
+    """Scatter a shard's packed tiles into a full (height, width, c) frame
+    (rtx_unpack_tiles, the reassembly the multi-GPU driver runs)."""
+    src = np.ascontiguousarray(packed)
+    assert out.flags["C_CONTIGUOUS"] and out.dtype == src.dtype and out.shape[:2] == (height, width)
+    elem = src.dtype.itemsize * channels
+    _check_host(host_lib().rtx_unpack_tiles(src.ctypes.data, width, height, tile, shard, nshards, elem,
+                                            out.ctypes.data), "rtx_unpack_tiles")
+    return out
+
+
+def read_image(path: str):
+    """readImage (fileio/images.cc:47-53): (h, w, channels) uint8, row 0 = bottom."""
+    lib = host_lib()
+    w, h, ch = C.c_int32(), C.c_int32(), C.c_int32()
+    _check_host(lib.rtx_read_image(path.encode(), C.byref(w), C.byref(h), C.byref(ch), None, 0), "rtx_read_image")
+    out = np.zeros((h.value, w.value, ch.value), np.uint8)
+    _check_host(lib.rtx_read_image(path.encode(), C.byref(w), C.byref(h), C.byref(ch), out.ctypes.data, out.size),
+                "rtx_read_image")
     return out
 
 

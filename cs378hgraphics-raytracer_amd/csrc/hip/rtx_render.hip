@@ -39,9 +39,10 @@ using rtm::mk3;
 
 #define WG 256
 #define WAVES_PER_WG (WG / 64)
-#define MAX_DEPTH 16               // -r limit of this build
-#define MAX_PENDING (MAX_DEPTH + 2)
-#define MAX_DOF 64
+// -r limit: the pending-ray stack holds depth + 2 entries per slot in HBM
+// and the slot pool shrinks to fit device memory, so this only bounds the
+// stack's size (the reference's recursion is bounded by its C stack)
+#define MAX_DEPTH 4096
 #define QCHUNK 256                 // samples per queue atomic
 // occupancy targets (waves per SIMD) of the wavefront kernels, measured on
 // the headline frame: traversal at 3 waves (<= 168 VGPRs, no spills) beats 4
@@ -59,7 +60,7 @@ using rtm::mk3;
 struct FrameParams {
   RtxRenderParams P;
   RtxCamera cam;
-  double offv[MAX_DOF * 3];  // DoF eye offsets (RayTracer.cpp:64-69), host cos/sin
+  const double* offv;        // DoF eye offsets [divs][3] in HBM (RayTracer.cpp:64-69), host cos/sin
   int spp;                   // samples per pixel (1 or s^2)
   int s;                     // s (AA grid)
   int ppw;                   // pixels per work item
@@ -79,11 +80,16 @@ struct FrameParams {
   // of a group take samples (sample slot g * wf_gsamp + l, samples dealt
   // sample slot + k * wf_nslot), the rest are fork slots
   int wf_gs, wf_gsamp, wf_groups;
-  // ray-tree forking (wavefront path, frames with fewer samples than slots):
-  // a reflection / refraction ray at heap position 2 .. fork_npos + 1 of its
-  // sample's ray tree (root 1, children 2p and 2p + 1) may run its sub-tree
-  // on a fork slot; the sub-tree's colour sum goes to fbuf[sample][pos - 2]
-  // and its bit to fmask[sample], reduce_kernel adds them before the clamp
+  // ray-tree buckets (wavefront path, no DoF / anaglyph; DESIGN.md "Ray-tree
+  // forking"): the rays at heap positions 2 .. fork_npos + 1 of a sample's
+  // ray tree (root 1, children 2p and 2p + 1, down to heap depth
+  // fork_depth) are nodes; every other ray belongs to its nearest node
+  // ancestor.  A ray's colour goes to its node's bucket — the root's to the
+  // lane's acc, node p's to fbuf[sample][p - 2] (first write sets bit p - 2
+  // of fmask[sample]) — and reduce_kernel adds the buckets in heap order
+  // before the clamp.  A bucket's sum is the same whether its node ran on
+  // the sample's own slot or was forked onto a spare slot, so the image does
+  // not depend on which nodes won a fork slot.
   int fork_on, fork_npos;
   double* fbuf;
   unsigned int* fmask;
@@ -94,15 +100,14 @@ struct FrameParams {
 // its index, so shards own diagonal stripes of tiles rather than columns
 // when nshards divides tiles_x (render cost is correlated along columns:
 // 2-way shards of the headline frame 49.5 / 42.0 ms with column stripes).
-#ifndef RTX_DEAL_SKEW
-#define RTX_DEAL_SKEW 1
-#endif
+// The same deal is restated by the host (rtx_shard_tiles, librtx_host) and
+// by the Python mirror (owned_tiles); a test checks all three agree.
 __host__ __device__ __forceinline__ void deal_tile(int d, int tiles_x, int& tx, int& ty) {
   ty = d / tiles_x;
-  tx = (d % tiles_x + RTX_DEAL_SKEW * ty) % tiles_x;
+  tx = (d % tiles_x + ty) % tiles_x;
 }
 __host__ __device__ __forceinline__ int tile_deal(int tx, int ty, int tiles_x) {
-  return ty * tiles_x + ((tx - RTX_DEAL_SKEW * ty) % tiles_x + tiles_x) % tiles_x;
+  return ty * tiles_x + ((tx - ty) % tiles_x + tiles_x) % tiles_x;
 }
 
 // Work item -> pixel; out_index is the output slot (packed tile order or
@@ -599,11 +604,32 @@ struct ForkCtx {
   unsigned int* live_cnt;
 };
 
-// pending-ray entry field 12: heap position (0: past the fork depth), depth
-// and kind (0 camera, 1 reflection, 2 refraction), exact in a double
+// pending-ray entry field 12: bucket (the ray's heap position if it is a
+// node, else its nearest node ancestor's; 0 without buckets), depth and kind
+// (0 camera, 1 reflection, 2 refraction), exact in a double
 __device__ __forceinline__ double pend_code(int pos, int depth, int kind) {
   return static_cast<double>((static_cast<int64_t>(pos) << 40) + (int64_t(1) << 39) + depth * 4 + kind);
 }
+
+// colour c of a ray in bucket b >= 2 of sample s: fbuf[s][b - 2] (written by
+// one lane at a time, in that lane's ray order; the fmask bit says whether
+// the bucket already holds a sum)
+__device__ __forceinline__ void bucket_add(const FrameParams& F, int s, int b, const dvec3& c) {
+  double* f = F.fbuf + (static_cast<int64_t>(s) * F.fork_npos + (b - 2)) * 3;
+  const unsigned int bit = 1u << (b - 2);
+  const unsigned int old = atomicOr(&F.fmask[s], bit);
+  if (old & bit) {
+    f[0] += c.x;
+    f[1] += c.y;
+    f[2] += c.z;
+  } else {
+    f[0] = c.x;
+    f[1] = c.y;
+    f[2] = c.z;
+  }
+}
+
+__host__ __device__ __forceinline__ int ilog2i(int v) { return 31 - __builtin_clz(static_cast<unsigned int>(v)); }
 
 // Run one lane's state machine (trace / traceRay / shade / srsAttenuation,
 // RayTracer.cpp:35-174, material.cpp:34-69, light.cpp:16-53) until it needs
@@ -634,12 +660,18 @@ __device__ __forceinline__ void advance_lane(LaneRef& LR, const DevScene& S, con
     put_entry(pbuf + static_cast<size_t>(tp) * 13 * nlanes + LR.g, p, d, w, k, depth, kind, pos);
     ++tp;
   };
-  // child ray at heap position cpos: its sub-tree on a fork slot, if one is
-  // free (same result as the own stack: the sub-tree's sum joins the
-  // sample's in reduce_kernel); false leaves it to the own stack
+  // colour of the current ray (bucket LR.rpos()): the root's bucket is the
+  // lane's acc, a node's bucket its fbuf entry
+  auto contrib = [&](const dvec3& c) {
+    if (F.fork_on && LR.rpos() >= 2) bucket_add(F, LR.sample_slot(), LR.rpos(), c);
+    else LR.acc() += c;
+  };
+  // child node at heap position cpos: its sub-tree on a fork slot, if one is
+  // free (same buckets, same sums as on the own stack); false leaves it to
+  // the own stack
   auto fork_child = [&](const dvec3& p, const dvec3& d, const dvec3& w, const dvec3& k, int depth, int kind,
                         int cpos) -> bool {
-    if (!FORK || cpos == 0 || fk->spare_n == 0) return false;
+    if (!FORK || cpos < 2 || fk->spare_n == 0) return false;
     const unsigned int idx = atomicAdd(fk->fcnt, 1u);
     if (idx >= fk->spare_n) return false;
     const int T = fk->spare_base + static_cast<int>(idx);
@@ -657,7 +689,6 @@ __device__ __forceinline__ void advance_lane(LaneRef& LR, const DevScene& S, con
     LT.fpos() = cpos;
     LT.dret() = DISC_NONE;
     LT.st() = ST_POP;
-    atomicOr(&F.fmask[LR.sample_slot()], 1u << (cpos - 2));
     fk->live_out[atomicAdd(fk->live_cnt, 1u)] = T;
     return true;
   };
@@ -674,16 +705,20 @@ __device__ __forceinline__ void advance_lane(LaneRef& LR, const DevScene& S, con
     const double eta = next_trans ? (leaving ? hit_index(S, R) : idx_o) / (leaving ? idx_o : hit_index(S, R)) : 0;
     const double radicand = 1 - eta * eta * (1 - c * c);
     const bool tir = next_trans && radicand < 0;
-    // heap positions of the children (0 past the fork depth)
-    const int ppos = LR.rpos();
-    const int pos_refl = ppos > 0 && 2 * ppos < F.fork_npos + 2 ? 2 * ppos : 0;
-    const int pos_refr = ppos > 0 && 2 * ppos + 1 < F.fork_npos + 2 ? 2 * ppos + 1 : 0;
+    // buckets of the children: their own heap positions when they are nodes
+    // (this ray is a node above the fork depth), else this ray's bucket
+    const int pb = LR.rpos();
+    const bool node = pb > 0 && P.depth - LR.rdepth() == ilog2i(pb);
+    const int node_refl = node && 2 * pb < F.fork_npos + 2 ? 2 * pb : 0;
+    const int node_refr = node && 2 * pb + 1 < F.fork_npos + 2 ? 2 * pb + 1 : 0;
+    const int pos_refl = node_refl ? node_refl : pb;
+    const int pos_refr = node_refr ? node_refr : pb;
     // push refraction first so that reflection is traced first
     if (next_trans && !tir && LR.top() < pend_cap) {
       const dvec3 tp = rtm::ray_at(LR.rp(), LR.rd(), LR.st_t() + RTX_RAY_EPS);
       const dvec3 td = eta * LR.rd() + (eta * c - sqrt(radicand)) * normal;
       const dvec3 kf = leaving ? kt_o : hit_param(S, R, RTX_P_KT);
-      if (!fork_child(tp, td, LR.W(), kf, depth, 2, pos_refr)) push(LR.top(), tp, td, LR.W(), kf, depth, 2, pos_refr);
+      if (!fork_child(tp, td, LR.W(), kf, depth, 2, node_refr)) push(LR.top(), tp, td, LR.W(), kf, depth, 2, pos_refr);
       if (STATS) C.secondary++;
     }
     if (((LR.m_flags() & RTX_MF_REFL) || tir) && LR.top() < pend_cap) {
@@ -691,7 +726,7 @@ __device__ __forceinline__ void advance_lane(LaneRef& LR, const DevScene& S, con
       const dvec3 rs = rtm::ray_at(LR.rp(), LR.rd(), LR.st_t() - RTX_RAY_EPS);
       const dvec3 wr = LR.W() * hit_param(S, R, RTX_P_KR);
       const dvec3 kf = leaving ? hit_param(S, R, RTX_P_KT) : kt_o;
-      if (!fork_child(rs, rdir, wr, kf, depth, 1, pos_refl)) push(LR.top(), rs, rdir, wr, kf, depth, 1, pos_refl);
+      if (!fork_child(rs, rdir, wr, kf, depth, 1, node_refl)) push(LR.top(), rs, rdir, wr, kf, depth, 1, pos_refl);
       if (STATS) C.secondary++;
     }
   };
@@ -715,11 +750,8 @@ __device__ __forceinline__ void advance_lane(LaneRef& LR, const DevScene& S, con
         // next camera ray of trace(x, y) (RayTracer.cpp:35-79)
         if (LR.camk() == LR.cam_end()) {
           if (LR.fpos() != 0) {
-            // a forked sub-tree: its sum and its rays join the sample's
-            double* fo = F.fbuf + (static_cast<int64_t>(LR.sample_slot()) * F.fork_npos + (LR.fpos() - 2)) * 3;
-            fo[0] = LR.acc().x;
-            fo[1] = LR.acc().y;
-            fo[2] = LR.acc().z;
+            // a forked sub-tree: its colours are in its buckets already, its
+            // rays join the sample's count
             if (LR.rec_on()) atomicAdd(&hits[LR.sample_slot()].nrays, LR.nrays());
             LR.fpos() = 0;
             LR.st() = ST_IDLE;
@@ -829,8 +861,8 @@ __device__ __forceinline__ void advance_lane(LaneRef& LR, const DevScene& S, con
         const int pdepth = dk >= 0 ? dk / 4 : -((-dk + 3) / 4);
         if (pdepth < 0) {  // `depth >= 0 &&` (RayTracer.cpp:116): no query, the miss colour
           if (S.cube[0] >= 0)
-            LR.acc() += mk3(b[6 * nlanes], b[7 * nlanes], b[8 * nlanes]) *
-                        cube_color(S, mk3(b[3 * nlanes], b[4 * nlanes], b[5 * nlanes]));
+            contrib(mk3(b[6 * nlanes], b[7 * nlanes], b[8 * nlanes]) *
+                    cube_color(S, mk3(b[3 * nlanes], b[4 * nlanes], b[5 * nlanes])));
           break;
         }
         LR.rp() = mk3(b[0 * nlanes], b[1 * nlanes], b[2 * nlanes]);
@@ -866,7 +898,7 @@ __device__ __forceinline__ void advance_lane(LaneRef& LR, const DevScene& S, con
         }
         if (!LR.bhave()) {  // miss: the cube map's colour, else black (RayTracer.cpp:167-169)
           // a child's kt^t factor is kt^0 = 1 on a miss (decision U3)
-          if (S.cube[0] >= 0) LR.acc() += LR.W() * cube_color(S, LR.rd());
+          if (S.cube[0] >= 0) contrib(LR.W() * cube_color(S, LR.rd()));
           LR.st() = ST_POP;
           break;
         }
@@ -894,7 +926,7 @@ __device__ __forceinline__ void advance_lane(LaneRef& LR, const DevScene& S, con
         if (LR.li() == S.n_lights) {
           // colorC = shade(...); adaptive termination; recursion
           const dvec3 col = LR.i_out();
-          LR.acc() += LR.W() * col;
+          contrib(LR.W() * col);
           const int depth = LR.rdepth() - 1;
           LR.st() = ST_POP;
           if (aterm > 0.0 && rtm::dot(col, col) < aterm) break;
@@ -1920,6 +1952,8 @@ struct SceneState {
   unsigned long long* d_stats = nullptr;
   double* d_picks = nullptr;
   int picks_res = -1;
+  double* d_offv = nullptr;     // DoF eye offsets
+  size_t offv_bytes = 0;
   double* d_sbuf = nullptr;     // per-sample colours (HBM), grown on demand
   size_t sbuf_bytes = 0;
   double* d_pbuf = nullptr;     // per-lane pending-ray stacks (HBM)
@@ -2163,6 +2197,7 @@ rtx_status rtx_scene_destroy(void* scene) {
   if (st->d_work) (void)hipFree(st->d_work);
   if (st->d_stats) (void)hipFree(st->d_stats);
   if (st->d_picks) (void)hipFree(st->d_picks);
+  if (st->d_offv) (void)hipFree(st->d_offv);
   if (st->d_sbuf) (void)hipFree(st->d_sbuf);
   if (st->d_pbuf) (void)hipFree(st->d_pbuf);
   if (st->d_fbuf) (void)hipFree(st->d_fbuf);
@@ -2183,7 +2218,8 @@ rtx_status rtx_scene_destroy(void* scene) {
   return RTX_OK;
 }
 
-static rtx_status build_frame(const SceneState* st, const RtxRenderParams* p, FrameParams& F) {
+static rtx_status build_frame(const SceneState* st, const RtxRenderParams* p, FrameParams& F,
+                              std::vector<double>& offv) {
   std::memset(&F, 0, sizeof(F));
   F.P = *p;
   F.cam = st->cam;
@@ -2192,11 +2228,11 @@ static rtx_status build_frame(const SceneState* st, const RtxRenderParams* p, Fr
     return RTX_ERR_INVALID;
   }
   if (p->depth > MAX_DEPTH) {
-    g_err = "rtx_render: recursion depth above 16 is not supported by this build";
+    g_err = "rtx_render: recursion depth above 4096 is not supported by this build";
     return RTX_ERR_CAPACITY;
   }
-  if (p->dof && (p->dof_div < 0 || p->dof_div > MAX_DOF)) {
-    g_err = "rtx_render: DoF samples must be in [0, 64]";
+  if (p->dof && (p->dof_div < 0 || p->dof_div > (1 << 20))) {
+    g_err = "rtx_render: DoF samples must be in [0, 2^20]";
     return RTX_ERR_CAPACITY;
   }
   if (p->aa_mode != RTX_AA_NONE && p->aa_samples <= 0) {
@@ -2258,13 +2294,14 @@ static rtx_status build_frame(const SceneState* st, const RtxRenderParams* p, Fr
     const int divs = p->dof_div;
     const double baseAngle = PI / divs;
     const dvec3 V = ld3(st->cam.v), U = ld3(st->cam.u);
+    offv.assign(size_t(divs) * 3, 0.0);
     for (int k = 0; k < divs; k++) {
       double offsetAngle = PI / 2;
       offsetAngle = offsetAngle / divs + (k - 1) * baseAngle;
       dvec3 o = (std::cos(offsetAngle) * V + std::sin(offsetAngle) * U) * sz;
-      F.offv[k * 3 + 0] = o.x;
-      F.offv[k * 3 + 1] = o.y;
-      F.offv[k * 3 + 2] = o.z;
+      offv[k * 3 + 0] = o.x;
+      offv[k * 3 + 1] = o.y;
+      offv[k * 3 + 2] = o.z;
     }
   }
   return RTX_OK;
@@ -2293,8 +2330,21 @@ rtx_status rtx_render(void* scene, const RtxRenderParams* params, uint8_t* rgb8,
   HIP_TRY(hipSetDevice(st->device));
   hipStream_t stream = static_cast<hipStream_t>(stream_v);
   FrameParams F;
-  rtx_status rc = build_frame(st, params, F);
+  std::vector<double> offv;
+  rtx_status rc = build_frame(st, params, F, offv);
   if (rc != RTX_OK) return rc;
+  if (!offv.empty()) {
+    const size_t need = offv.size() * sizeof(double);
+    if (need > st->offv_bytes) {
+      if (st->d_offv) (void)hipFree(st->d_offv);
+      st->d_offv = nullptr;
+      st->offv_bytes = 0;
+      HIP_TRY(hipMalloc(&st->d_offv, need));
+      st->offv_bytes = need;
+    }
+    HIP_TRY(hipMemcpyAsync(st->d_offv, offv.data(), need, hipMemcpyHostToDevice, stream));
+    F.offv = st->d_offv;
+  }
   // area-light pick tables depend on ss_res
   st->S_launch = st->S;
   DevScene& S = st->S_launch;
@@ -2322,7 +2372,15 @@ rtx_status rtx_render(void* scene, const RtxRenderParams* params, uint8_t* rgb8,
   uint8_t* d_rgb8 = rgb8;
   double* d_rgbf = rgb_f64;
   RtxHitRecord* d_hits = hits;
-  std::vector<void*> tmp;
+  // host-mode staging buffers: freed on every exit path (a failed call
+  // must not leak them)
+  struct TmpBufs {
+    std::vector<void*> v;
+    void push_back(void* p) { v.push_back(p); }
+    ~TmpBufs() {
+      for (void* p : v) (void)hipFree(p);
+    }
+  } tmp;
   if (!device_ptrs) {
     if (rgb8) { HIP_TRY(hipMalloc(&d_rgb8, npix * 3)); tmp.push_back(d_rgb8); HIP_TRY(hipMemsetAsync(d_rgb8, 0, npix * 3, stream)); }
     if (rgb_f64) { HIP_TRY(hipMalloc(&d_rgbf, npix * 3 * sizeof(double))); tmp.push_back(d_rgbf); HIP_TRY(hipMemsetAsync(d_rgbf, 0, npix * 3 * sizeof(double), stream)); }
@@ -2393,7 +2451,6 @@ rtx_status rtx_render(void* scene, const RtxRenderParams* params, uint8_t* rgb8,
     const size_t lds = lds_per_wave * WAVES_PER_WG;
     if (lds > 160 * 1024) {
       g_err = "rtx_render: LDS budget exceeded (BVH too deep or too many AA samples)";
-      for (void* p : tmp) (void)hipFree(p);
       return RTX_ERR_CAPACITY;
     }
     // persistent grid: as many resident workgroups as the occupancy allows
@@ -2455,27 +2512,41 @@ rtx_status rtx_render(void* scene, const RtxRenderParams* params, uint8_t* rgb8,
     const char* g_env = getenv("RTX_GROUPS");
     if (g_env && atoi(g_env) > 0) G = atoi(g_env);
     if (G > 16) G = 16;
-    // ray-tree forking when the frame has fewer samples than 3/4 of the
-    // slots (a shard of a multi-GPU frame): the spare slots run forked
-    // reflection / refraction sub-trees, so a sample's critical path is its
-    // deepest sub-tree instead of its whole tree (RTX_FORK=0: off;
-    // RTX_FORK_DEPTH: heap depth of the deepest forked ray, 1..4)
+    // Ray-tree buckets + forking (DESIGN.md "Ray-tree forking"; no DoF /
+    // anaglyph): every frame of this kind accumulates per-node buckets; when
+    // the frame has fewer samples than 3/4 of the slots, the spare slots run
+    // forked reflection / refraction sub-trees, so a sample's critical path
+    // is its deepest sub-tree instead of its whole tree (RTX_FORK=0: no
+    // buckets, no forks; RTX_FORK_DEPTH: heap depth of the deepest node, 1..4)
     const char* fork_env = getenv("RTX_FORK");
     int fork_depth = 3;
     const char* fd_env = getenv("RTX_FORK_DEPTH");
     if (fd_env && atoi(fd_env) > 0) fork_depth = std::min(4, atoi(fd_env));
-    const bool fork_ok = !(fork_env && atoi(fork_env) == 0) && !F.cam_split && !params->dof && !params->anaglyph;
-    if (fork_ok && !(ns_env && atoll(ns_env) > 0)) {
-      // one slot per sample plus half as many fork slots, within a memory
-      // budget for the slot state + pending-ray stacks (headline frame:
-      // 50 M slots, 89 -> 84 ms; 2-way shard 58 -> 50 ms)
-      const size_t per_slot = lane_mem_bytes(1) + size_t(pend_cap) * 13 * sizeof(double) +
-                              2 * (3 * sizeof(int) + QL_D * sizeof(double)) + 2 * sizeof(int);
-      const int64_t cap = static_cast<int64_t>((size_t(96) << 30) / per_slot);
-      const int64_t want = std::min<int64_t>(cap, F.n_samples + F.n_samples / 2 + int64_t(G) * 2 * WG);
-      if (want > nslot64) nslot64 = want;
+    bool fork_ok = !(fork_env && atoi(fork_env) == 0) && !F.cam_split && !params->dof && !params->anaglyph;
+    const size_t per_slot = lane_mem_bytes(1) + size_t(pend_cap) * 13 * sizeof(double) +
+                            2 * (3 * sizeof(int) + QL_D * sizeof(double)) + 2 * sizeof(int);
+    {
+      // memory budget: what the device has free plus the frame buffers this
+      // scene already holds (they are reused or replaced), less a reserve
+      size_t freeb = 0, totb = 0;
+      HIP_TRY(hipMemGetInfo(&freeb, &totb));
+      const size_t held = st->lane_bytes + st->pbuf_bytes + st->wf_bytes + st->fbuf_bytes + st->fmask_bytes;
+      const size_t sbuf_need = size_t(npix) * F.spp * 3 * sizeof(double);
+      const size_t avail = freeb + held > sbuf_need ? (freeb + held - sbuf_need) / 10 * 8 : 0;
+      const size_t npos = (size_t(1) << (fork_depth + 1)) - 2;
+      const size_t bucket_need = fork_ok ? size_t(npix) * F.spp * (npos * 3 * sizeof(double) + sizeof(unsigned)) : 0;
+      if (bucket_need > avail / 2) fork_ok = false;  // buckets would crowd out the slots: plain accumulation
+      const size_t slot_budget = std::min<size_t>(size_t(96) << 30, avail - (fork_ok ? bucket_need : 0));
+      const int64_t cap = static_cast<int64_t>(slot_budget / per_slot);
+      if (fork_ok && !(ns_env && atoll(ns_env) > 0)) {
+        // one slot per sample plus half as many fork slots (headline frame:
+        // 50 M slots, 89 -> 84 ms; 2-way shard 58 -> 50 ms)
+        const int64_t want = std::min<int64_t>(cap, F.n_samples + F.n_samples / 2 + int64_t(G) * 2 * WG);
+        if (want > nslot64) nslot64 = want;
+      }
+      if (nslot64 > cap && !(ns_env && atoll(ns_env) > 0)) nslot64 = std::max<int64_t>(cap, int64_t(G) * 4 * WG);
     }
-    const bool fork = fork_ok && F.n_samples * 4 <= nslot64 * 3;
+    const bool fork = fork_ok && F.n_samples * 4 <= nslot64 * 3;  // spare slots for forked sub-trees
     int64_t gsamp = (F.n_samples + G - 1) / G;  // sample slots per group
     if (gsamp > (nslot64 + G - 1) / G) gsamp = (nslot64 + G - 1) / G;
     gsamp = (gsamp + 63) / 64 * 64;  // whole 64-unit runs (slot_unit)
@@ -2489,11 +2560,11 @@ rtx_status rtx_render(void* scene, const RtxRenderParams* params, uint8_t* rgb8,
     F.wf_gs = static_cast<int>(gslots);
     F.wf_gsamp = static_cast<int>(gsamp);
     F.wf_groups = G;
-    F.fork_on = fork ? 1 : 0;
-    F.fork_npos = fork ? (1 << (fork_depth + 1)) - 2 : 0;
+    F.fork_on = fork_ok ? 1 : 0;
+    F.fork_npos = fork_ok ? (1 << (fork_depth + 1)) - 2 : 0;
     F.fbuf = nullptr;
     F.fmask = nullptr;
-    if (fork) {
+    if (fork_ok) {
       const size_t nsamp_out = size_t(npix) * F.spp;
       if ((rc = ensure(reinterpret_cast<void**>(&st->d_fbuf), &st->fbuf_bytes,
                        nsamp_out * F.fork_npos * 3 * sizeof(double))) != RTX_OK)
@@ -2580,7 +2651,6 @@ rtx_status rtx_render(void* scene, const RtxRenderParams* params, uint8_t* rgb8,
 #endif
     if (lds > 160 * 1024) {
       g_err = "rtx_render: LDS budget exceeded (BVH too deep)";
-      for (void* p : tmp) (void)hipFree(p);
       return RTX_ERR_CAPACITY;
     }
     const void* tfn = stats ? reinterpret_cast<const void*>(trace_kernel<true, Q_CLOSEST>)
@@ -2705,7 +2775,6 @@ rtx_status rtx_render(void* scene, const RtxRenderParams* params, uint8_t* rgb8,
     if (rgb_f64) HIP_TRY(hipMemcpyAsync(rgb_f64, d_rgbf, npix * 3 * sizeof(double), hipMemcpyDeviceToHost, stream));
     if (hits) HIP_TRY(hipMemcpyAsync(hits, d_hits, npix * F.spp * sizeof(RtxHitRecord), hipMemcpyDeviceToHost, stream));
     HIP_TRY(hipStreamSynchronize(stream));
-    for (void* p : tmp) (void)hipFree(p);
   }
   if (stats) {
     unsigned long long c[18];

@@ -442,4 +442,74 @@ int32_t rtx_image_height(int32_t width, double aspect) {
   return static_cast<int32_t>(width / aspect + 0.5);
 }
 
+rtx_status rtx_read_image(const char* path, int32_t* w, int32_t* h, int32_t* channels, uint8_t* out, int64_t cap) {
+  if (!path || !w || !h || !channels) {
+    g_host_err = "rtx_read_image: null argument";
+    return RTX_ERR_INVALID;
+  }
+  int iw = 0, ih = 0;
+  std::vector<uint8_t> d = rtxh::read_image(path, iw, ih);
+  if (d.empty()) {
+    g_host_err = std::string("Unable to load texture map '") + path + "'.";
+    return RTX_ERR_INVALID;
+  }
+  *w = iw;
+  *h = ih;
+  *channels = static_cast<int32_t>(d.size() / (size_t(iw) * ih));
+  if (out) {
+    if (cap < static_cast<int64_t>(d.size())) {
+      g_host_err = "rtx_read_image: output buffer too small";
+      return RTX_ERR_INVALID;
+    }
+    std::memcpy(out, d.data(), d.size());
+  }
+  return RTX_OK;
+}
+
+// the deal of rtx_render.hip (deal_tile): deal index d = shard + k * nshards
+// is tile row d / tiles_x, column (d % tiles_x + row) % tiles_x
+rtx_status rtx_shard_tiles(int32_t width, int32_t height, int32_t tile, int32_t shard, int32_t nshards, int32_t* ids,
+                           int32_t cap, int32_t* count) {
+  if (width <= 0 || height <= 0 || tile <= 0 || nshards <= 0 || shard < 0 || shard >= nshards || !count) {
+    g_host_err = "rtx_shard_tiles: bad arguments";
+    return RTX_ERR_INVALID;
+  }
+  const int32_t tx = (width + tile - 1) / tile, ty = (height + tile - 1) / tile;
+  int32_t n = 0;
+  for (int64_t d = shard; d < int64_t(tx) * ty; d += nshards, ++n) {
+    if (!ids) continue;
+    if (n >= cap) {
+      g_host_err = "rtx_shard_tiles: id buffer too small";
+      return RTX_ERR_INVALID;
+    }
+    const int32_t row = static_cast<int32_t>(d / tx);
+    ids[n] = row * tx + static_cast<int32_t>((d % tx + row) % tx);
+  }
+  *count = n;
+  return RTX_OK;
+}
+
+rtx_status rtx_unpack_tiles(const void* packed, int32_t width, int32_t height, int32_t tile, int32_t shard,
+                            int32_t nshards, int32_t elem, void* frame) {
+  if (!packed || !frame || elem <= 0) {
+    g_host_err = "rtx_unpack_tiles: bad arguments";
+    return RTX_ERR_INVALID;
+  }
+  int32_t n = 0;
+  if (rtx_shard_tiles(width, height, tile, shard, nshards, nullptr, 0, &n) != RTX_OK) return RTX_ERR_INVALID;
+  std::vector<int32_t> ids(n);
+  rtx_shard_tiles(width, height, tile, shard, nshards, ids.data(), n, &n);
+  const int32_t tx = (width + tile - 1) / tile;
+  const uint8_t* src = static_cast<const uint8_t*>(packed);
+  uint8_t* dst = static_cast<uint8_t*>(frame);
+  for (int32_t k = 0; k < n; ++k) {
+    const int32_t x0 = (ids[k] % tx) * tile, y0 = (ids[k] / tx) * tile;
+    const int32_t cw = std::min(tile, width - x0), chh = std::min(tile, height - y0);
+    for (int32_t r = 0; r < chh; ++r)
+      std::memcpy(dst + (size_t(y0 + r) * width + x0) * elem, src + ((size_t(k) * tile + r) * tile) * elem,
+                  size_t(cw) * elem);
+  }
+  return RTX_OK;
+}
+
 }  // extern "C"

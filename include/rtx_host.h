@@ -47,6 +47,24 @@ rtx_status rtx_host_cubemap(void* handle, const char* one_cubemap_file);
 /* writeImage (fileio/images.cc:59-68): .png / .bmp by extension, RGB8 with
  * buffer row 0 at the bottom. */
 rtx_status rtx_write_image(const char* path, int32_t w, int32_t h, const uint8_t* rgb);
+/* readImage (fileio/images.cc:47-53; readBMP bitmap.cpp:17-93, readPNG
+ * pngimage.cpp:195-216): decodes `path` (.bmp / .png by extension) into
+ * `out` (capacity `cap` bytes; NULL to query the size), row 0 = bottom,
+ * `*channels` bytes per pixel (3, or 4 for a PNG with alpha).  Returns
+ * RTX_ERR_INVALID when the file cannot be read (the reference then throws
+ * "Unable to load texture map"). */
+rtx_status rtx_read_image(const char* path, int32_t* w, int32_t* h, int32_t* channels, uint8_t* out, int64_t cap);
+/* Multi-GPU tile partition, the host side of the deal the
+ * kernels use (rtx_render.hip deal_tile): the tiles shard `shard` of
+ * `nshards` renders, as row-major tile ids from the bottom-left, in its
+ * packed order.  `ids` may be NULL to query the count. */
+rtx_status rtx_shard_tiles(int32_t width, int32_t height, int32_t tile, int32_t shard, int32_t nshards,
+                           int32_t* ids, int32_t cap, int32_t* count);
+/* Scatter one shard's packed tiles (tile*tile pixels per tile, `elem`
+ * bytes per pixel, rows from the bottom) into a full width x height frame
+ * (row 0 = bottom) — the reassembly after the gather. */
+rtx_status rtx_unpack_tiles(const void* packed, int32_t width, int32_t height, int32_t tile, int32_t shard,
+                            int32_t nshards, int32_t elem, void* frame);
 /* height the CLI derives from -w (CommandLineUI.cpp:156) */
 int32_t rtx_image_height(int32_t width, double aspect);
 

@@ -29,4 +29,21 @@ CASES = [
     ("overlap_hitchcock", "hitchcock.ray", "-w 40 -r 3 -O o"),
     ("overlap_trimesh_aa", "trimesh2_square.ray", "-w 24 -r 3 -O o -O r -A 2"),
     ("overlap_area_cube", "lava_box.ray", "-w 32 -r 3 -O o -O s -A 4 -c cubemap/posz.bmp"),
+    # BASELINE.json configs at parity size: C3 (1024^2 square trimesh2,
+    # 4x4 regular AA, depth 5), the headline (16:9 trimesh2, 4x4 AA, depth
+    # 5) and C4 (DoF x16, focal 2.5, aperture 0.05, depth 5)
+    ("c3_trimesh2_aa4", "trimesh2_square.ray", "-w 32 -r 5 -O r -A 4"),
+    ("headline_aa4", "trimesh2.ray", "-w 32 -r 5 -O r -A 4"),
+    ("c4_dof16", "trimesh2.ray", "-w 32 -r 5 -O d -A 2.5 -B 16 -C 0.05"),
+    # next-tier rows: area_light_circ, per-vertex materials, composed
+    # transforms, quaternion camera, PNG textures + bump
+    ("circ_light", "circ_light.ray", "-w 40 -r 3 -O s -A 5"),
+    ("vmats", "vmats.ray", "-w 40 -r 4"),
+    ("xforms_aa", "xforms.ray", "-w 48 -r 4 -O r -A 2"),
+    ("xforms_quat", "xforms_quat.ray", "-w 32 -r 3"),
+    ("png_tex", "png_tex.ray", "-w 40 -r 2"),
+    # recursion deeper than the old -r 16 cap (RayTracer.cpp:108-174 is
+    # unbounded): 2.3 M secondary rays in a 16 x 16 frame
+    ("spheres_deep_r20", "spheres_overlap.ray", "-w 16 -r 20"),
+    ("circ_deep_r40", "circ_light.ray", "-w 16 -r 40"),
 ]

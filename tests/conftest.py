@@ -8,6 +8,7 @@ import pytest
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 GOLDEN = os.path.join(ROOT, "tests", "golden")
 NEWSCENE = os.path.join(GOLDEN, "newScene")
+FEATURE = os.path.join(GOLDEN, "feature")
 SCENES = os.path.join(ROOT, "scenes")
 
 
@@ -56,7 +57,7 @@ def cli_opts(pkg, flags):
 
 
 def scene_path(name):
-    for d in (NEWSCENE, SCENES, GOLDEN):
+    for d in (NEWSCENE, FEATURE, SCENES, GOLDEN):
         p = os.path.join(d, name)
         if os.path.exists(p):
             return p

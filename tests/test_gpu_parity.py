@@ -11,7 +11,14 @@ import numpy as np
 import pytest
 
 from cases import CASES
-from conftest import cli_opts, scene_path
+from conftest import ROOT, cli_opts, scene_path
+
+
+def scene_path_or_none(name):
+    try:
+        return scene_path(name)
+    except FileNotFoundError:
+        return None
 
 pytestmark = pytest.mark.gpu
 
@@ -84,22 +91,41 @@ def test_parity(pkg, orc, render_path, name, scene, flags):
         assert gpu["stats"][k] == ref["stats"][k], (k, gpu["stats"][k], ref["stats"][k])
 
 
-def test_sharded_tiles_reassemble(pkg, render_path):
-    """Tile sharding: packed shards reassemble to the full frame."""
-    path = scene_path("hitchcock.ray")
-    opts = pkg.RenderOptions.from_cli("-w 100 -r 2 -O r -A 2".split())
+SHARD_CASES = [
+    # C4: DoF x16 at depth 5, image-tiled across 8 ranks
+    ("c4_dof16_x8", "trimesh2.ray", "-w 64 -r 5 -O d -A 2.5 -B 16 -C 0.05", 16, 8),
+    # the headline (4x4 AA, depth 5) tiled across 8 ranks: ray-tree buckets
+    # and forks on every shard
+    ("headline_aa4_x8", "trimesh2.ray", "-w 64 -r 5 -O r -A 4", 16, 8),
+    ("hitchcock_aa2_x3", "hitchcock.ray", "-w 100 -r 2 -O r -A 2", 32, 3),
+]
+
+
+@pytest.mark.parametrize("name,scene,flags,tile,nshards", SHARD_CASES, ids=[c[0] for c in SHARD_CASES])
+def test_sharded_tiles_reassemble(pkg, orc, render_path, name, scene, flags, tile, nshards):
+    """Tile sharding: every shard's packed tiles, scattered by
+    rtx_unpack_tiles (the multi-GPU driver's reassembly), give the full
+    frame bit for bit, and that frame matches the CPU restatement."""
+    path = scene_path(scene)
+    opts = cli_opts(pkg, flags)
     host = pkg.HostScene(path)
     dev = pkg.DeviceScene(host, 0)
     full = dev.render(opts, want_f64=True)
     h = full["height"]
     out8 = np.zeros((h, opts.width, 3), np.uint8)
     outf = np.zeros((h, opts.width, 3), np.float64)
-    for shard in range(3):
-        part = dev.render(opts, want_f64=True, tile=32, shard=shard, nshards=3, packed=True)
-        pkg.unpack_tiles(part["rgb8"], opts.width, h, 32, shard, 3, out8)
-        pkg.unpack_tiles(part["rgb"], opts.width, h, 32, shard, 3, outf)
+    for shard in range(nshards):
+        part = dev.render(opts, want_f64=True, tile=tile, shard=shard, nshards=nshards, packed=True)
+        assert part["npix"] == len(pkg.owned_tiles(opts.width, h, tile, shard, nshards)) * tile * tile
+        pkg.unpack_tiles(part["rgb8"], opts.width, h, tile, shard, nshards, out8)
+        pkg.unpack_tiles(part["rgb"], opts.width, h, tile, shard, nshards, outf)
     assert np.array_equal(out8, full["rgb8"])
     assert np.array_equal(outf, full["rgb"])
+    ref = orc.render(pkg, path, opts, want_hits=False)
+    assert np.abs(outf - ref["rgb"]).max() <= 1e-4
+    scaled = 255.0 * ref["rgb"]
+    boundary = np.abs(scaled - np.round(scaled)) < 1e-9
+    assert not ((out8 != ref["rgb8"]) & ~boundary).any()
 
 
 def test_repeat_deterministic(pkg):
@@ -109,6 +135,59 @@ def test_repeat_deterministic(pkg):
     a = dev.render(opts)
     b = dev.render(opts)
     assert np.array_equal(a["rgb"], b["rgb"])
+
+
+@pytest.mark.parametrize("slots", ["20000", "40000", "1000000"])
+def test_buckets_independent_of_fork_slots(pkg, slots):
+    """Ray-tree buckets make the image independent of which sub-trees won a
+    fork slot: a frame whose spare slots run out, one with a few
+    spares and one with plenty render bit-identical images, equal to the
+    auto-sized default."""
+    path = scene_path("spheres_overlap.ray")
+    opts = pkg.RenderOptions.from_cli("-w 64 -r 5 -O r -A 2".split())  # 16384 samples
+    dev = pkg.DeviceScene(pkg.HostScene(path), 0)
+    base = dev.render(opts)
+    saved = os.environ.get("RTX_SLOTS")
+    os.environ["RTX_SLOTS"] = slots
+    try:
+        for _ in range(2):
+            r = dev.render(opts)
+            assert np.array_equal(r["rgb"], base["rgb"])
+    finally:
+        if saved is None:
+            os.environ.pop("RTX_SLOTS", None)
+        else:
+            os.environ["RTX_SLOTS"] = saved
+
+
+@pytest.fixture(scope="session")
+def dragon_path(tmp_path_factory):
+    """The generated 1M-triangle dragon stand-in (tools/gen_scenes.py, seed
+    7; not committed)."""
+    import subprocess
+    import sys
+
+    p = scene_path_or_none("dragon.ray")
+    if p:
+        return p
+    d = tmp_path_factory.mktemp("dragon")
+    subprocess.run([sys.executable, os.path.join(ROOT, "tools", "gen_scenes.py"), str(d), "--dragon"], check=True,
+                   stdout=subprocess.DEVNULL)
+    return os.path.join(str(d), "dragon.ray")
+
+
+def test_c5_dragon_adaptive(pkg, orc, dragon_path):
+    """C5 at parity size: the 1M-triangle dragon, 8x8 adaptive AA
+    (RayTracer.cpp:316-365), depth 5 — mesh BVH of 951,423 nodes."""
+    opts = pkg.RenderOptions.from_cli("-w 16 -r 5 -O a -A 8".split())
+    host = pkg.HostScene(dragon_path)
+    assert host.info.n_faces == 1000000
+    dev = pkg.DeviceScene(host, 0)
+    gpu = dev.render(opts, want_f64=True, want_hits=True, stats=True)
+    ref = orc.render(pkg, dragon_path, opts, want_hits=True)
+    _compare(gpu, ref, opts.spp)
+    for k in ("camera_rays", "secondary_rays", "shadow_rays"):
+        assert gpu["stats"][k] == ref["stats"][k], (k, gpu["stats"][k], ref["stats"][k])
 
 
 def test_no_device_fallback_error(pkg):
