@@ -4,10 +4,13 @@
 //   tokenizer   ray/src/parser/Tokenizer.cpp:70-237, Token.cpp:121-196,
 //               fileio/buffer.cpp (line-at-a-time reading, '\0' at EOF)
 //   parser      ray/src/parser/Parser.cpp:26-1308
-//   scene build scene/scene.cpp:78-153 (world boxes), SceneObjects/trimesh.cpp
-//               (addFace degeneracy, generateNormals), camera.cpp, light.h ctors
-// Errors are reported as ParseError carrying the message RayTracer::loadScene
-// would print (RayTracer.cpp:216-234).
+// It produces the RAW records of scene_model.h only (transform chains,
+// camera attribute ops, raw faces / normals, light attributes): the scene
+// build arithmetic (transforms, world boxes, camera basis, face records,
+// light axes) is scene_build.cpp's, so the CPU oracle can link this parser
+// and restate the build on its own.  Errors are reported as ParseError
+// carrying the message RayTracer::loadScene would print
+// (RayTracer.cpp:216-234).
 #include <dirent.h>
 #include <cmath>
 #include <cstdlib>
@@ -32,61 +35,6 @@ void Material::setBools() {
   recur = refl || trans;
   spec = refl || !isZero(p[P_KS]);
   both = refl && trans;
-}
-
-// ---------------------------------------------------------------- Camera
-// camera.cpp:4 defines its own PI
-static const double CAM_PI = 3.14159265359;
-
-Camera::Camera() { m = mat3_identity(); }
-
-void Camera::update() {  // camera.cpp:94-99
-  dvec3 ex = rtm::mat3_mul(m.m, mk3(1, 0, 0));
-  dvec3 ey = rtm::mat3_mul(m.m, mk3(0, 1, 0));
-  dvec3 ez = rtm::mat3_mul(m.m, mk3(0, 0, -1));
-  u = (ex * normalizedHeight) * aspectRatio;
-  v = ey * normalizedHeight;
-  look = ez;
-}
-
-void Camera::setFOV(double fov) {  // camera.cpp:77-84
-  fov /= (180.0 / CAM_PI);
-  normalizedHeight = 2 * std::tan(fov / 2);
-  update();
-}
-
-void Camera::setAspectRatio(double ar) {
-  aspectRatio = ar;
-  update();
-}
-
-void Camera::setLook(const dvec3& viewDir, const dvec3& upDir) {  // camera.cpp:64-74
-  dvec3 z = -viewDir;
-  const dvec3& y = upDir;
-  dvec3 x = rtm::cross(y, z);
-  // dmat3x3(x, y, z): columns
-  m.m[0] = x.x; m.m[1] = x.y; m.m[2] = x.z;
-  m.m[3] = y.x; m.m[4] = y.y; m.m[5] = y.z;
-  m.m[6] = z.x; m.m[7] = z.y; m.m[8] = z.z;
-  update();
-}
-
-void Camera::setLookQuat(double r, double i, double j, double k) {  // camera.cpp:39-62
-  double a[3][3];  // a[c][r] as in the reference's m[c][r]
-  a[0][0] = 1.0 - 2.0 * (i * i + j * j);
-  a[0][1] = 2.0 * (r * i - j * k);
-  a[0][2] = 2.0 * (j * r + i * k);
-  a[1][0] = 2.0 * (r * i + j * k);
-  a[1][1] = 1.0 - 2.0 * (j * j + r * r);
-  a[1][2] = 2.0 * (i * j - r * k);
-  a[2][0] = 2.0 * (j * r - i * k);
-  a[2][1] = 2.0 * (i * j + r * k);
-  a[2][2] = 1.0 - 2.0 * (i * i + r * r);
-  Mat3 t;
-  for (int c = 0; c < 3; ++c)
-    for (int rr = 0; rr < 3; ++rr) t.m[c * 3 + rr] = a[c][rr];
-  m = mat3_transpose(t);
-  update();
 }
 
 // ---------------------------------------------------------------- Tokenizer
@@ -337,6 +285,13 @@ class Tokenizer {
 };
 
 // ---------------------------------------------------------------- Parser
+// a transform node of the parse: its raw operation and its parent (nullptr:
+// the root node, identity)
+struct TNode {
+  const TNode* parent;
+  XformOp op;
+};
+
 class Parser {
  public:
   Parser(Tokenizer& tk, const std::string& base) : tk_(tk), base_(base) {}
@@ -383,20 +338,39 @@ class Parser {
     for (;;) {
       switch (tk_.peek().kind) {
         case POSITION: sc_.camera.eye = parseVec3dExpression(); break;
-        case FOV: sc_.camera.setFOV(parseScalarExpression()); break;
+        case FOV: {
+          CamOp op;
+          op.kind = CAM_FOV;
+          op.v[0] = parseScalarExpression();
+          sc_.camera.ops.push_back(op);
+          break;
+        }
         case QUATERNIAN: {
           double q[4];
           parseVec4dExpression(q);
-          sc_.camera.setLookQuat(q[0], q[1], q[2], q[3]);
+          CamOp op;
+          op.kind = CAM_QUAT;
+          for (int k = 0; k < 4; ++k) op.v[k] = q[k];
+          sc_.camera.ops.push_back(op);
           break;
         }
-        case ASPECTRATIO: sc_.camera.setAspectRatio(parseScalarExpression()); break;
+        case ASPECTRATIO: {
+          CamOp op;
+          op.kind = CAM_ASPECT;
+          op.v[0] = parseScalarExpression();
+          sc_.camera.ops.push_back(op);
+          break;
+        }
         case VIEWDIR: viewDir = parseVec3dExpression(); hasViewDir = true; break;
         case UPDIR: upDir = parseVec3dExpression(); hasUpDir = true; break;
         case RBRACE:
           if (hasViewDir) {
             if (!hasUpDir) tk_.syntax("Expected: 'updir'");
-            sc_.camera.setLook(viewDir, upDir);
+            CamOp op;  // setLook(viewDir, upDir) at the block's end
+            op.kind = CAM_LOOK;
+            op.v[0] = viewDir.x; op.v[1] = viewDir.y; op.v[2] = viewDir.z;
+            op.v[3] = upDir.x; op.v[4] = upDir.y; op.v[5] = upDir.z;
+            sc_.camera.ops.push_back(op);
           } else if (hasUpDir) {
             tk_.syntax("Expected: 'viewdir'");
           }
@@ -408,7 +382,7 @@ class Parser {
   }
 
   // ------------------------------------------------------------ geometry
-  void parseTransformableElement(const Transform* tf, const Material& mat) {
+  void parseTransformableElement(const TNode* tf, const Material& mat) {
     switch (tk_.peek().kind) {
       case SPHERE: case BOX: case SQUARE: case CYLINDER: case CONE: case TRIMESH:
       case TRANSLATE: case ROTATE: case SCALE: case TRANSFORM:
@@ -419,7 +393,7 @@ class Parser {
     }
   }
 
-  void parseGroup(const Transform* tf, const Material& mat) {  // Parser.cpp:180-211
+  void parseGroup(const TNode* tf, const Material& mat) {  // Parser.cpp:180-211
     tk_.read(LBRACE);
     for (;;) {
       switch (tk_.peek().kind) {
@@ -438,7 +412,7 @@ class Parser {
     }
   }
 
-  void parseGeometry(const Transform* tf, const Material& mat) {
+  void parseGeometry(const TNode* tf, const Material& mat) {
     switch (tk_.peek().kind) {
       case SPHERE: parseSimple(tf, mat, SPHERE, OBJ_SPHERE, "sphere"); return;
       case BOX: parseSimple(tf, mat, BOX, OBJ_BOX, "box"); return;
@@ -455,41 +429,51 @@ class Parser {
   }
 
   // Each transform node is created before the child is parsed and lives for
-  // the whole parse (TransformNode::createChild, scene.h:85-90).
-  const Transform* child(const Transform* parent, const Mat4& local) {
-    nodes_.emplace_back(new Transform(make_transform(parent, local)));
+  // the whole parse (TransformNode::createChild, scene.h:85-90); a node
+  // records its raw operation, an object the chain of operations from the
+  // root (identity) down to it.
+  const TNode* child(const TNode* parent, const XformOp& op) {
+    nodes_.emplace_back(new TNode{parent, op});
     return nodes_.back().get();
   }
-  const Transform* rootOr(const Transform* tf) {
-    if (tf) return tf;
-    if (!root_) root_.reset(new Transform(make_transform(nullptr, mat4_identity())));
-    return root_.get();
+  const TNode* rootOr(const TNode* tf) { return tf; }  // nullptr = the root node
+  static std::vector<XformOp> chain_of(const TNode* n) {
+    std::vector<XformOp> c;
+    for (; n; n = n->parent) c.push_back(n->op);
+    return std::vector<XformOp>(c.rbegin(), c.rend());
+  }
+  static XformOp xop(int kind, std::initializer_list<double> v) {
+    XformOp op;
+    op.kind = kind;
+    int k = 0;
+    for (double x : v) op.v[k++] = x;
+    return op;
   }
 
-  void parseTranslate(const Transform* tf, const Material& mat) {
+  void parseTranslate(const TNode* tf, const Material& mat) {
     tk_.read(TRANSLATE);
     tk_.read(LPAREN);
     double x = parseScalar(); tk_.read(COMMA);
     double y = parseScalar(); tk_.read(COMMA);
     double z = parseScalar(); tk_.read(COMMA);
-    parseTransformableElement(child(rootOr(tf), mat4_translate(mk3(x, y, z))), mat);
+    parseTransformableElement(child(rootOr(tf), xop(XF_TRANSLATE, {x, y, z})), mat);
     tk_.read(RPAREN);
     tk_.condRead(SEMICOLON);
   }
 
-  void parseRotate(const Transform* tf, const Material& mat) {
+  void parseRotate(const TNode* tf, const Material& mat) {
     tk_.read(ROTATE);
     tk_.read(LPAREN);
     double x = parseScalar(); tk_.read(COMMA);
     double y = parseScalar(); tk_.read(COMMA);
     double z = parseScalar(); tk_.read(COMMA);
     double w = parseScalar(); tk_.read(COMMA);
-    parseTransformableElement(child(rootOr(tf), mat4_rotate(w, mk3(x, y, z))), mat);
+    parseTransformableElement(child(rootOr(tf), xop(XF_ROTATE, {x, y, z, w})), mat);
     tk_.read(RPAREN);
     tk_.condRead(SEMICOLON);
   }
 
-  void parseScale(const Transform* tf, const Material& mat) {
+  void parseScale(const TNode* tf, const Material& mat) {
     tk_.read(SCALE);
     tk_.read(LPAREN);
     double x = parseScalar(), y, z;
@@ -501,12 +485,12 @@ class Parser {
       y = x;
       z = x;
     }
-    parseTransformableElement(child(rootOr(tf), mat4_scale(mk3(x, y, z))), mat);
+    parseTransformableElement(child(rootOr(tf), xop(XF_SCALE, {x, y, z})), mat);
     tk_.read(RPAREN);
     tk_.condRead(SEMICOLON);
   }
 
-  void parseTransform(const Transform* tf, const Material& mat) {
+  void parseTransform(const TNode* tf, const Material& mat) {
     tk_.read(TRANSFORM);
     tk_.read(LPAREN);
     double rows[4][4];
@@ -514,17 +498,18 @@ class Parser {
       parseVec4d(rows[r]);
       tk_.read(COMMA);
     }
-    // glm::transpose(dmat4x4(row1..row4)): dmat4x4 takes the rows as columns
-    Mat4 a;
-    for (int c = 0; c < 4; ++c)
-      for (int r = 0; r < 4; ++r) a.m[c * 4 + r] = rows[c][r];
-    parseTransformableElement(child(rootOr(tf), mat4_transpose(a)), mat);
+    // the scene build applies glm::transpose(dmat4x4(row1..row4))
+    XformOp op;
+    op.kind = XF_MATRIX;
+    for (int r = 0; r < 4; ++r)
+      for (int c = 0; c < 4; ++c) op.v[r * 4 + c] = rows[r][c];
+    parseTransformableElement(child(rootOr(tf), op), mat);
     tk_.read(RPAREN);
     tk_.condRead(SEMICOLON);
   }
 
   // sphere / box / square / cylinder (Parser.cpp:348-470)
-  void parseSimple(const Transform* tf, const Material& mat, Sym kw, int type, const char* what) {
+  void parseSimple(const TNode* tf, const Material& mat, Sym kw, int type, const char* what) {
     tk_.read(kw);
     tk_.read(LBRACE);
     bool haveMat = false;
@@ -537,7 +522,7 @@ class Parser {
           tk_.read(RBRACE);
           Object o;
           o.type = type;
-          o.tf = *rootOr(tf);
+          o.chain = chain_of(tf);
           addObject(o, haveMat ? newMat : mat);
           return;
         }
@@ -546,7 +531,7 @@ class Parser {
     }
   }
 
-  void parseCone(const Transform* tf, const Material& mat) {  // Parser.cpp:472-518
+  void parseCone(const TNode* tf, const Material& mat) {  // Parser.cpp:472-518
     tk_.read(CONE);
     tk_.read(LBRACE);
     bool haveMat = false;
@@ -565,7 +550,7 @@ class Parser {
           tk_.read(RBRACE);
           Object o;
           o.type = OBJ_CONE;
-          o.tf = *rootOr(tf);
+          o.chain = chain_of(tf);
           // Cone::Cone (Cone.h:11-37), same operations in the same order
           o.cone_h = height;
           o.cone_br = (bottomRadius < 0.0f) ? (-bottomRadius) : (bottomRadius);
@@ -587,56 +572,15 @@ class Parser {
     }
   }
 
-  // local bounds + world box (scene.cpp:78-116)
+  // Scene::add (scene.cpp:133-138): the object and its material copy; the
+  // world box is the scene build's (scene_build.cpp)
   void addObject(Object& o, const Material& m) {
-    dvec3 lmin, lmax;
-    bool empty = false;
-    switch (o.type) {
-      case OBJ_SPHERE: lmin = mk3(-1, -1, -1); lmax = mk3(1, 1, 1); break;
-      case OBJ_BOX: lmin = mk3(-0.5, -0.5, -0.5); lmax = mk3(0.5, 0.5, 0.5); break;
-      case OBJ_CYLINDER: lmin = mk3(-1, -1, 0); lmax = mk3(1, 1, 1); break;
-      case OBJ_SQUARE: lmin = mk3(-0.5, -0.5, -0.00000001); lmax = mk3(0.5, 0.5, 0.00000001); break;
-      case OBJ_CONE: {  // Cone::ComputeLocalBoundingBox (Cone.h:42-50)
-        const double big = (o.cone_br > o.cone_tr) ? (o.cone_br) : (o.cone_tr);
-        lmin = mk3(-big, -big, (o.cone_h < 0.0f) ? (o.cone_h) : (0.0f));
-        lmax = mk3(big, big, (o.cone_h < 0.0f) ? (0.0f) : (o.cone_h));
-        break;
-      }
-      case OBJ_TRIMESH: {
-        const Mesh& me = sc_.meshes[o.mesh];
-        lmin = me.lmin;
-        lmax = me.lmax;
-        empty = me.lbox_empty;
-        break;
-      }
-      default: lmin = lmax = mk3(0, 0, 0);
-    }
-    (void)empty;  // an empty local box still yields corners at (0,0,0)
-    const dvec3 c[8] = {mk3(lmin.x, lmin.y, lmin.z), mk3(lmax.x, lmin.y, lmin.z),
-                        mk3(lmin.x, lmax.y, lmin.z), mk3(lmax.x, lmax.y, lmin.z),
-                        mk3(lmin.x, lmin.y, lmax.z), mk3(lmax.x, lmin.y, lmax.z),
-                        mk3(lmin.x, lmax.y, lmax.z), mk3(lmax.x, lmax.y, lmax.z)};
-    double nmax[4], nmin[4];
-    for (int k = 0; k < 8; ++k) {
-      double in[4] = {c[k].x, c[k].y, c[k].z, 1.0}, v[4];
-      mat4_mul_vec4(o.tf.xform, in, v);
-      if (k == 0) {
-        for (int a = 0; a < 4; ++a) nmax[a] = nmin[a] = v[a];
-      } else {
-        for (int a = 0; a < 4; ++a) {
-          nmax[a] = rtm::gmax(nmax[a], v[a]);
-          nmin[a] = rtm::gmin(nmin[a], v[a]);
-        }
-      }
-    }
-    o.wmax = mk3(nmax[0], nmax[1], nmax[2]);
-    o.wmin = mk3(nmin[0], nmin[1], nmin[2]);
     o.material = static_cast<int>(sc_.materials.size());
     sc_.materials.push_back(m);
     sc_.objects.push_back(o);
   }
 
-  void parseTrimesh(const Transform* tf, const Material& mat) {  // Parser.cpp:520-653
+  void parseTrimesh(const TNode* tf, const Material& mat) {  // Parser.cpp:520-653
     Material meshMat = mat;
     tk_.read(TRIMESH);
     tk_.read(LBRACE);
@@ -664,11 +608,11 @@ class Parser {
         case NORMALS:
           tk_.read(NORMALS); tk_.read(EQUALS); tk_.read(LPAREN);
           if (tk_.peek().kind != RPAREN) {
-            me.normals.push_back(parseVec3d());
+            me.raw_normals.push_back(parseVec3d());
             for (;;) {
               if (tk_.peek().kind == RPAREN) break;
               tk_.read(COMMA);
-              me.normals.push_back(parseVec3d());
+              me.raw_normals.push_back(parseVec3d());
             }
           }
           tk_.read(RPAREN); tk_.read(SEMICOLON);
@@ -707,27 +651,20 @@ class Parser {
               o << "Parser: fatal exception Bad face in trimesh: (" << f[0] << ", " << f[1] << ", " << f[2] << ")";
               throw ParseError(o.str());
             }
-            addFace(me, a, b, c);
+            me.raw_faces.push_back({a, b, c});  // Trimesh::addFace drops degenerate ones (scene build)
           }
-          if (genNormals) generateNormals(me);
+          me.gennormals = genNormals;
+          // generateNormals resizes the normals to the vertex count first
+          // (trimesh.cpp:192-217), so only a mesh without gennormals can
+          // have the wrong number (Parser.cpp:640-651)
           if (!vmats.empty() && vmats.size() != me.verts.size())
             throw ParseError("Parser: fatal exception Bad Trimesh: Wrong number of materials.");
-          if (!me.normals.empty() && me.normals.size() != me.verts.size())
+          if (!genNormals && !me.raw_normals.empty() && me.raw_normals.size() != me.verts.size())
             throw ParseError("Parser: fatal exception Bad Trimesh: Wrong number of normals.");
           me.vmats = vmats;
-          // ComputeLocalBoundingBox (trimesh.h:63-80)
-          if (!me.verts.empty()) {
-            me.lmax = me.verts[0];
-            me.lmin = me.verts[0];
-            for (const auto& v : me.verts) {
-              me.lmax = rtm::gmax3(me.lmax, v);
-              me.lmin = rtm::gmin3(me.lmin, v);
-            }
-            me.lbox_empty = false;
-          }
           Object o;
           o.type = OBJ_TRIMESH;
-          o.tf = *rootOr(tf);
+          o.chain = chain_of(tf);
           o.mesh = static_cast<int>(sc_.meshes.size());
           sc_.meshes.push_back(std::move(me));
           addObject(o, meshMat);
@@ -736,35 +673,6 @@ class Parser {
         default: tk_.syntax("Expected: trimesh attributes");
       }
     }
-  }
-
-  // TrimeshFace ctor + Trimesh::addFace (trimesh.h:100-130, trimesh.cpp:38-56)
-  static void addFace(Mesh& me, int a, int b, int c) {
-    const dvec3 A = me.verts[a], B = me.verts[b], C = me.verts[c];
-    dvec3 vab = B - A, vac = C - A, vcb = B - C;
-    if (rtm::length(vab) == 0.0 || rtm::length(vac) == 0.0 || rtm::length(vcb) == 0.0) return;  // degen
-    dvec3 n = rtm::normalize(rtm::cross(B - A, C - A));
-    // ComputeLocalBoundingBox (trimesh.h:149-161)
-    dvec3 bmax = rtm::gmax3(A, B), bmin = rtm::gmin3(A, B);
-    bmax = rtm::gmax3(C, bmax);
-    bmin = rtm::gmin3(C, bmin);
-    me.faces.push_back({a, b, c});
-    me.face_normals.push_back(n);
-    me.face_boxes.push_back({bmin, bmax});
-  }
-
-  static void generateNormals(Mesh& me) {  // trimesh.cpp:192-217
-    const size_t cnt = me.verts.size();
-    me.normals.resize(cnt, dvec3{0, 0, 0});
-    std::vector<int> numFaces(cnt, 0);
-    for (size_t f = 0; f < me.faces.size(); ++f) {
-      for (int i = 0; i < 3; ++i) {
-        me.normals[me.faces[f][i]] += me.face_normals[f];
-        ++numFaces[me.faces[f][i]];
-      }
-    }
-    for (size_t i = 0; i < cnt; ++i)
-      if (numFaces[i]) me.normals[i] = me.normals[i] / static_cast<double>(numFaces[i]);
   }
 
   void parseFaces(std::list<std::array<double, 3>>& faces) {  // Parser.cpp:655-671
@@ -839,7 +747,7 @@ class Parser {
           if (!hasCol) tk_.syntax("Expected: 'color'");
           if (!hasDir) tk_.syntax("Expected: 'position'");
           tk_.read(RBRACE);
-          L.orient = rtm::normalize(dir);  // DirectionalLight ctor (light.h:39-40)
+          L.raw_dir = dir;  // DirectionalLight ctor normalizes it (scene build)
           return L;
         default: tk_.syntax("expecting 'position' or 'color' attribute");
       }
@@ -904,19 +812,8 @@ class Parser {
           if (!hasDir) tk_.syntax("Expected: 'direction'");
           tk_.read(RBRACE);
           L.c = c; L.l = l; L.q = q;
-          L.orient = rtm::normalize(dir);  // AreaLight ctor (light.h:102-104)
-          if (type == L_AREA_RECT) {
-            // AreaLightRect ctor (light.h:120-127): u(normalize(u)),
-            // v(cross(ori, u)) where ori/u are the constructor PARAMETERS.
-            L.u = rtm::normalize(up);
-            L.v = rtm::cross(dir, up);
-          }
-          if (type == L_SPOT) {
-            // SpotLight ctor (light.h:153-155), PI from util.h
-            const double PI = 3.1415926535897932384626433832795028841971;
-            L.ang_tan = std::tan(L.angle / 360 * PI);
-            L.offset = L.ang_tan * L.radius;
-          }
+          L.raw_dir = dir;  // the light ctors' axes are the scene build's
+          L.raw_up = up;
           return L;
         }
         default:
@@ -1107,8 +1004,7 @@ class Parser {
   SceneModel sc_;
   std::map<std::string, Material> named_;
   std::map<std::string, int> tex_cache_;
-  std::vector<std::unique_ptr<Transform>> nodes_;
-  std::unique_ptr<Transform> root_;
+  std::vector<std::unique_ptr<TNode>> nodes_;
 };
 
 }  // namespace
@@ -1119,7 +1015,7 @@ SceneModel parse_ray_text(const std::string& text, const std::string& base_path)
   return p.parseScene();
 }
 
-SceneModel load_ray_file(const std::string& path) {  // RayTracer::loadScene (RayTracer.cpp:196-240)
+SceneModel parse_ray_file_raw(const std::string& path) {  // RayTracer::loadScene's parse (RayTracer.cpp:196-240)
   std::ifstream ifs(path, std::ios::binary);
   if (!ifs) throw ParseError("Error: couldn't read scene file " + path);
   std::stringstream ss;

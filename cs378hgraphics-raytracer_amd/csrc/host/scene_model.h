@@ -54,12 +54,31 @@ struct Transform {
   Mat3 normi;
 };
 
+// ---- raw parse records --------------------------------------------------
+// What the .ray text says, before any scene-build arithmetic.  The parser
+// fills only these (plus materials, textures, colours, attenuation
+// coefficients and raw vertex / face lists); finalize_scene() (product,
+// scene_build.cpp) derives every Transform, world box, camera basis, mesh
+// face record and light axis from them, and the CPU oracle derives the same
+// quantities with its own restatement (oracle/scene_build_restated.cpp).
+enum XformKind { XF_TRANSLATE = 0, XF_ROTATE = 1, XF_SCALE = 2, XF_MATRIX = 3 };
+struct XformOp {
+  int kind = XF_TRANSLATE;
+  double v[16] = {0};  // translate / scale: x y z; rotate: axis x y z, angle (rad); matrix: the 4 rows as written
+};
+enum CamOpKind { CAM_FOV = 0, CAM_ASPECT = 1, CAM_LOOK = 2, CAM_QUAT = 3 };
+struct CamOp {
+  int kind = CAM_FOV;
+  double v[6] = {0};  // fov (deg); aspect; look: viewdir xyz, updir xyz; quat: r i j k
+};
+
 // Geometry (scene/scene.h:140-188) with its world bounding box.
 struct Object {
   int type = OBJ_SPHERE;
   int material = -1;  // index into SceneModel::materials
   int mesh = -1;      // index into SceneModel::meshes
-  Transform tf;
+  std::vector<XformOp> chain;  // raw: transform nodes from the root down to the object
+  Transform tf;                // derived (finalize): root * chain[0] * ... * chain[n-1]
   dvec3 wmin{0, 0, 0}, wmax{0, 0, 0};
   bool has_box = true;  // hasBoundingBoxCapability() (true for every supported primitive)
   // Cone (Cone.h:11-37): height, b_radius, t_radius, beta_squared, gamma
@@ -71,6 +90,12 @@ struct Object {
 // non-degenerate faces, in Trimesh::faces order (addFace, trimesh.cpp:38-56).
 struct Mesh {
   std::vector<dvec3> verts;
+  // raw: fan-triangulated faces as parsed (indices range-checked), the
+  // parsed per-vertex normals, and the gennormals flag
+  std::vector<std::array<int, 3>> raw_faces;
+  std::vector<dvec3> raw_normals;
+  bool gennormals = false;
+  // derived (finalize):
   std::vector<std::array<int, 3>> faces;
   std::vector<dvec3> face_normals;            // TrimeshFace::normal
   std::vector<std::array<dvec3, 2>> face_boxes;  // local bounds (min, max)
@@ -88,10 +113,12 @@ struct Light {
   int type = L_POINT;
   dvec3 color{0, 0, 0};
   dvec3 pos{0, 0, 0};
-  dvec3 orient{0, 0, 0};  // normalized (DirectionalLight / AreaLight ctor)
+  dvec3 raw_dir{0, 0, 0}, raw_up{0, 0, 0};  // raw: direction / updir attributes
+  dvec3 orient{0, 0, 0};  // derived: normalized (DirectionalLight / AreaLight ctor)
   float c = 0.0f, l = 0.0f, q = 1.0f;
-  double width = 0, height = 0, radius = 0, angle = 0, ang_tan = 0, offset = 0;
-  dvec3 u{0, 0, 0}, v{0, 0, 0};  // area-rect axes
+  double width = 0, height = 0, radius = 0, angle = 0;  // raw
+  double ang_tan = 0, offset = 0;                        // derived (SpotLight ctor)
+  dvec3 u{0, 0, 0}, v{0, 0, 0};                          // derived: area-rect axes
 };
 
 struct Texture {
@@ -100,16 +127,18 @@ struct Texture {
   std::vector<uint8_t> data;  // RGB8, row 0 = bottom row of the file
 };
 
-// Camera (scene/camera.cpp)
+// Camera (scene/camera.cpp).  eye and ops are raw (the camera block's
+// attributes in file order; viewdir + updir become one CAM_LOOK at the
+// block's end, as Parser.cpp:97-154 applies them); m .. v are derived.
 struct Camera {
-  Mat3 m;  // default identity (glm 0.9.8 default dmat3)
+  std::vector<CamOp> ops;
+  Mat3 m{{1, 0, 0, 0, 1, 0, 0, 0, 1}};  // default identity (glm 0.9.8 default dmat3)
   double normalizedHeight = 1.0;
   double aspectRatio = 1.0;
   dvec3 eye{0, 0, 0};
   dvec3 look{0, 0, -1};
   dvec3 u{1, 0, 0};
   dvec3 v{0, 1, 0};
-  Camera();
   void update();
   void setFOV(double fov);
   void setAspectRatio(double ar);
@@ -126,16 +155,23 @@ struct SceneModel {
   Camera camera;
   dvec3 ambient{0, 0, 0};
   std::string base_path;
+  bool finalized = false;  // derived fields filled (finalize_scene)
 };
 
 struct ParseError : public std::runtime_error {
   explicit ParseError(const std::string& m) : std::runtime_error(m) {}
 };
 
-// Parse a .ray file (Parser::parseScene semantics).  Throws ParseError with
-// the reference's messages on malformed input.
-SceneModel load_ray_file(const std::string& path);
+// Parse a .ray file (Parser::parseScene semantics) into the raw records.
+// Throws ParseError with the reference's messages on malformed input.
+SceneModel parse_ray_file_raw(const std::string& path);
 SceneModel parse_ray_text(const std::string& text, const std::string& base_path);
+// Product scene build (scene_build.cpp): the derived fields from the raw
+// records (TransformNode ctor, Geometry::ComputeBoundingBox, Camera,
+// Trimesh::addFace / generateNormals / ComputeLocalBoundingBox, light ctors).
+void finalize_scene(SceneModel& sc);
+// parse_ray_file_raw + finalize_scene: RayTracer::loadScene's scene.
+SceneModel load_ray_file(const std::string& path);
 
 // glm 0.9.8 matrix helpers (glm_compat.cpp)
 Mat4 mat4_identity();

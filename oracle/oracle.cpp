@@ -27,6 +27,8 @@ using rtm::mk3;
 
 namespace orc {
 
+void restate_scene_build(rtxh::SceneModel& sc);  // scene_build_restated.cpp
+
 const double RAY_EPSILON = 0.00000001;                            // scene/ray.h:136
 const double PI = 3.1415926535897932384626433832795028841971;     // util.h:11
 const double EPS_BACKUP = 0.0000000001;                           // light.cpp:13
@@ -266,7 +268,14 @@ struct Geom {
   virtual bool intersectLocal(Ray& r, Isect& i) const = 0;
   virtual void intersectLocalList(Ray& r, std::vector<Isect>& iv) const = 0;
 
-  dvec3 globalToLocal(const dvec3& v) const { return rtxh::mat4_mul_point(tf->inverse, v); }
+  // operator*(dmat4x4, dvec3) (scene.h:57-62): glm mat4 * dvec4(v, 1),
+  // (m0 x + m1 y) + (m2 z + m3 w) per row
+  dvec3 globalToLocal(const dvec3& v) const {
+    const double* m = tf->inverse.m;
+    double o[3];
+    for (int r = 0; r < 3; ++r) o[r] = (m[0 * 4 + r] * v.x + m[1 * 4 + r] * v.y) + (m[2 * 4 + r] * v.z + m[3 * 4 + r] * 1.0);
+    return mk3(o[0], o[1], o[2]);
+  }
   dvec3 localToGlobalNormal(const dvec3& v) const { return rtm::normalize(rtm::mat3_mul(tf->normi.m, v)); }
 
   bool intersect(Ray& r, Isect& i) const {  // scene.cpp:13-38
@@ -1241,7 +1250,11 @@ struct Tracer {
 
 std::unique_ptr<Scene> build_scene(const std::string& path) {
   std::unique_ptr<Scene> S(new Scene());
-  S->model = rtxh::load_ray_file(path);
+  // the parser's raw records; every derived quantity (transforms, world
+  // boxes, camera basis, face records, light axes) is this oracle's own
+  // restatement of the scene build (scene_build_restated.cpp)
+  S->model = rtxh::parse_ray_file_raw(path);
+  restate_scene_build(S->model);
   rtxh::SceneModel& M = S->model;
   for (const auto& t : M.textures) S->texs.push_back(Tex{&t});
   // trimesh KdTrees over local face boxes (trimesh.cpp:69-77)
@@ -1328,6 +1341,51 @@ std::unique_ptr<Scene> build_scene(const std::string& path) {
 extern "C" {
 
 const char* oracle_last_error(void) { return orc::g_err.c_str(); }
+
+int oracle_scene_dump(const char* ray_path, double* objs, int32_t cap, int32_t* n, double* cam) {
+  try {
+    rtxh::SceneModel m = rtxh::parse_ray_file_raw(ray_path);
+    orc::restate_scene_build(m);
+    *n = static_cast<int32_t>(m.objects.size());
+    if (cam) {
+      const rtm::dvec3 cv[4] = {m.camera.eye, m.camera.look, m.camera.u, m.camera.v};
+      for (int k = 0; k < 4; ++k) {
+        cam[k * 3 + 0] = cv[k].x;
+        cam[k * 3 + 1] = cv[k].y;
+        cam[k * 3 + 2] = cv[k].z;
+      }
+    }
+    if (!objs) return 0;
+    if (cap < *n) {
+      orc::g_err = "oracle_scene_dump: buffer too small";
+      return -1;
+    }
+    for (int32_t k = 0; k < *n; ++k) {
+      const rtxh::Object& o = m.objects[size_t(k)];
+      double* d = objs + size_t(k) * 27;
+      const double b[6] = {o.wmin.x, o.wmin.y, o.wmin.z, o.wmax.x, o.wmax.y, o.wmax.z};
+      for (int i = 0; i < 6; ++i) d[i] = b[i];
+      for (int c = 0; c < 4; ++c)
+        for (int r = 0; r < 3; ++r) d[6 + c * 3 + r] = o.tf.inverse.m[c * 4 + r];
+      for (int i = 0; i < 9; ++i) d[18 + i] = o.tf.normi.m[i];
+    }
+    return 0;
+  } catch (const std::exception& e) {
+    orc::g_err = e.what();
+    return -1;
+  }
+}
+
+double oracle_aspect(const char* ray_path) {
+  try {
+    rtxh::SceneModel m = rtxh::parse_ray_file_raw(ray_path);
+    orc::restate_scene_build(m);
+    return m.camera.aspectRatio;
+  } catch (const std::exception& e) {
+    orc::g_err = e.what();
+    return -1.0;
+  }
+}
 
 int oracle_render(const char* ray_path, const char* cubemap_file, const RtxRenderParams* params,
                   const OracleRect* rect, uint8_t* rgb8, double* rgb_f64, RtxHitRecord* hits, RtxStats* stats) {

@@ -31,12 +31,20 @@ typedef struct OracleRect {
 } OracleRect;
 
 const char* oracle_last_error(void);
+/* RayTracer::aspectRatio (RayTracer.cpp:191-194) of the restated camera;
+ * < 0 on a load error. */
+double oracle_aspect(const char* ray_path);
 /* Render `ray_path` with the reference algorithm.  Outputs are full-frame
  * (reference buffer indexing (i + j*w)*3); only pixels inside `rect` are
  * written.  hits: aa-samples-per-pixel records (NULL allowed).
  * cubemap_file: -c (NULL or "": none). */
 int oracle_render(const char* ray_path, const char* cubemap_file, const RtxRenderParams* params,
                   const OracleRect* rect, uint8_t* rgb8, double* rgb_f64, RtxHitRecord* hits, RtxStats* stats);
+/* The restated scene build (scene_build_restated.cpp) of `ray_path`: per
+ * object (parse order) 27 doubles — world box min, max (6), inverse rows
+ * 0..2 as inv[c*3+r] (12), normi[c*3+r] (9); and the camera's eye, look, u,
+ * v (12).  *n = object count; objs may be NULL to query it. */
+int oracle_scene_dump(const char* ray_path, double* objs, int32_t cap, int32_t* n, double* cam);
 /* Structural hashes of the oracle's own KdTree builds (same definition as
  * RtxHostInfo.scene_bvh_hash / mesh_bvh_hash). */
 int oracle_bvh_hash(const char* ray_path, uint64_t* scene_hash, uint64_t* mesh_hash);

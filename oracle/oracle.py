@@ -39,6 +39,9 @@ def lib(pkg):
             build()
         L = C.CDLL(LIB)
         L.oracle_last_error.restype = C.c_char_p
+        L.oracle_aspect.restype = C.c_double
+        L.oracle_aspect.argtypes = [C.c_char_p]
+        L.oracle_scene_dump.argtypes = [C.c_char_p, C.c_void_p, C.c_int32, C.POINTER(C.c_int32), C.c_void_p]
         L.oracle_render.argtypes = [C.c_char_p, C.c_char_p, C.POINTER(pkg.RtxRenderParams), C.POINTER(OracleRect),
                                     C.c_void_p, C.c_void_p, C.c_void_p, C.POINTER(pkg.RtxStats)]
         L.oracle_bvh_hash.argtypes = [C.c_char_p, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]
@@ -72,13 +75,20 @@ def query_batch(pkg, path: str, P, D, mode: int, kmax: int = 1):
     return t, o, f, nh
 
 
+def height_for(pkg, path: str, width: int) -> int:
+    """CommandLineUI.cpp:156: height = (int)(w / aspectRatio + 0.5), with the
+    restated camera's aspect ratio."""
+    a = lib(pkg).oracle_aspect(path.encode())
+    if a < 0:
+        raise RuntimeError(lib(pkg).oracle_last_error().decode())
+    return int(width / a + 0.5)
+
+
 def render(pkg, path: str, opts, rect=None, threads: int = 0, want_hits: bool = True):
     """Render with the restatement.  Returns dict(rgb8, rgb, hits, stats) in
     the same layout as DeviceScene.render (full frame)."""
     L = lib(pkg)
-    host = pkg.HostScene(path)
-    h = host.height_for(opts.width)
-    host.close()
+    h = height_for(pkg, path, opts.width)
     p = opts.params(h)
     w = opts.width
     rgb8 = np.zeros((h, w, 3), np.uint8)
@@ -95,6 +105,21 @@ def render(pkg, path: str, opts, rect=None, threads: int = 0, want_hits: bool = 
     if rc != 0:
         raise RuntimeError(L.oracle_last_error().decode())
     return {"rgb8": rgb8, "rgb": rgb, "hits": hits, "stats": st.as_dict(), "height": h, "width": w}
+
+
+def scene_dump(pkg, path: str):
+    """The restated scene build: (objects (n, 27) float64 — wmin, wmax,
+    inverse rows 0..2 [c*3+r], normi [c*3+r] — and camera (4, 3): eye,
+    look, u, v)."""
+    L = lib(pkg)
+    n = C.c_int32()
+    cam = np.zeros((4, 3), np.float64)
+    if L.oracle_scene_dump(path.encode(), None, 0, C.byref(n), cam.ctypes.data) != 0:
+        raise RuntimeError(L.oracle_last_error().decode())
+    objs = np.zeros((n.value, 27), np.float64)
+    if L.oracle_scene_dump(path.encode(), objs.ctypes.data, n.value, C.byref(n), cam.ctypes.data) != 0:
+        raise RuntimeError(L.oracle_last_error().decode())
+    return objs, cam
 
 
 def bvh_hash(pkg, path: str):

@@ -16,7 +16,7 @@ int main(int argc, char** argv) {
   if (rc) return rc;
   double aspect = 1.0;
   try {
-    aspect = rtxh::load_ray_file(o.ray_name).camera.aspectRatio;
+    aspect = oracle_aspect(o.ray_name.c_str());
   } catch (const std::exception& e) {
     std::cerr << e.what() << std::endl;
     std::cerr << "Unable to load ray file '" << o.ray_name << "'" << std::endl;

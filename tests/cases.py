@@ -42,6 +42,10 @@ CASES = [
     ("xforms_aa", "xforms.ray", "-w 48 -r 4 -O r -A 2"),
     ("xforms_quat", "xforms_quat.ray", "-w 32 -r 3"),
     ("png_tex", "png_tex.ray", "-w 40 -r 2"),
+    # the composed-transform and per-vertex-material known-answer scenes
+    ("kat_xform_nested", "xform_nested.ray", "-w 24 -r 1"),
+    ("kat_xform_matrix", "xform_matrix.ray", "-w 24 -r 1"),
+    ("kat_vmat_quad", "vmat_quad.ray", "-w 16 -r 0"),
     # recursion deeper than the old -r 16 cap (RayTracer.cpp:108-174 is
     # unbounded): 2.3 M secondary rays in a 16 x 16 frame
     ("spheres_deep_r20", "spheres_overlap.ray", "-w 16 -r 20"),

@@ -57,7 +57,7 @@ def cli_opts(pkg, flags):
 
 
 def scene_path(name):
-    for d in (NEWSCENE, FEATURE, SCENES, GOLDEN):
+    for d in (NEWSCENE, FEATURE, SCENES, GOLDEN, os.path.join(GOLDEN, "kat")):
         p = os.path.join(d, name)
         if os.path.exists(p):
             return p

@@ -317,3 +317,92 @@ def test_dragon_bvh_matches_restated_kdtree(pkg, orc, tmp_path_factory):
     assert h.info.mesh_depth == 19
     sh, mh = orc.bvh_hash(pkg, path)
     assert (h.info.scene_bvh_hash, h.info.mesh_bvh_hash) == (sh, mh)
+
+
+# ------------------------------------------------------------------ oracle independence
+class _RtxObject(C.Structure):
+    _fields_ = [("wmin", C.c_double * 3), ("wmax", C.c_double * 3), ("inv", C.c_double * 12),
+                ("normi", C.c_double * 9), ("type", C.c_int32), ("material", C.c_int32), ("mesh", C.c_int32),
+                ("orig_id", C.c_int32), ("leaf", C.c_int32), ("pad", C.c_int32 * 5)]
+
+
+def test_oracle_links_no_product_scene_build():
+    """The checker restates the scene build itself: oracle/
+    compiles neither glm_compat.cpp nor scene_build.cpp, and liboracle.so
+    defines none of their symbols."""
+    mk = open(os.path.join(ROOT, "oracle", "Makefile")).read()
+    src = [ln for ln in mk.splitlines() if ln.startswith("SRC")][0]
+    assert "glm_compat" not in src and "scene_build.cpp" not in src
+    out = subprocess.run(["nm", "-C", "--defined-only", os.path.join(ROOT, "oracle", "_build", "liboracle.so")],
+                         check=True, capture_output=True, text=True).stdout
+    for sym in ("rtxh::mat4_inverse", "rtxh::finalize_scene", "rtxh::Camera::setLook", "rtxh::make_transform"):
+        assert sym not in out, sym
+
+
+SCENE_BUILD_CASES = ["xforms.ray", "xforms_quat.ray", "vmats.ray", "circ_light.ray", "png_tex.ray", "hitchcock.ray",
+                     "trimesh2.ray", "spheres_overlap.ray", "distance.ray", "lava_box.ray", "concrete_2.ray",
+                     "box_cyl_opaque_shadow_spotlight.ray", "cones.ray"]
+
+
+@pytest.mark.parametrize("scene", SCENE_BUILD_CASES)
+def test_scene_build_matches_restatement(pkg, orc, scene):
+    """Product scene build (scene_build.cpp over glm_compat.cpp) vs the
+    oracle's own restatement: world boxes, inverse rows, normi and the camera
+    basis agree bit for bit."""
+    path = scene_path(scene)
+    h = pkg.HostScene(path)
+    objs, cam = orc.scene_dump(pkg, path)
+    n = h.desc.n_objects
+    assert n == objs.shape[0]
+    arr = (_RtxObject * n).from_address(h.desc.objects)
+    got = np.zeros((n, 27))
+    for o in arr:
+        got[o.orig_id] = list(o.wmin) + list(o.wmax) + list(o.inv) + list(o.normi)
+    assert np.array_equal(got.view(np.uint64), objs.view(np.uint64)), np.argwhere(got != objs)[:5]
+    c = h.desc.camera
+    pc = np.array([list(c.eye), list(c.look), list(c.u), list(c.v)])
+    assert np.array_equal(pc.view(np.uint64), cam.view(np.uint64))
+
+
+def test_kat_composed_transforms(pkg, orc):
+    """translate(1, 2, -3, rotate(z, pi/2, scale(2, 1, 1, sphere))): an
+    ellipsoid centred at (1, 2, -3) with semi-axis 2 along world y.  A ray
+    down -y from y = 12 meets its top at y = 4 (t = 8); one along -z meets
+    the front at z = -2 (t = 12)."""
+    hit, t, n, obj, _ = _probe(pkg, orc, "xform_nested.ray", (1, 12, -3), (0, -1, 0))
+    assert hit and abs(t - 8.0) < 1e-12 and np.abs(np.array(n) - [0, 1, 0]).max() < 1e-12
+    hit, t, n, _, _ = _probe(pkg, orc, "xform_nested.ray", (1, 2, 10), (0, 0, -1))
+    assert hit and abs(t - 12.0) < 1e-12 and np.abs(np.array(n) - [0, 0, 1]).max() < 1e-12
+    hit, *_ = _probe(pkg, orc, "xform_nested.ray", (2.5, 2, 10), (0, 0, -1))  # |x - 1| > 1: outside
+    assert not hit
+    objs, cam = orc.scene_dump(pkg, os.path.join(KAT, "xform_nested.ray"))
+    assert np.abs(objs[0, :6] - [0, 0, -4, 2, 4, -2]).max() < 1e-12  # world box
+    # fov 90 with camera.cpp's PI = 3.14159265359: v = (0, 2 tan(pi/4), 0)
+    assert cam[1].tolist() == [0.0, 0.0, -1.0] and abs(cam[3][1] - 2.0) < 1e-11
+
+
+def test_kat_transform_matrix(pkg, orc):
+    """transform((1,0,0,.5), (0,2,0,0), (0,0,1,-1), (0,0,0,1), box): rows as
+    written (glm::transpose of the column constructor, Parser.cpp:313-346) —
+    the unit box stretched 2x in y and centred at (0.5, 0, -1)."""
+    hit, t, n, _, _ = _probe(pkg, orc, "xform_matrix.ray", (0.5, 0, 5), (0, 0, -1))
+    assert hit and t == 5.5 and n == (0.0, 0.0, 1.0)
+    hit, t, n, _, _ = _probe(pkg, orc, "xform_matrix.ray", (0.5, 10, -1), (0, -1, 0))
+    assert hit and t == 9.0 and n == (0.0, 1.0, 0.0)
+    hit, *_ = _probe(pkg, orc, "xform_matrix.ray", (0.5, 1.01, 5), (0, 0, -1))
+    assert not hit
+
+
+def test_kat_per_vertex_materials(pkg, orc):
+    """trimesh.cpp:157-163: a hit's material is Material() += b_k * M_k over
+    the face's vertices — with ambient light 1 and nothing else, the colour
+    at barycentric (u, v, w) is the interpolated ambient (ka = (u, v, w))."""
+    opts = pkg.RenderOptions.from_cli("-w 16 -r 0".split())
+    r = orc.render(pkg, os.path.join(KAT, "vmat_quad.ray"), opts, want_hits=True)
+    # the camera looks at (0.25, 0.25) down -z: the pixel at the image centre
+    # sees the triangle at (0.25 + dx, 0.25 + dy); ka = (1 - x - y, x, y)
+    hit = r["hits"][..., 0]["object"] >= 0
+    assert hit.sum() > 40
+    rgb = r["rgb"][hit]
+    assert np.abs(rgb.sum(axis=1) - 1.0).max() < 1e-12  # barycentric weights sum to 1
+    assert (rgb >= -1e-12).all()
