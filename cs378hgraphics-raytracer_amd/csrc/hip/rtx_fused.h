@@ -1,0 +1,583 @@
+// rtx_fused.h — fused shadow walks on the wavefront path (DESIGN.md §4
+// "Fused shadow walks").  Included by rtx_render.hip after the lane state,
+// the query lists and the sample claim.
+//
+// A frame whose lights are all point / directional lights (and that has no
+// overlapping media and no adaptive termination) runs this state machine
+// instead of advance_lane:
+//   * at a closest hit the lane evaluates Material::shade's light loop
+//     (material.cpp:34-69) for every light at once and appends one next-hit
+//     record per light whose term can be non-zero — the shadow ray of
+//     shadowAttenuation / srsAttenuation (light.cpp:16-53);
+//   * trace_kernel<Q_NEXT, FUSED> runs each record's whole walk (hit after
+//     hit, walk_hit below) in the same persistent launch and writes the
+//     light's finished term dattn * sattn * color * (d + s) to a per-(light,
+//     slot) buffer — no round trip through the lane state per hit;
+//   * the lane does not wait for its terms: it pushes the hit's reflection /
+//     refraction rays (with m_out = air and no adaptive termination they do
+//     not depend on the colour), pops the next ray and issues its closest
+//     query in the same step.  The hit's colour W * (i_out + terms) is added
+//     at the start of the lane's next step, before anything else reaches the
+//     sample's sum, so the sum's order — and every bit of it — is the
+//     sequential machine's (the terms are added to i_out in light order).
+// The tail kernel runs the same machine with the walks inline (INLINE).
+#pragma once
+
+#define Q_WAIT 3  // no query: the lane waits one iteration for its shadow terms
+
+// next-hit record of a fused walk, field-major in the group's next list
+enum {
+  QF_PX = 0, QF_PY, QF_PZ,     // walk origin: the shading point backed up (light.cpp:13, 28)
+  QF_DX, QF_DY, QF_DZ,         // toward the light
+  QF_TP, QF_TLIM, QF_TBLK,     // key of the last hit, query bounds (shadow_bounds)
+  QF_DATTN, QF_SCX, QF_SCY, QF_SCZ,  // distanceAttenuation, d_comp + s_comp
+  QF_WPX, QF_WPY, QF_WPZ,      // the walk's moved origin (light.cpp:37)
+  QF_SAX, QF_SAY, QF_SAZ,      // sattn so far
+  QF_LAST,                     // t of the last hit
+  QF_D
+};
+#define QF_I 3  // ints: rp (last hit's object, -1 before the first), sq, light
+
+struct WalkState {
+  dvec3 wpos, sattn;
+  double last_t;
+};
+
+// One hit of srsAttenuation's sorted walk (light.cpp:30-50) toward a point
+// or directional light with m_out = air (what ST_WALK + walk_on do on the
+// sequential machine).  true: the walk is over and res is its attenuation.
+__device__ __forceinline__ bool walk_hit(const DevScene& S, const RtxLight& L, const dvec3& pb, const dvec3& sdir,
+                                         bool have, double bt, int bobj, int bsub, WalkState& w, dvec3& res) {
+  if (!have) {
+    res = w.sattn;
+    return true;
+  }
+  const double t = bt - w.last_t;
+  w.last_t = bt;
+  const HitRef R = resolve_hit(S, pb, sdir, bobj, bsub, nullptr, nullptr);
+  const bool is_inside = rtm::dot(R.N, sdir) > 0;
+  w.wpos = rtm::ray_at(w.wpos, sdir, t);
+  // sattnLimitCheck with the relative t (U14); directional lights never trip it
+  if (L.type == RTX_LIGHT_POINT && rtm::dot(ld3(L.pos) - rtm::ray_at(w.wpos, sdir, t), sdir) <= 0) {
+    res = w.sattn;
+    return true;
+  }
+  const bool next_trans = is_inside ? true : ((hit_flags(S, R) & RTX_MF_TRANS) != 0);
+  if (!next_trans) {
+    res = mk3(0.0, 0.0, 0.0);
+    return true;
+  }
+  const dvec3 kt = is_inside ? hit_param(S, R, RTX_P_KT) : mk3(1.0, 1.0, 1.0);
+  w.sattn *= rtm::pow3(kt, t);
+  return false;
+}
+
+// A whole walk in the calling lane (tail kernel): successive next-hit
+// queries from the list start.
+template <bool STATS>
+__device__ __forceinline__ dvec3 walk_inline(const DevScene& S, const RtxLight& L, const dvec3& pb, const dvec3& sdir,
+                                             int* __restrict__ stk, int lane, Counters& C) {
+  WalkState w = {pb, mk3(1.0, 1.0, 1.0), 0.0};
+  double tp = -RTX_INF;
+  int rp = -1, sq = -1;
+  for (;;) {
+    double qlim, qblk;
+    shadow_bounds(S, L, pb, rp < 0, qlim, qblk);
+    double bt;
+    int bo, bs;
+    const bool have = traverse<STATS>(S, Q_NEXT, pb, sdir, tp, rp, sq, qlim, bt, bo, bs, stk, lane, C);
+    dvec3 res;
+    if (walk_hit(S, L, pb, sdir, have, bt, bo, bs, w, res)) return res;
+    tp = bt;
+    rp = bo;
+    sq = bs;
+  }
+}
+
+// the group's next-hit list and its append counter
+struct WalkEmit {
+  QList q;
+  unsigned int* cnt;
+};
+
+// Append a walk record for the lanes with `on` (wave-aggregated: one atomic
+// per call per wave, offsets by mbcnt).  Called from divergent code: the
+// ballot covers the lanes executing it, the lowest of them claims.
+__device__ __forceinline__ void emit_walk(const WalkEmit& E, bool on, int slot, int li, const dvec3& pb,
+                                          const dvec3& sdir, double qlim, double qblk, double dattn,
+                                          const dvec3& dscomp) {
+  const unsigned long long m = __ballot(on);
+  if (!on) return;
+  const int leader = __builtin_ctzll(m);
+  const int lane = threadIdx.x & 63;
+  unsigned int base = 0;
+  if (lane == leader) base = atomicAdd(E.cnt, static_cast<unsigned int>(__popcll(m)));
+  base = __shfl(base, leader);
+  const size_t k = base + lane_prefix(m);
+  const size_t cap = E.q.cap;
+  double* d = E.q.d;
+  d[QF_PX * cap + k] = pb.x;
+  d[QF_PY * cap + k] = pb.y;
+  d[QF_PZ * cap + k] = pb.z;
+  d[QF_DX * cap + k] = sdir.x;
+  d[QF_DY * cap + k] = sdir.y;
+  d[QF_DZ * cap + k] = sdir.z;
+  d[QF_TP * cap + k] = -RTX_INF;
+  d[QF_TLIM * cap + k] = qlim;
+  d[QF_TBLK * cap + k] = qblk;
+  d[QF_DATTN * cap + k] = dattn;
+  d[QF_SCX * cap + k] = dscomp.x;
+  d[QF_SCY * cap + k] = dscomp.y;
+  d[QF_SCZ * cap + k] = dscomp.z;
+  E.q.iv[0 * cap + k] = -1;
+  E.q.iv[1 * cap + k] = -1;
+  E.q.iv[2 * cap + k] = li;
+  E.q.slot[k] = slot;
+}
+
+// colour c into bucket pos of the lane's sample (the root's bucket is acc)
+__device__ __forceinline__ void contrib_at(LaneRef& LR, const FrameParams& F, int pos, const dvec3& c) {
+  if (F.fork_on && pos >= 2) bucket_add(F, LR.sample_slot(), pos, c);
+  else LR.acc() += c;
+}
+
+// The deferred colour of the lane's last hit: W * (i_out + its lights'
+// terms in light order) (material.cpp:45-66, RayTracer.cpp:125).
+__device__ __forceinline__ void flush_terms(LaneRef& LR, const FrameParams& F) {
+  unsigned int m = static_cast<unsigned int>(LR.wmask());
+  if (!m) return;
+  dvec3 col = LR.i_out();
+  while (m) {
+    const int l = __builtin_ctz(m);
+    m &= m - 1;
+    col += ld3(F.wterm + (size_t(l) * LR.m.n + LR.g) * 3);
+  }
+  contrib_at(LR, F, LR.rpos(), LR.W() * col);
+  LR.wmask() = 0;
+}
+
+// The fused state machine (CAM -> POP -> HIT): runs until the lane needs a
+// closest-hit query (Q_CLOSEST: the ray is pending-stack entry `top`), has to
+// wait for its terms (Q_WAIT) or its sample is finished (ST_IDLE).
+// INLINE: walks run in this lane (tail kernel); else they are appended to
+// the group's next list (we) and the hit's colour is deferred.
+template <bool STATS, bool INLINE, bool FORK>
+__device__ __forceinline__ void advance_fused(LaneRef& LR, const DevScene& S, const FrameParams& F, Counters& C,
+                                              double* __restrict__ sbuf, RtxHitRecord* __restrict__ hits,
+                                              double* __restrict__ pbuf, size_t nlanes, int pend_cap,
+                                              const ForkCtx* fk, const WalkEmit* we, int* __restrict__ stk,
+                                              int lane) {
+  const RtxRenderParams& P = F.P;
+  auto put_entry = [&](double* b, const dvec3& p, const dvec3& d, const dvec3& w, const dvec3& k, int depth, int kind,
+                       int pos) {
+    b[0 * nlanes] = p.x; b[1 * nlanes] = p.y; b[2 * nlanes] = p.z;
+    b[3 * nlanes] = d.x; b[4 * nlanes] = d.y; b[5 * nlanes] = d.z;
+    b[6 * nlanes] = w.x; b[7 * nlanes] = w.y; b[8 * nlanes] = w.z;
+    b[9 * nlanes] = k.x; b[10 * nlanes] = k.y; b[11 * nlanes] = k.z;
+    b[12 * nlanes] = pend_code(pos, depth, kind);
+  };
+  auto push = [&](const dvec3& p, const dvec3& d, const dvec3& w, const dvec3& k, int depth, int kind, int pos) {
+    put_entry(pbuf + static_cast<size_t>(LR.top()) * 13 * nlanes + LR.g, p, d, w, k, depth, kind, pos);
+    ++LR.top();
+  };
+  // child node at heap position cpos: its sub-tree on a fork slot, if one is
+  // free (same buckets, same sums as on the own stack)
+  auto fork_child = [&](const dvec3& p, const dvec3& d, const dvec3& w, const dvec3& k, int depth, int kind,
+                        int cpos) -> bool {
+    if (!FORK || cpos < 2 || fk->spare_n == 0) return false;
+    const unsigned int idx = atomicAdd(fk->fcnt, 1u);
+    if (idx >= fk->spare_n) return false;
+    const int T = fk->spare_base + static_cast<int>(idx);
+    LaneRef LT(LR.m, static_cast<size_t>(T));
+    put_entry(pbuf + static_cast<size_t>(T), p, d, w, k, depth, kind, cpos);
+    LT.top() = 1;
+    LT.acc() = mk3(0.0, 0.0, 0.0);
+    LT.nrays() = 0;
+    LT.camk() = 1;
+    LT.cam_end() = 1;
+    LT.pass() = 0;
+    LT.first_query() = 0;
+    LT.rec_on() = LR.rec_on();
+    LT.sample_slot() = LR.sample_slot();
+    LT.fpos() = cpos;
+    LT.wmask() = 0;
+    LT.st() = ST_POP;
+    fk->live_out[atomicAdd(fk->live_cnt, 1u)] = T;
+    return true;
+  };
+  LR.qmode() = Q_NONE;
+  while (LR.st() != ST_IDLE && LR.qmode() == Q_NONE) {
+    LR.refresh();
+    switch (LR.st()) {
+      case ST_CAM: {
+        // next camera ray of trace(x, y) (RayTracer.cpp:35-79)
+        if (LR.camk() == LR.cam_end()) {
+          if (LR.wmask()) {  // the last hit's colour belongs to this sum
+            LR.qmode() = Q_WAIT;
+            break;
+          }
+          if (LR.fpos() != 0) {  // a forked sub-tree: sums in its buckets, rays join the sample's count
+            if (LR.rec_on()) atomicAdd(&hits[LR.sample_slot()].nrays, LR.nrays());
+            LR.fpos() = 0;
+            LR.st() = ST_IDLE;
+            break;
+          }
+          if (F.fork_on) {  // the root's sum; reduce_kernel adds the buckets, then clamps
+            double* out = sbuf + static_cast<int64_t>(LR.sample_slot()) * 3;
+            out[0] = LR.acc().x;
+            out[1] = LR.acc().y;
+            out[2] = LR.acc().z;
+            if (LR.rec_on()) atomicAdd(&hits[LR.sample_slot()].nrays, LR.nrays() + 1);
+            LR.st() = ST_IDLE;
+            break;
+          }
+          if (F.cam_split) {  // one camera ray of a DoF sample: its own sum (reduce_kernel scales, clamps)
+            const int64_t u = static_cast<int64_t>(LR.sample_slot()) * F.ncam + (LR.cam_end() - 1);
+            sbuf[u * 3 + 0] = LR.acc().x;
+            sbuf[u * 3 + 1] = LR.acc().y;
+            sbuf[u * 3 + 2] = LR.acc().z;
+            if (LR.rec_on()) atomicAdd(&hits[LR.sample_slot()].nrays, LR.nrays() + (LR.cam_end() == 1 ? 1 : 0));
+            LR.st() = ST_IDLE;
+            break;
+          }
+          dvec3 ret = LR.acc();
+          if (P.dof) ret *= (1.0 / (P.dof_div + 1.0));
+          ret = rtm::gclamp3(ret, 0.0, 1.0);
+          double* out = sbuf + static_cast<int64_t>(LR.sample_slot()) * 3;
+          if (P.anaglyph && LR.pass() == 0) {  // tracePixel (RayTracer.cpp:92-99): park pass 0
+            out[0] = ret.x;
+            out[1] = ret.y;
+            out[2] = ret.z;
+            LR.pass() = 1;
+            LR.camk() = 0;
+            LR.acc() = mk3(0, 0, 0);
+            break;
+          }
+          if (P.anaglyph) {
+            out[0] = ret.x;  // red from the shifted eye, green/blue from pass 0
+          } else {
+            out[0] = ret.x;
+            out[1] = ret.y;
+            out[2] = ret.z;
+          }
+          if (LR.rec_on()) hits[LR.sample_slot()].nrays = LR.nrays();
+          LR.st() = ST_IDLE;
+          break;
+        }
+        const RtxCamera& cam = F.cam;
+        const dvec3 eye = LR.pass() ? ld3(cam.eye) + mk3(0.25, 0.0, 0.0) : ld3(cam.eye);
+        const double x = LR.sx() - 0.5, y = LR.sy() - 0.5;
+        const dvec3 cdir = rtm::normalize(ld3(cam.look) + x * ld3(cam.u) + y * ld3(cam.v));
+        dvec3 rp = eye, rd = cdir;
+        if (LR.camk() == 0) {
+          LR.first_query() = LR.rec_on() && LR.pass() == 0;
+          if (LR.first_query()) {  // default record: miss (also what depth < 0 leaves)
+            RtxHitRecord* hr = &hits[LR.sample_slot()];
+            hr->object = hr->face = hr->scene_leaf = hr->mesh_leaf = -1;
+            hr->t = 1000.0;
+            hr->pad = 0;
+          }
+        } else {
+          const double fd = rtm::gmax(P.dof_fd, 1.0);
+          const dvec3 fp_n = -cdir;
+          const dvec3 fp_pt = rtm::ray_at(eye, cdir, fd);
+          double t = rtm::dot(fp_n, cdir);
+          t = rtm::dot(fp_pt - eye, fp_n) / t;
+          const dvec3 dest = rtm::ray_at(eye, cdir, t);
+          rp = eye + ld3(&F.offv[(LR.camk() - 1) * 3]);
+          rd = rtm::normalize(dest - rp);
+          LR.first_query() = false;
+        }
+        LR.camk()++;
+        if (STATS) C.camera++;
+        LR.top() = 0;
+        push(rp, rd, mk3(1, 1, 1), mk3(1, 1, 1), P.depth, 0, F.fork_on ? 1 : 0);
+        LR.st() = ST_POP;
+        break;
+      }
+      case ST_POP: {
+        if (LR.top() == 0) {
+          LR.st() = ST_CAM;
+          break;
+        }
+        const double* b = pbuf + static_cast<size_t>(LR.top() - 1) * 13 * nlanes + LR.g;
+        const int64_t code = static_cast<int64_t>(b[12 * nlanes]);
+        const int dk = static_cast<int>((code & ((int64_t(1) << 40) - 1)) - (int64_t(1) << 39));
+        const int pdepth = dk >= 0 ? dk / 4 : -((-dk + 3) / 4);
+        if (pdepth < 0) {  // `depth >= 0 &&` (RayTracer.cpp:116): no query, the miss colour
+          if (S.cube[0] >= 0) {
+            if (LR.wmask()) {
+              LR.qmode() = Q_WAIT;
+              break;
+            }
+            contrib_at(LR, F, static_cast<int>(code >> 40),
+                       mk3(b[6 * nlanes], b[7 * nlanes], b[8 * nlanes]) *
+                           cube_color(S, mk3(b[3 * nlanes], b[4 * nlanes], b[5 * nlanes])));
+          }
+          --LR.top();
+          LR.nrays()++;
+          break;
+        }
+        --LR.top();
+        LR.nrays()++;
+        LR.qmode() = Q_CLOSEST;  // the ray stays in entry `top` until its hit is shaded
+        LR.st() = ST_HIT;
+        break;
+      }
+      case ST_HIT: {
+        // traceRay after scene->intersect (RayTracer.cpp:116-165) + shade
+        const double* b = pbuf + static_cast<size_t>(LR.top()) * 13 * nlanes + LR.g;
+        const dvec3 rp = mk3(b[0 * nlanes], b[1 * nlanes], b[2 * nlanes]);
+        const dvec3 rd = mk3(b[3 * nlanes], b[4 * nlanes], b[5 * nlanes]);
+        dvec3 W = mk3(b[6 * nlanes], b[7 * nlanes], b[8 * nlanes]);
+        const int64_t code = static_cast<int64_t>(b[12 * nlanes]);
+        const int dk = static_cast<int>((code & ((int64_t(1) << 40) - 1)) - (int64_t(1) << 39));
+        const int pos = static_cast<int>(code >> 40);
+        const int rdepth = dk >= 0 ? dk / 4 : -((-dk + 3) / 4);
+        const int rkind = dk - rdepth * 4;
+        const double bt = LR.bt();
+        const int bobj = LR.bobj(), bsub = LR.bsub();
+        if (LR.first_query()) {
+          LR.first_query() = false;
+          if (LR.bhave()) {
+            RtxHitRecord* hr = &hits[LR.sample_slot()];
+            const RtxObject& o = S.objs[bobj];
+            hr->object = o.orig_id;
+            hr->scene_leaf = o.leaf;
+            hr->t = bt;
+            if (o.type == RTX_OBJ_TRIMESH) {
+              const RtxMesh me = S.meshes[o.mesh];
+              const RtxFaceIds fi = S.fids[me.face_off + bsub];
+              hr->face = fi.orig_id;
+              hr->mesh_leaf = fi.leaf;
+            }
+          }
+        }
+        LR.st() = ST_POP;
+        if (!LR.bhave()) {  // miss: the cube map's colour, else black (RayTracer.cpp:167-169; U3)
+          if (S.cube[0] >= 0) contrib_at(LR, F, pos, W * cube_color(S, rd));
+          break;
+        }
+        if (rkind != 0) {  // the parked kt factor of a child ray (RayTracer.cpp:140-158)
+          const dvec3 ktf = mk3(b[9 * nlanes], b[10 * nlanes], b[11 * nlanes]);
+          if (rkind == 1)
+            W = W * rtm::gmax3(rtm::gmin3(rtm::pow3(ktf, bt), rtm::splat3(1.0)), rtm::splat3(0.0));
+          else
+            W = W * rtm::pow3(ktf, bt);
+        }
+        const HitRef R = resolve_hit(S, rp, rd, bobj, bsub, nullptr, nullptr);
+        const dvec3 N = R.N;
+        const int flags = hit_flags(S, R);
+        if (STATS) C.shades++;
+        // Material::shade (material.cpp:34-69)
+        dvec3 i_out = hit_param(S, R, RTX_P_KE) + hit_param(S, R, RTX_P_KA) * mk3(S.ambient[0], S.ambient[1], S.ambient[2]);
+        {
+          const dvec3 kd = hit_param(S, R, RTX_P_KD), ks = hit_param(S, R, RTX_P_KS);
+          const double sh = hit_shininess(S, R);
+          const dvec3 X = rtm::ray_at(rp, rd, bt);
+          const dvec3 pb = X - rd * RTX_EPS_BACKUP;
+          unsigned int wm = 0;
+          for (int li = 0; li < S.n_lights; ++li) {
+            const RtxLight& L = S.lights[li];
+            const dvec3 l_i = light_dir(L, X);
+            const dvec3 l_r = (l_i - 2 * (rtm::dot(l_i, N)) * N);
+            double dt = rtm::dot(l_i, N);
+            if (flags & RTX_MF_TRANS) dt = fabs(dt);
+            const dvec3 d_comp = kd * rtm::gmax(0.0, dt);
+            const dvec3 s_comp = ks * rtm::splat3(rtm::rpow(rtm::gmax(0.0, rtm::dot(l_r, rd)), sh));
+            const dvec3 dscomp = d_comp + s_comp;
+            const double dattn = light_dist_atten(L, X);
+            if (STATS) C.shadow++;
+            LR.nrays()++;
+            // a zero colour factor with finite attenuations adds +0 (DESIGN.md:
+            // dark lights are counted, not traced)
+            const bool on = !(S.skip_dark && dscomp.x == 0.0 && dscomp.y == 0.0 && dscomp.z == 0.0);
+            const dvec3 sdir = light_dir(L, pb);
+            if (INLINE) {
+              if (on) {
+                const dvec3 res = walk_inline<STATS>(S, L, pb, sdir, stk, lane, C);
+                i_out += dattn * res * ld3(L.color) * dscomp;
+              }
+            } else {
+              double qlim, qblk;
+              shadow_bounds(S, L, pb, true, qlim, qblk);
+              emit_walk(*we, on, static_cast<int>(LR.g), li, pb, sdir, qlim, qblk, dattn, dscomp);
+              if (on) wm |= 1u << li;
+            }
+          }
+          if (wm == 0) {
+            contrib_at(LR, F, pos, W * i_out);
+          } else {  // colorC = W * shade(...) once the terms are in (flush_terms)
+            LR.W() = W;
+            LR.i_out() = i_out;
+            LR.wmask() = static_cast<int>(wm);
+            LR.rpos() = pos;
+          }
+        }
+        // recursion (RayTracer.cpp:127-164), m_out = air; no adaptive
+        // termination on this path, so it does not wait for the colour
+        const int depth = rdepth - 1;
+        if (!((flags & RTX_MF_RECUR) && depth > 0)) break;
+        const bool leaving = rtm::dot(N, rd) >= 0;
+        const bool next_trans = leaving ? true : (flags & RTX_MF_TRANS) != 0;
+        const dvec3 normal = (leaving ? -1.0 : 1.0) * N;
+        const double c = -1 * rtm::dot(normal, rd);
+        const double eta =
+            next_trans ? (leaving ? hit_index(S, R) : S.air_index) / (leaving ? S.air_index : hit_index(S, R)) : 0;
+        const double radicand = 1 - eta * eta * (1 - c * c);
+        const bool tir = next_trans && radicand < 0;
+        // buckets of the children: their own heap positions when they are
+        // nodes (this ray is a node above the fork depth), else this ray's
+        const bool node = pos > 0 && P.depth - rdepth == ilog2i(pos);
+        const int node_refl = node && 2 * pos < F.fork_npos + 2 ? 2 * pos : 0;
+        const int node_refr = node && 2 * pos + 1 < F.fork_npos + 2 ? 2 * pos + 1 : 0;
+        // push refraction first so that reflection is traced first (the
+        // entry at `top` is this ray's own, read above: it is overwritten)
+        if (next_trans && !tir && LR.top() < pend_cap) {
+          const dvec3 tp = rtm::ray_at(rp, rd, bt + RTX_RAY_EPS);
+          const dvec3 td = eta * rd + (eta * c - sqrt(radicand)) * normal;
+          const dvec3 kf = leaving ? mk3(1.0, 1.0, 1.0) : hit_param(S, R, RTX_P_KT);
+          if (!fork_child(tp, td, W, kf, depth, 2, node_refr)) push(tp, td, W, kf, depth, 2, node_refr ? node_refr : pos);
+          if (STATS) C.secondary++;
+        }
+        if (((flags & RTX_MF_REFL) || tir) && LR.top() < pend_cap) {
+          const dvec3 rdir = rd + 2 * c * normal;
+          const dvec3 rs = rtm::ray_at(rp, rd, bt - RTX_RAY_EPS);
+          const dvec3 wr = W * hit_param(S, R, RTX_P_KR);
+          const dvec3 kf = leaving ? hit_param(S, R, RTX_P_KT) : mk3(1.0, 1.0, 1.0);
+          if (!fork_child(rs, rdir, wr, kf, depth, 1, node_refl)) push(rs, rdir, wr, kf, depth, 1, node_refl ? node_refl : pos);
+          if (STATS) C.secondary++;
+        }
+        break;
+      }
+      default:
+        LR.st() = ST_IDLE;
+        break;
+    }
+  }
+}
+
+// One step of every live slot of a group on a fused frame: add the last
+// hit's colour, then run the machine to the next closest query (appended to
+// q0 with ballot + popc + mbcnt, the ray read from the slot's pending stack)
+// while walks go to q1 as they are found.
+template <bool STATS, bool FORK>
+__global__ void __launch_bounds__(WG, RTX_ADV_WAVES)
+    advance_fused_kernel(DevScene S, const DevScene* __restrict__ Sg, const FrameParams* __restrict__ Fp, LaneMem lm,
+                         double* __restrict__ sbuf, RtxHitRecord* __restrict__ hits, double* __restrict__ pbuf,
+                         int pend_cap, QList q0, QList q1, unsigned int* __restrict__ counters,
+                         unsigned long long* __restrict__ stats, int slot_off, const int* __restrict__ live_in,
+                         int* __restrict__ live_out, int first, int in_cnt, int out_cnt) {
+  const FrameParams& F = *Fp;
+  const int tid = blockIdx.x * WG + threadIdx.x;
+  const bool valid = first || tid < static_cast<int>(counters[in_cnt]);
+  const int slot = first ? slot_off + tid : (valid ? live_in[tid] : slot_off);
+  const int lane = threadIdx.x & 63;
+  Counters C = {0, 0, 0, 0, 0, 0, 0};
+  LaneRef L(lm, static_cast<size_t>(slot));
+  int qm = Q_NONE;
+  const ForkCtx fk = {counters + CNT_FORK, slot_off + F.wf_gsamp,
+                      first ? 0u : static_cast<unsigned int>(F.wf_gs - F.wf_gsamp), live_out, counters + out_cnt};
+  const WalkEmit we = {q1, counters + CNT_Q + CNT_LINE};
+  if (valid && (L.st() != ST_IDLE || slot_unit(F, slot, L.kdone()) >= 0)) {
+    flush_terms(L, F);
+    L.qmode() = Q_NONE;
+    for (;;) {
+      claim_sample(L, F, hits, slot);
+      if (L.st() == ST_IDLE) break;
+      advance_fused<STATS, false, FORK>(L, *Sg, F, C, sbuf, hits, pbuf, lm.n, pend_cap, &fk, &we, nullptr, lane);
+      if (L.qmode() != Q_NONE) break;
+    }
+    qm = L.qmode();
+  }
+  const unsigned long long mask = __ballot(qm == Q_CLOSEST);
+  if (mask) {
+    unsigned int base = 0;
+    if (lane == 0) base = atomicAdd(&counters[CNT_Q], static_cast<unsigned int>(__popcll(mask)));
+    base = __shfl(base, 0);
+    if (qm == Q_CLOSEST) {
+      const size_t cap = q0.cap, n = lm.n;
+      const size_t k = base + lane_prefix(mask);
+      const double* b = pbuf + static_cast<size_t>(L.top()) * 13 * n + slot;
+      q0.slot[k] = slot;
+      q0.d[0 * cap + k] = b[0 * n];
+      q0.d[1 * cap + k] = b[1 * n];
+      q0.d[2 * cap + k] = b[2 * n];
+      q0.d[3 * cap + k] = b[3 * n];
+      q0.d[4 * cap + k] = b[4 * n];
+      q0.d[5 * cap + k] = b[5 * n];
+      q0.d[6 * cap + k] = -RTX_INF;
+      q0.d[7 * cap + k] = RTX_INF;
+      q0.d[8 * cap + k] = -RTX_INF;
+      q0.iv[0 * cap + k] = -1;
+      q0.iv[1 * cap + k] = -1;
+    }
+  }
+  const bool live = valid && L.st() != ST_IDLE;  // a query pending or waiting for terms
+  const unsigned long long alive = __ballot(live);
+  if (alive) {
+    unsigned int base = 0;
+    if (lane == 0) base = atomicAdd(&counters[out_cnt], static_cast<unsigned int>(__popcll(alive)));
+    base = __shfl(base, 0);
+    if (live) live_out[base + lane_prefix(alive)] = slot;
+  }
+  if (STATS) {
+    int64_t v[7] = {C.camera, C.secondary, C.shadow, C.nodes, C.objects, C.tris, C.shades};
+#pragma unroll
+    for (int k = 0; k < 7; ++k) {
+      int64_t x = v[k];
+      for (int off = 32; off > 0; off >>= 1) x += __shfl_down(x, off);
+      if (lane == 0 && x) atomicAdd(&stats[k], static_cast<unsigned long long>(x));
+    }
+  }
+}
+
+// Tail of a fused frame (see tail_kernel): each slot runs its own chain,
+// walks inline.
+template <bool STATS>
+__global__ void __launch_bounds__(WG) tail_fused_kernel(DevScene S, const DevScene* __restrict__ Sg,
+                                                         const FrameParams* __restrict__ Fp, LaneMem lm,
+                                                         double* __restrict__ sbuf, RtxHitRecord* __restrict__ hits,
+                                                         double* __restrict__ pbuf, int pend_cap,
+                                                         const unsigned int* __restrict__ counters,
+                                                         const int* __restrict__ live_in, int in_cnt, int stack_cap,
+                                                         unsigned long long* __restrict__ stats) {
+  extern __shared__ int lds_stack[];
+  const FrameParams& F = *Fp;
+  const int lane = threadIdx.x & 63;
+  int* stk = lds_stack + (threadIdx.x >> 6) * stack_cap * 64;
+  const int tid = blockIdx.x * WG + threadIdx.x;
+  Counters C = {0, 0, 0, 0, 0, 0, 0};
+  const bool valid = tid < static_cast<int>(counters[in_cnt]);
+  const int slot = valid ? live_in[tid] : 0;
+  LaneRef L(lm, static_cast<size_t>(slot));
+  if (valid) {
+    flush_terms(L, F);
+    for (;;) {
+      L.qmode() = Q_NONE;
+      claim_sample(L, F, hits, slot);
+      if (L.st() == ST_IDLE) break;
+      advance_fused<STATS, true, false>(L, *Sg, F, C, sbuf, hits, pbuf, lm.n, pend_cap, nullptr, nullptr, stk, lane);
+      if (L.qmode() != Q_CLOSEST) continue;
+      const double* b = pbuf + static_cast<size_t>(L.top()) * 13 * lm.n + slot;
+      const dvec3 qP = mk3(b[0 * lm.n], b[1 * lm.n], b[2 * lm.n]);
+      const dvec3 qD = mk3(b[3 * lm.n], b[4 * lm.n], b[5 * lm.n]);
+      double bt;
+      int bobj, bsub;
+      const bool have = traverse<STATS>(S, Q_CLOSEST, qP, qD, -RTX_INF, -1, -1, RTX_INF, bt, bobj, bsub, stk, lane, C);
+      L.bt() = bt;
+      L.bobj() = bobj;
+      L.bsub() = bsub;
+      L.bhave() = have ? 1 : 0;
+    }
+  }
+  if (STATS) {
+    int64_t v[7] = {C.camera, C.secondary, C.shadow, C.nodes, C.objects, C.tris, C.shades};
+#pragma unroll
+    for (int k = 0; k < 7; ++k) {
+      int64_t x = v[k];
+      for (int off = 32; off > 0; off >>= 1) x += __shfl_down(x, off);
+      if (lane == 0 && x) atomicAdd(&stats[k], static_cast<unsigned long long>(x));
+    }
+  }
+}

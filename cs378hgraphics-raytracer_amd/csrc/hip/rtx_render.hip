@@ -93,6 +93,10 @@ struct FrameParams {
   int fork_on, fork_npos;
   double* fbuf;
   unsigned int* fmask;
+  // fused shadow walks (rtx_fused.h): the finished terms of the walks,
+  // wterm[(light * nslot + slot) * 3 + c]
+  int fuse;
+  double* wterm;
 };
 
 // Tile deal: deal index d = shard + k * nshards is tile row d / tiles_x,
@@ -357,7 +361,7 @@ struct Pending {
 // with it.  LaneRef gives a lane's fields as accessors (LR.st(), LR.acc(), ...).
 #define LANE_INT_FIELDS(X) X(st) X(sample_slot) X(rec_on) X(pass) X(camk) X(nrays) X(top) X(rdepth) X(rkind) \
   X(first_query) X(cam_end) X(sobj) X(ssub) X(m_flags) X(li) X(pick) X(qmode) X(qrp) X(qsq) X(kdone) X(bobj) X(bsub) X(bhave) \
-  X(dret) X(dpass) X(dpush) X(dhead) X(dtot) X(dlast) X(dopq) X(mo_trans) X(wobj) X(wsub) X(fpos) X(rpos)
+  X(dret) X(dpass) X(dpush) X(dhead) X(dtot) X(dlast) X(dopq) X(mo_trans) X(wobj) X(wsub) X(fpos) X(rpos) X(wmask)
 #define LANE_DBL_FIELDS(X) X(sx) X(sy) X(st_t) X(m_sh) X(dattn) X(last_t) X(qtp) X(bt) X(mo_idx) X(wt) X(wtr)
 #define LANE_VEC_FIELDS(X) X(acc) X(rp) X(rd) X(W) X(N) X(i_out) X(dscomp) X(m_kd) X(m_ks) X(area_sum) X(sdir) \
   X(wpos) X(sattn) X(dpos) X(ddir) X(dkt) X(didx) X(mo_kt)
@@ -1475,6 +1479,8 @@ __device__ __forceinline__ void claim_sample(LaneRef& L, const FrameParams& F, R
   }
 }
 
+#include "rtx_fused.h"
+
 template <bool STATS, bool MEDIA, bool FORK>
 __global__ void __launch_bounds__(WG, RTX_ADV_WAVES) advance_kernel(DevScene S, const DevScene* __restrict__ Sg, const FrameParams* __restrict__ Fp, LaneMem lm,
                                                       double* __restrict__ sbuf, RtxHitRecord* __restrict__ hits,
@@ -1733,10 +1739,14 @@ struct ShadowBlocker {
 // 64 queries at a time (one atomic); lanes whose query ended take the next
 // ones of the claim (ballot + mbcnt) once fewer than RTX_REFILL lanes are
 // still stepping.
-template <bool STATS, int MODE>
+// FUSED (Q_NEXT on fused frames, rtx_fused.h): the list holds walk records;
+// a lane whose query completes runs the walk's next step (walk_hit) and
+// either queries again from the hit's key or writes the light's term to
+// wterm[light][slot].
+template <bool STATS, int MODE, bool FUSED = false>
 __global__ void __launch_bounds__(WG, RTX_TRACE_WAVES)
     trace_kernel(DevScene S, const DevScene* __restrict__ Sg, QList Q, unsigned int* __restrict__ counters,
-                 LaneMem lm, int stack_cap, unsigned long long* __restrict__ stats) {
+                 LaneMem lm, int stack_cap, unsigned long long* __restrict__ stats, double* __restrict__ wterm) {
   extern __shared__ int lds_stack[];
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
@@ -1789,7 +1799,56 @@ __global__ void __launch_bounds__(WG, RTX_TRACE_WAVES)
     lm.i[size_t(LI_bsub) * lm.n + slot] = T.bsub;
     lm.i[size_t(LI_bhave) * lm.n + slot] = T.blocked ? 2 : (T.have ? 1 : 0);
   };
+  bool pend = false;  // FUSED: the lane's walk query completed, its walk step is due
+  // FUSED: the walk step of a completed query — the next query of the walk
+  // (its record keeps the walk's state and the new key) or the light's term
+  auto walk_phase = [&]() {
+    while (pend) {
+      const size_t k = kq;
+      const int li = Q.iv[2 * cap + k];
+      const RtxLight& L = S.lights[li];
+      const dvec3 pb = mk3(Q.d[QF_PX * cap + k], Q.d[QF_PY * cap + k], Q.d[QF_PZ * cap + k]);
+      const dvec3 sdir = mk3(Q.d[QF_DX * cap + k], Q.d[QF_DY * cap + k], Q.d[QF_DZ * cap + k]);
+      WalkState w;
+      if (Q.iv[0 * cap + k] < 0) {  // the walk's first hit (light.cpp:28-29)
+        w.wpos = pb;
+        w.sattn = mk3(1.0, 1.0, 1.0);
+        w.last_t = 0.0;
+      } else {
+        w.wpos = mk3(Q.d[QF_WPX * cap + k], Q.d[QF_WPY * cap + k], Q.d[QF_WPZ * cap + k]);
+        w.sattn = mk3(Q.d[QF_SAX * cap + k], Q.d[QF_SAY * cap + k], Q.d[QF_SAZ * cap + k]);
+        w.last_t = Q.d[QF_LAST * cap + k];
+      }
+      const double bt = T.bt;
+      const int bo = T.bobj, bs = T.bsub;
+      dvec3 res;
+      if (walk_hit(S, L, pb, sdir, T.have, bt, bo, bs, w, res)) {
+        const size_t slot = static_cast<size_t>(Q.slot[k]);
+        const dvec3 dsc = mk3(Q.d[QF_SCX * cap + k], Q.d[QF_SCY * cap + k], Q.d[QF_SCZ * cap + k]);
+        const dvec3 term = Q.d[QF_DATTN * cap + k] * res * ld3(L.color) * dsc;
+        double* o = wterm + (static_cast<size_t>(li) * lm.n + slot) * 3;
+        o[0] = term.x;
+        o[1] = term.y;
+        o[2] = term.z;
+        pend = false;
+      } else {
+        Q.d[QF_WPX * cap + k] = w.wpos.x;
+        Q.d[QF_WPY * cap + k] = w.wpos.y;
+        Q.d[QF_WPZ * cap + k] = w.wpos.z;
+        Q.d[QF_SAX * cap + k] = w.sattn.x;
+        Q.d[QF_SAY * cap + k] = w.sattn.y;
+        Q.d[QF_SAZ * cap + k] = w.sattn.z;
+        Q.d[QF_LAST * cap + k] = w.last_t;
+        Q.iv[0 * cap + k] = bo;
+        double qlim, qblk;
+        shadow_bounds(S, L, pb, false, qlim, qblk);
+        active = trav_init<STATS, MODE>(T, S, pb, sdir, bt, bo, bs, qlim, qblk, C);
+        pend = !active;  // answered by the root test: the walk's next step
+      }
+    }
+  };
   for (;;) {
+    if (FUSED) walk_phase();
     unsigned long long idle = __ballot(!active);
     while (idle != 0ull && !exhausted) {
       if (qnext >= qend) {
@@ -1808,18 +1867,21 @@ __global__ void __launch_bounds__(WG, RTX_TRACE_WAVES)
       const unsigned int avail = qend - qnext;
       const unsigned int nidle = __popcll(idle);
       const unsigned int take = avail < nidle ? avail : nidle;
-      if (!active && rank < take) {
+      if (!active && !pend && rank < take) {
         kq = static_cast<size_t>(qnext) + rank;
         const dvec3 P = mk3(Q.d[0 * cap + kq], Q.d[1 * cap + kq], Q.d[2 * cap + kq]);
         const dvec3 D = mk3(Q.d[3 * cap + kq], Q.d[4 * cap + kq], Q.d[5 * cap + kq]);
         active = trav_init<STATS, MODE>(T, S, P, D, Q.d[6 * cap + kq], Q.iv[0 * cap + kq], Q.iv[1 * cap + kq],
                                   Q.d[7 * cap + kq], MODE == Q_NEXT ? Q.d[8 * cap + kq] : -RTX_INF, C);
-        if (!active) finish();
+        if (!active) {
+          if (FUSED) pend = true;
+          else finish();
+        }
       }
       qnext += take;
-      idle = __ballot(!active);
+      idle = __ballot(!active && !pend);
     }
-    if (__ballot(active) == 0ull) break;  // nothing claimed and nothing left
+    if (__ballot(active || pend) == 0ull) break;  // nothing claimed and nothing left
     const int thresh = exhausted ? 1 : RTX_REFILL;
     do {
       if (STATS) {  // SIMD efficiency of the walk (RTX_DEBUG report)
@@ -1829,7 +1891,8 @@ __global__ void __launch_bounds__(WG, RTX_TRACE_WAVES)
       if (active) {
         if (STATS) qsteps++;
         if (trav_step<STATS, MODE>(T, S, stk, lane, blk, C)) {
-          finish();
+          if (FUSED) pend = true;
+          else finish();
           active = false;
           if (STATS) {  // per-query step statistics (RTX_DEBUG report)
             atomicMax(&stats[12 + (MODE - 1)], static_cast<unsigned long long>(qsteps));
@@ -1962,6 +2025,8 @@ struct SceneState {
   size_t fbuf_bytes = 0;
   unsigned int* d_fmask = nullptr;  // forked positions per sample
   size_t fmask_bytes = 0;
+  double* d_wterm = nullptr;    // fused walks' terms [light][slot][3]
+  size_t wterm_bytes = 0;
   // wavefront path: slot state, query lists, counters
   void* d_wf = nullptr;
   size_t wf_bytes = 0;
@@ -2202,6 +2267,7 @@ rtx_status rtx_scene_destroy(void* scene) {
   if (st->d_pbuf) (void)hipFree(st->d_pbuf);
   if (st->d_fbuf) (void)hipFree(st->d_fbuf);
   if (st->d_fmask) (void)hipFree(st->d_fmask);
+  if (st->d_wterm) (void)hipFree(st->d_wterm);
   if (st->d_wf) (void)hipFree(st->d_wf);
   if (st->d_lane) (void)hipFree(st->d_lane);
   for (auto e : st->wf_join) (void)hipEventDestroy(e);
@@ -2523,14 +2589,28 @@ rtx_status rtx_render(void* scene, const RtxRenderParams* params, uint8_t* rgb8,
     const char* fd_env = getenv("RTX_FORK_DEPTH");
     if (fd_env && atoi(fd_env) > 0) fork_depth = std::min(4, atoi(fd_env));
     bool fork_ok = !(fork_env && atoi(fork_env) == 0) && !F.cam_split && !params->dof && !params->anaglyph;
-    const size_t per_slot = lane_mem_bytes(1) + size_t(pend_cap) * 13 * sizeof(double) +
-                            2 * (3 * sizeof(int) + QL_D * sizeof(double)) + 2 * sizeof(int);
+    // fused shadow walks (rtx_fused.h): every light a point or directional
+    // light, no overlapping media, no adaptive termination (RTX_FUSE=0: the
+    // sequential machine)
+    const char* fuse_env = getenv("RTX_FUSE");
+    bool fuse = !(fuse_env && atoi(fuse_env) == 0) && !media && !(params->aterm_thresh > 0.0) &&
+                st->lights.size() <= 8;
+    for (const auto& L : st->lights) fuse &= L.type == RTX_LIGHT_POINT || L.type == RTX_LIGHT_DIRECTIONAL;
+    const size_t nl = fuse ? st->lights.size() : 0;
+    // query records: closest (slot, 9 doubles, 2 ints); next: one per slot,
+    // or one per light and slot with fused walks (slot, QF_D doubles, 3 ints)
+    const size_t rec_c = sizeof(int) + QL_D * sizeof(double) + 2 * sizeof(int);
+    const size_t rec_n = fuse ? sizeof(int) + QF_D * sizeof(double) + QF_I * sizeof(int) : rec_c;
+    const size_t nrec_n = fuse ? std::max<size_t>(1, nl) : 1;
+    const size_t per_slot = lane_mem_bytes(1) + size_t(pend_cap) * 13 * sizeof(double) + rec_c + nrec_n * rec_n +
+                            2 * sizeof(int) + nl * 3 * sizeof(double);
     {
       // memory budget: what the device has free plus the frame buffers this
       // scene already holds (they are reused or replaced), less a reserve
       size_t freeb = 0, totb = 0;
       HIP_TRY(hipMemGetInfo(&freeb, &totb));
-      const size_t held = st->lane_bytes + st->pbuf_bytes + st->wf_bytes + st->fbuf_bytes + st->fmask_bytes;
+      const size_t held =
+          st->lane_bytes + st->pbuf_bytes + st->wf_bytes + st->fbuf_bytes + st->fmask_bytes + st->wterm_bytes;
       const size_t sbuf_need = size_t(npix) * F.spp * 3 * sizeof(double);
       const size_t avail = freeb + held > sbuf_need ? (freeb + held - sbuf_need) / 10 * 8 : 0;
       const size_t npos = (size_t(1) << (fork_depth + 1)) - 2;
@@ -2579,11 +2659,23 @@ rtx_status rtx_render(void* scene, const RtxRenderParams* params, uint8_t* rgb8,
     }
     const size_t ns = static_cast<size_t>(nslot64);
     const size_t gs = static_cast<size_t>(gslots);
-    const size_t bytes_q = gs * (sizeof(int) + QL_D * sizeof(double) + 2 * sizeof(int)) + 1024;
     auto al = [](size_t x) { return (x + 255) & ~size_t(255); };
-    // per group: two query lists, then two live-slot lists (ping-pong)
-    if ((rc = ensure(&st->d_wf, &st->wf_bytes, size_t(G) * (2 * al(bytes_q) + 2 * al(gs * sizeof(int))))) != RTX_OK)
+    // per group: the closest and the next query list, then two live-slot
+    // lists (ping-pong)
+    const size_t capn = gs * nrec_n;
+    const size_t bytes_qc = al(gs * sizeof(int)) + al(gs * QL_D * sizeof(double)) + al(gs * 2 * sizeof(int));
+    const size_t nd = fuse ? QF_D : QL_D, ni = fuse ? QF_I : 2;
+    const size_t bytes_qn = al(capn * sizeof(int)) + al(capn * nd * sizeof(double)) + al(capn * ni * sizeof(int));
+    if ((rc = ensure(&st->d_wf, &st->wf_bytes, size_t(G) * (bytes_qc + bytes_qn + 2 * al(gs * sizeof(int))))) != RTX_OK)
       return rc;
+    F.fuse = fuse ? 1 : 0;
+    F.wterm = nullptr;
+    if (fuse && nl > 0) {
+      if ((rc = ensure(reinterpret_cast<void**>(&st->d_wterm), &st->wterm_bytes, nl * ns * 3 * sizeof(double))) !=
+          RTX_OK)
+        return rc;
+      F.wterm = st->d_wterm;
+    }
     if ((rc = ensure(&st->d_lane, &st->lane_bytes, lane_mem_bytes(ns))) != RTX_OK) return rc;
     const LaneMem A = lane_mem_at(st->d_lane, ns);
     if ((rc = ensure(reinterpret_cast<void**>(&st->d_pbuf), &st->pbuf_bytes,
@@ -2609,16 +2701,17 @@ rtx_status rtx_render(void* scene, const RtxRenderParams* params, uint8_t* rgb8,
     {
       char* base = static_cast<char*>(st->d_wf);
       for (size_t m = 0; m < ql.size(); ++m) {
+        const size_t cap = (m & 1) ? capn : gs, dn = (m & 1) ? nd : QL_D;
         ql[m].slot = reinterpret_cast<int*>(base);
-        ql[m].d = reinterpret_cast<double*>(base + al(gs * sizeof(int)));
-        ql[m].iv = reinterpret_cast<int*>(base + al(gs * sizeof(int)) + al(gs * QL_D * sizeof(double)));
-        ql[m].cap = gs;
-        base += al(bytes_q);
+        ql[m].d = reinterpret_cast<double*>(base + al(cap * sizeof(int)));
+        ql[m].iv = reinterpret_cast<int*>(base + al(cap * sizeof(int)) + al(cap * dn * sizeof(double)));
+        ql[m].cap = cap;
+        base += (m & 1) ? bytes_qn : bytes_qc;
       }
     }
     std::vector<int*> live(size_t(G) * 2);  // [g * 2 + 0]: list A, [g * 2 + 1]: list B
     {
-      char* base = static_cast<char*>(st->d_wf) + size_t(G) * 2 * al(bytes_q);
+      char* base = static_cast<char*>(st->d_wf) + size_t(G) * (bytes_qc + bytes_qn);
       for (size_t k = 0; k < live.size(); ++k) {
         live[k] = reinterpret_cast<int*>(base);
         base += al(gs * sizeof(int));
@@ -2640,7 +2733,7 @@ rtx_status rtx_render(void* scene, const RtxRenderParams* params, uint8_t* rgb8,
     HIP_TRY(hipMemcpyAsync(st->d_frame, &F, sizeof(FrameParams), hipMemcpyHostToDevice, stream));
     // every slot ST_IDLE, kdone = 0, outside a discoverMat walk (every other
     // field is written before it is read; the int rows are field-major)
-    for (int f : {int(LI_st), int(LI_kdone), int(LI_dret)})
+    for (int f : {int(LI_st), int(LI_kdone), int(LI_dret), int(LI_wmask)})
       HIP_TRY(hipMemsetAsync(A.i + size_t(f) * ns, 0, ns * sizeof(int), stream));
     HIP_TRY(hipMemsetAsync(st->d_counters, 0, 16 * CNT_PER_GROUP * sizeof(unsigned int), stream));
     const size_t lds_stacks = size_t(st->stack_cap) * 64 * sizeof(int) * WAVES_PER_WG;
@@ -2684,11 +2777,20 @@ rtx_status rtx_render(void* scene, const RtxRenderParams* params, uint8_t* rgb8,
           const int* live_in = live[size_t(g) * 2 + (odd ? 0 : 1)];
           const int64_t lb = grid_bound[size_t(g)];
           const int64_t grid = std::max<int64_t>(1, (lb + WG - 1) / WG);
-          dispatch2(stats, media, [&](auto st_, auto md_) {
-            hipLaunchKernelGGL((tail_kernel<decltype(st_)::value, decltype(md_)::value>), dim3(grid), dim3(WG), lds, sg,
-                               S, st->d_scene, st->d_frame, A, sb, d_hits, st->d_pbuf, pend_cap, cnt, live_in, in_cnt,
-                               st->stack_cap, st->d_stats);
-          });
+          if (fuse) {
+            if (stats)
+              hipLaunchKernelGGL((tail_fused_kernel<true>), dim3(grid), dim3(WG), lds, sg, S, st->d_scene, st->d_frame,
+                                 A, sb, d_hits, st->d_pbuf, pend_cap, cnt, live_in, in_cnt, st->stack_cap, st->d_stats);
+            else
+              hipLaunchKernelGGL((tail_fused_kernel<false>), dim3(grid), dim3(WG), lds, sg, S, st->d_scene, st->d_frame,
+                                 A, sb, d_hits, st->d_pbuf, pend_cap, cnt, live_in, in_cnt, st->stack_cap, st->d_stats);
+          } else {
+            dispatch2(stats, media, [&](auto st_, auto md_) {
+              hipLaunchKernelGGL((tail_kernel<decltype(st_)::value, decltype(md_)::value>), dim3(grid), dim3(WG), lds,
+                                 sg, S, st->d_scene, st->d_frame, A, sb, d_hits, st->d_pbuf, pend_cap, cnt, live_in,
+                                 in_cnt, st->stack_cap, st->d_stats);
+            });
+          }
           HIP_TRY(hipGetLastError());
           done[size_t(g)] = 1;
           ++ndone;
@@ -2705,22 +2807,42 @@ rtx_status rtx_render(void* scene, const RtxRenderParams* params, uint8_t* rgb8,
         const int64_t lb = grid_bound[size_t(g)];
         const int64_t agrid = first ? per : std::max<int64_t>(1, std::min<int64_t>(per, (lb + WG - 1) / WG));
         const int64_t tg = std::max<int64_t>(1, std::min<int64_t>(tgrid, (lb + WG - 1) / WG));
-        dispatch3(stats, media, fork, [&](auto st_, auto md_, auto fk_) {
-          hipLaunchKernelGGL((advance_kernel<decltype(st_)::value, decltype(md_)::value, decltype(fk_)::value>),
-                             dim3(agrid), dim3(WG), 0, sg,
-                             S, st->d_scene, st->d_frame, A, sb, d_hits, st->d_pbuf, pend_cap, q0, q1, cnt,
-                             st->d_stats, static_cast<int>(g * gslots), live_in, live_out, first, in_cnt, out_cnt);
-        });
+        if (fuse) {
+          dispatch2(stats, fork, [&](auto st_, auto fk_) {
+            hipLaunchKernelGGL((advance_fused_kernel<decltype(st_)::value, decltype(fk_)::value>), dim3(agrid),
+                               dim3(WG), 0, sg, S, st->d_scene, st->d_frame, A, sb, d_hits, st->d_pbuf, pend_cap, q0,
+                               q1, cnt, st->d_stats, static_cast<int>(g * gslots), live_in, live_out, first, in_cnt,
+                               out_cnt);
+          });
+        } else {
+          dispatch3(stats, media, fork, [&](auto st_, auto md_, auto fk_) {
+            hipLaunchKernelGGL((advance_kernel<decltype(st_)::value, decltype(md_)::value, decltype(fk_)::value>),
+                               dim3(agrid), dim3(WG), 0, sg,
+                               S, st->d_scene, st->d_frame, A, sb, d_hits, st->d_pbuf, pend_cap, q0, q1, cnt,
+                               st->d_stats, static_cast<int>(g * gslots), live_in, live_out, first, in_cnt, out_cnt);
+          });
+        }
+        // the next-hit grid: fused walks can outnumber the live slots
+        const int64_t tgn = fuse ? std::max<int64_t>(1, std::min<int64_t>(tgrid, (lb * int64_t(nrec_n) + WG - 1) / WG))
+                                 : tg;
         if (stats) {
           hipLaunchKernelGGL((trace_kernel<true, Q_CLOSEST>), dim3(tg), dim3(WG), lds, sg, S, st->d_scene, q0,
-                             cnt, A, st->stack_cap, st->d_stats);
-          hipLaunchKernelGGL((trace_kernel<true, Q_NEXT>), dim3(tg), dim3(WG), lds, sg, S, st->d_scene, q1, cnt,
-                             A, st->stack_cap, st->d_stats);
+                             cnt, A, st->stack_cap, st->d_stats, nullptr);
+          if (fuse)
+            hipLaunchKernelGGL((trace_kernel<true, Q_NEXT, true>), dim3(tgn), dim3(WG), lds, sg, S, st->d_scene, q1,
+                               cnt, A, st->stack_cap, st->d_stats, st->d_wterm);
+          else
+            hipLaunchKernelGGL((trace_kernel<true, Q_NEXT>), dim3(tg), dim3(WG), lds, sg, S, st->d_scene, q1, cnt,
+                               A, st->stack_cap, st->d_stats, nullptr);
         } else {
           hipLaunchKernelGGL((trace_kernel<false, Q_CLOSEST>), dim3(tg), dim3(WG), lds, sg, S, st->d_scene, q0,
-                             cnt, A, st->stack_cap, st->d_stats);
-          hipLaunchKernelGGL((trace_kernel<false, Q_NEXT>), dim3(tg), dim3(WG), lds, sg, S, st->d_scene, q1, cnt,
-                             A, st->stack_cap, st->d_stats);
+                             cnt, A, st->stack_cap, st->d_stats, nullptr);
+          if (fuse)
+            hipLaunchKernelGGL((trace_kernel<false, Q_NEXT, true>), dim3(tgn), dim3(WG), lds, sg, S, st->d_scene, q1,
+                               cnt, A, st->stack_cap, st->d_stats, st->d_wterm);
+          else
+            hipLaunchKernelGGL((trace_kernel<false, Q_NEXT>), dim3(tg), dim3(WG), lds, sg, S, st->d_scene, q1, cnt,
+                               A, st->stack_cap, st->d_stats, nullptr);
         }
         HIP_TRY(hipGetLastError());
         if (it % check_every == check_every - 1) {

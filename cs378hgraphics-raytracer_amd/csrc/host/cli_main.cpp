@@ -5,13 +5,31 @@
 // rtx_host_load (RayTracer::loadScene) -> rtx_scene_create -> rtx_render
 // (traceSetup + traceImage) -> rtx_write_image (writeImage).  There is no CPU
 // fallback: without a gfx950 device the command fails loudly.
+#include <cerrno>
 #include <chrono>
 #include <cstdio>
+#include <cstring>
 #include <vector>
 
 #include "cli_opts.h"
 #include "rtx.h"
 #include "rtx_host.h"
+
+// raw dump of an extension output (--dump-f64 / --dump-hits); false after
+// printing why it could not be written
+static bool dump_raw(const std::string& path, const void* data, size_t elem, size_t n) {
+  FILE* f = std::fopen(path.c_str(), "wb");
+  if (!f) {
+    std::cerr << "cannot open '" << path << "' for writing: " << std::strerror(errno) << std::endl;
+    return false;
+  }
+  const bool ok = std::fwrite(data, elem, n, f) == n;
+  if (std::fclose(f) != 0 || !ok) {
+    std::cerr << "write to '" << path << "' failed" << std::endl;
+    return false;
+  }
+  return true;
+}
 
 int main(int argc, char** argv) {
   rtxh::CliOptions o;
@@ -60,16 +78,8 @@ int main(int argc, char** argv) {
     std::cerr << rtx_host_last_error() << std::endl;
     return 1;
   }
-  if (!o.dump_f64.empty()) {
-    FILE* f = std::fopen(o.dump_f64.c_str(), "wb");
-    std::fwrite(f64.data(), sizeof(double), f64.size(), f);
-    std::fclose(f);
-  }
-  if (!o.dump_hits.empty()) {
-    FILE* f = std::fopen(o.dump_hits.c_str(), "wb");
-    std::fwrite(hits.data(), sizeof(RtxHitRecord), hits.size(), f);
-    std::fclose(f);
-  }
+  if (!o.dump_f64.empty() && !dump_raw(o.dump_f64, f64.data(), sizeof(double), f64.size())) rc = 1;
+  if (!o.dump_hits.empty() && !dump_raw(o.dump_hits, hits.data(), sizeof(RtxHitRecord), hits.size())) rc = 1;
   if (o.stats)
     std::printf("{\"backend\": \"hip-gfx950\", \"ms\": %.3f, \"kernel_ms\": %.3f, \"rays\": %lld, "
                 "\"mrays_per_s\": %.3f, \"node_visits\": %lld, \"object_tests\": %lld, \"tri_tests\": %lld, "
@@ -78,5 +88,5 @@ int main(int argc, char** argv) {
                 (long long)st.object_tests, (long long)st.tri_tests, (long long)st.shades);
   rtx_scene_destroy(scene);
   rtx_host_free(hs);
-  return 0;
+  return rc;
 }
