@@ -17,6 +17,7 @@ of the frame's kernels, rtx_kernel_time).  cpu_baseline = the CPU restatement (o
 host's cores over row bands of the same frame.
 """
 import argparse
+import hashlib
 import importlib.util
 import json
 import os
@@ -29,7 +30,9 @@ METRIC = "Mrays/sec + frame ms, trimesh2.ray 1920×1080 depth-5 4×AA; 1/2/4/8 M
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 # algorithmic bytes per unit: ray in + hit out, BVH node, object
 # record, triangle record, material record per shade
-B_RAY, B_NODE, B_OBJ, B_TRI, B_SHADE = 48 + 72, 64, 224, 96, 176
+# (a BVH box test reads one 32-B entry of a 128-B 4-wide float record)
+B_RAY, B_NODE, B_OBJ, B_TRI, B_SHADE = 48 + 72, 32, 224, 96, 176
+LIB = os.path.join(ROOT, "cs378hgraphics-raytracer_amd", "lib", "librtx_hip.so")
 
 
 def load_package():
@@ -49,37 +52,83 @@ def ensure_built(pkg_dir):
         subprocess.run(["make", "-C", pkg_dir, "-j8", "all"], check=True)
 
 
-def cpu_baseline(pkg, path, opts, height, budget_s=15.0):
-    """Time the CPU restatement over row bands of the same frame."""
+def file_sha256(path):
+    h = hashlib.sha256()
+    with open(path, "rb") as f:
+        for blk in iter(lambda: f.read(1 << 20), b""):
+            h.update(blk)
+    return h.hexdigest()
+
+
+def build_id():
+    """git head the libraries were built from (lib/BUILD_ID, written by make)"""
+    p = os.path.join(ROOT, "cs378hgraphics-raytracer_amd", "lib", "BUILD_ID")
+    return open(p).read().strip() if os.path.exists(p) else None
+
+
+def host_cpu():
+    """CPU model, logical CPUs of the host, and the share this job may use
+    (affinity mask, cgroup CPU quota)."""
+    model = None
+    try:
+        for ln in open("/proc/cpuinfo"):
+            if ln.startswith("model name"):
+                model = ln.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    ncpu = os.cpu_count() or 1
+    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else ncpu
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()
+        if q != "max":
+            quota = float(q) / float(per)
+    except (OSError, ValueError):
+        pass
+    share = aff if quota is None else max(1, min(aff, int(quota)))
+    return model, ncpu, aff, quota, share
+
+
+def cpu_baseline(pkg, path, opts, height, budget_s=10.0, repeats=3):
+    """Time the CPU restatement (oracle/, OpenMP over pixels, every core this
+    job may use) over row bands of the same frame: the band height is
+    calibrated to ~budget_s of CPU work, then the same bands are rendered
+    `repeats` times and the median rate is reported."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle  # test infrastructure: the CPU baseline leg
 
     if not os.path.exists(oracle.LIB):
         oracle.build()
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
+    model, ncpu, aff, quota, share = host_cpu()
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or share
     w = opts.width
-    # calibration band: 2 rows
-    rows_done, rays, secs = 0, 0, 0.0
-    band = 2
     nb = 4
     y_centres = [int(height * (k + 0.5) / nb) for k in range(nb)]
-    while True:
-        t_band = 0.0
+
+    def bands(band):
+        rays, secs = 0, 0.0
         for yc in y_centres:
             y0 = max(0, min(height - band, yc - band // 2))
             r = oracle.render(pkg, path, opts, rect=(0, y0, w, y0 + band), threads=threads, want_hits=False)
-            dt = r["stats"]["kernel_ms"] * 1e-3  # render loop only, parse excluded
-            t_band += dt
+            secs += r["stats"]["kernel_ms"] * 1e-3  # render loop only, parse excluded
             rays += r["stats"]["rays"]
-            secs += dt
-            rows_done += band
-        if secs >= budget_s * 0.4 or rows_done >= height:
+        return rays, secs
+
+    band = 2
+    while True:  # calibrate the band height
+        rays, secs = bands(band)
+        if secs >= budget_s * 0.5 or band >= height // nb:
             break
-        band = max(band, int(band * min(8.0, (budget_s - secs) / max(t_band, 1e-3))))
-        band = min(band, height // nb)
-    return {"value": rays / secs / 1e6, "unit": "Mrays/s", "cores": threads, "kind": "port",
-            "sample": f"CPU restatement (oracle/, -O2, OpenMP) on {rows_done} rows x {w} px of the same frame "
-                      f"({nb} bands spread over the image), {rays} rays in {secs:.1f} s"}
+        band = min(height // nb, max(band + 1, int(band * min(8.0, budget_s / max(secs, 1e-3)))))
+    runs = [bands(band) for _ in range(repeats)]
+    rates = sorted(r / s / 1e6 for r, s in runs)
+    med = rates[len(rates) // 2]
+    return {"value": med, "unit": "Mrays/s", "cores": threads, "kind": "port",
+            "cpu_model": model, "host_cpus": ncpu, "affinity_cpus": aff, "cgroup_cpu_quota": quota,
+            "runs_mrays_s": [round(x, 3) for x in rates],
+            "sample": f"CPU restatement (oracle/, g++ -O2, OpenMP {threads} threads) on {nb} bands of {band} rows x "
+                      f"{w} px of the same frame ({runs[0][0]} rays per run), median of {repeats} runs"}
 
 
 def main():
@@ -91,7 +140,7 @@ def main():
     ap.add_argument("--flags", default="-w 1920 -r 5 -O r -A 4")
     ap.add_argument("--tile", type=int, default=32)
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
-    ap.add_argument("--cpu-budget", type=float, default=15.0)
+    ap.add_argument("--cpu-budget", type=float, default=10.0, help="seconds of CPU work per baseline run")
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic_latest.json"),
                     help="PMC-measured HBM bytes per launch (tools/profile_traffic.sh output)")
     args = ap.parse_args()
@@ -170,6 +219,12 @@ def main():
         frame_rays = int(tot.item())
     else:
         frame_rays = st["rays"]
+    shadow_skipped = st["shadow_rays"] - st["shadow_traced"]
+    if world > 1:
+        t = torch.tensor([shadow_skipped], dtype=torch.int64, device="cuda")
+        dist.all_reduce(t)
+        shadow_skipped = int(t.item())
+    traced_rays = frame_rays - shadow_skipped
     ms_per_step = elapsed / args.steps * 1e3
     value = frame_rays * args.steps / elapsed / 1e6
 
@@ -187,14 +242,20 @@ def main():
         algo_bytes = (B_RAY * st["rays"] + B_NODE * st["node_visits"] + B_OBJ * st["object_tests"] +
                       B_TRI * st["tri_tests"] + B_SHADE * st["shades"])
         achieved = algo_bytes / (avg_kernel_ms * 1e-3) / 1e9
-        traffic = None
+        # PMC-measured HBM bytes of one frame (tools/profile_traffic.sh): only
+        # from a pass over this very library build, flags and GPU count
+        traffic, traffic_src = None, None
+        lib_hash = file_sha256(LIB)
         if os.path.exists(args.traffic):
             try:
                 with open(args.traffic) as f:
                     tr = json.load(f)
-                if tr.get("flags") == args.flags and tr.get("n_gpus", 1) == world:
+                if (tr.get("flags") == args.flags and tr.get("n_gpus", 1) == world and
+                        tr.get("lib_sha256") == lib_hash):
                     traffic = tr.get("hbm_bytes_per_launch")
-            except Exception:
+                    traffic_src = {"file": os.path.relpath(args.traffic, ROOT), "tag": tr.get("tag"),
+                                   "build_id": tr.get("build_id")}
+            except (OSError, ValueError):
                 traffic = None
         cpu = None
         if not args.no_cpu and world == 1:
@@ -209,17 +270,27 @@ def main():
                        "parallelism": f"tile-shard x{world} + RCCL gather" if world > 1 else "single GPU"},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                         # measured: PMC HBM bytes of a frame / the frame's GPU time / peak
+                         "frac_hbm": (round(traffic / (avg_kernel_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
+                                      if traffic else None),
+                         "traffic_source": traffic_src,
                          "kernel": ("render_kernel<false,false> (megakernel, 1 launch per frame)" if mega else
                                     "frame span: advance_kernel + trace_kernel<false,1|2> iterations on 3 streams"),
                          "avg_kernel_ms": round(avg_kernel_ms, 3), "launches_per_frame": launches_per_frame,
                          "algorithmic_bytes_per_launch": algo_bytes},
             "cpu_baseline": cpu,
             # traversal work of one frame (the counting pass of the same kernels)
-            "work": {k: st[k] for k in ("rays", "camera_rays", "secondary_rays", "shadow_rays", "node_visits",
-                                        "object_tests", "tri_tests", "shades")},
+            "work": {k: st[k] for k in ("rays", "camera_rays", "secondary_rays", "shadow_rays", "shadow_traced",
+                                        "node_visits", "object_tests", "tri_tests", "shades")},
+            # rays counted as the reference traces them vs rays the GPU traced
+            # (dark-light shadow rays are counted, not traced: DESIGN.md §2)
+            "rays_traced_per_frame": traced_rays,
+            "mrays_traced_per_s": round(traced_rays * args.steps / elapsed / 1e6, 3),
+            "build": {"build_id": build_id(), "lib_sha256": lib_hash},
         }
         if cpu:
             line["gpu_over_cpu"] = round(value / cpu["value"], 2)
+            line["gpu_traced_over_cpu"] = round(line["mrays_traced_per_s"] / cpu["value"], 2)
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.barrier()

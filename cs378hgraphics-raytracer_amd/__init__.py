@@ -85,7 +85,8 @@ assert HIT_DTYPE.itemsize == C.sizeof(RtxHitRecord)
 class RtxStats(C.Structure):
     _fields_ = [("rays", C.c_int64), ("camera_rays", C.c_int64), ("secondary_rays", C.c_int64),
                 ("shadow_rays", C.c_int64), ("node_visits", C.c_int64), ("object_tests", C.c_int64),
-                ("tri_tests", C.c_int64), ("shades", C.c_int64), ("kernel_ms", C.c_double)]
+                ("tri_tests", C.c_int64), ("shades", C.c_int64), ("kernel_ms", C.c_double),
+                ("shadow_traced", C.c_int64)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}

@@ -104,7 +104,7 @@ struct DevScene {
 };
 
 struct Counters {
-  int64_t camera, secondary, shadow, nodes, objects, tris, shades;
+  int64_t camera, secondary, shadow, nodes, objects, tris, shades, shadow_traced;
 };
 
 __host__ __device__ __forceinline__ dvec3 ld3(const double* p) { return mk3(p[0], p[1], p[2]); }

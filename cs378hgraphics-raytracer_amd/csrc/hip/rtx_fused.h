@@ -393,6 +393,7 @@ __device__ __forceinline__ void advance_fused(LaneRef& LR, const DevScene& S, co
             // dark lights are counted, not traced)
             const bool on = !(S.skip_dark && dscomp.x == 0.0 && dscomp.y == 0.0 && dscomp.z == 0.0);
             const dvec3 sdir = light_dir(L, pb);
+            if (STATS && on) C.shadow_traced++;
             if (INLINE) {
               if (on) {
                 const dvec3 res = walk_inline<STATS>(S, L, pb, sdir, stk, lane, C);
@@ -522,13 +523,7 @@ __global__ void __launch_bounds__(WG, RTX_ADV_WAVES)
     if (live) live_out[base + lane_prefix(alive)] = slot;
   }
   if (STATS) {
-    int64_t v[7] = {C.camera, C.secondary, C.shadow, C.nodes, C.objects, C.tris, C.shades};
-#pragma unroll
-    for (int k = 0; k < 7; ++k) {
-      int64_t x = v[k];
-      for (int off = 32; off > 0; off >>= 1) x += __shfl_down(x, off);
-      if (lane == 0 && x) atomicAdd(&stats[k], static_cast<unsigned long long>(x));
-    }
+    stats_add(C, stats, lane);
   }
 }
 
@@ -572,12 +567,6 @@ __global__ void __launch_bounds__(WG) tail_fused_kernel(DevScene S, const DevSce
     }
   }
   if (STATS) {
-    int64_t v[7] = {C.camera, C.secondary, C.shadow, C.nodes, C.objects, C.tris, C.shades};
-#pragma unroll
-    for (int k = 0; k < 7; ++k) {
-      int64_t x = v[k];
-      for (int off = 32; off > 0; off >>= 1) x += __shfl_down(x, off);
-      if (lane == 0 && x) atomicAdd(&stats[k], static_cast<unsigned long long>(x));
-    }
+    stats_add(C, stats, lane);
   }
 }

@@ -1011,7 +1011,10 @@ __device__ __forceinline__ void advance_lane(LaneRef& LR, const DevScene& S, con
             break;
           }
         }
-        if (STATS) C.shadow++;
+        if (STATS) {
+          C.shadow++;
+          C.shadow_traced++;
+        }
         LR.nrays()++;
         LR.sattn() = mk3(1.0, 1.0, 1.0);
         LR.wpos() = pb;
@@ -1087,6 +1090,18 @@ __device__ __forceinline__ void advance_lane(LaneRef& LR, const DevScene& S, con
     }
   }
 
+}
+
+// per-wave sums of a kernel's counters into the frame's stats (indices 0-6:
+// RtxStats rays..shades, 18: shadow rays traced)
+__device__ __forceinline__ void stats_add(const Counters& C, unsigned long long* stats, int lane) {
+  const int64_t v[8] = {C.camera, C.secondary, C.shadow, C.nodes, C.objects, C.tris, C.shades, C.shadow_traced};
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    int64_t x = v[k];
+    for (int off = 32; off > 0; off >>= 1) x += __shfl_down(x, off);
+    if (lane == 0 && x) atomicAdd(&stats[k < 7 ? k : 18], static_cast<unsigned long long>(x));
+  }
 }
 
 template <bool STATS, bool ADAPTIVE, bool MEDIA>
@@ -1557,13 +1572,7 @@ __global__ void __launch_bounds__(WG, RTX_ADV_WAVES) advance_kernel(DevScene S, 
     if (live) live_out[base + lane_prefix(alive)] = slot;
   }
   if (STATS) {
-    int64_t v[7] = {C.camera, C.secondary, C.shadow, C.nodes, C.objects, C.tris, C.shades};
-#pragma unroll
-    for (int k = 0; k < 7; ++k) {
-      int64_t x = v[k];
-      for (int off = 32; off > 0; off >>= 1) x += __shfl_down(x, off);
-      if (lane == 0 && x) atomicAdd(&stats[k], static_cast<unsigned long long>(x));
-    }
+    stats_add(C, stats, lane);
   }
 }
 
@@ -1688,13 +1697,7 @@ __global__ void __launch_bounds__(WG) tail_kernel(DevScene S, const DevScene* __
     atomicMax(&stats[7 + 10], static_cast<unsigned long long>(queries));
   }
   if (STATS) {
-    int64_t v[7] = {C.camera, C.secondary, C.shadow, C.nodes, C.objects, C.tris, C.shades};
-#pragma unroll
-    for (int k = 0; k < 7; ++k) {
-      int64_t x = v[k];
-      for (int off = 32; off > 0; off >>= 1) x += __shfl_down(x, off);
-      if (lane == 0 && x) atomicAdd(&stats[k], static_cast<unsigned long long>(x));
-    }
+    stats_add(C, stats, lane);
   }
 }
 
@@ -2244,7 +2247,7 @@ rtx_status rtx_scene_create(int device, const RtxSceneDesc* d, void** out) {
   st->lights.assign(d->lights, d->lights + d->n_lights);
   if (hipMalloc(&st->d_frame, sizeof(FrameParams)) != hipSuccess ||
       hipMalloc(&st->d_work, sizeof(unsigned long long)) != hipSuccess ||
-      hipMalloc(&st->d_stats, 18 * sizeof(unsigned long long)) != hipSuccess) {
+      hipMalloc(&st->d_stats, 20 * sizeof(unsigned long long)) != hipSuccess) {
     g_err = "rtx_scene_create: hipMalloc failed";
     rtx_scene_destroy(st);
     return RTX_ERR_HIP;
@@ -2485,7 +2488,7 @@ rtx_status rtx_render(void* scene, const RtxRenderParams* params, uint8_t* rgb8,
   // through this pointer (a kernel-argument copy has no address)
   if (!st->d_scene) HIP_TRY(hipMalloc(&st->d_scene, sizeof(DevScene)));
   HIP_TRY(hipMemcpyAsync(st->d_scene, &st->S_launch, sizeof(DevScene), hipMemcpyHostToDevice, stream));
-  if (stats) HIP_TRY(hipMemsetAsync(st->d_stats, 0, 18 * sizeof(unsigned long long), stream));
+  if (stats) HIP_TRY(hipMemsetAsync(st->d_stats, 0, 20 * sizeof(unsigned long long), stream));
   const int pend_cap = (params->depth > 0 ? params->depth : 0) + 2;
   auto get_event = [&](hipEvent_t* e) -> rtx_status {
     if (!st->ev_pool.empty()) {
@@ -2899,7 +2902,7 @@ rtx_status rtx_render(void* scene, const RtxRenderParams* params, uint8_t* rgb8,
     HIP_TRY(hipStreamSynchronize(stream));
   }
   if (stats) {
-    unsigned long long c[18];
+    unsigned long long c[20];
     HIP_TRY(hipMemcpyAsync(c, st->d_stats, sizeof(c), hipMemcpyDeviceToHost, stream));
     HIP_TRY(hipStreamSynchronize(stream));
     {
@@ -2922,6 +2925,7 @@ rtx_status rtx_render(void* scene, const RtxRenderParams* params, uint8_t* rgb8,
     stats->object_tests = c[4];
     stats->tri_tests = c[5];
     stats->shades = c[6];
+    stats->shadow_traced = c[18];
     double tot = 0.0;
     for (auto& pr : frame_events) {
       float ms = 0.0f;

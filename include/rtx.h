@@ -225,6 +225,8 @@ typedef struct RtxStats {
   int64_t tri_tests;     /* TrimeshFace::intersectLocal calls           */
   int64_t shades;        /* Material::shade calls                       */
   double kernel_ms;      /* device time of the render kernel(s)         */
+  int64_t shadow_traced; /* shadow queries actually traced: shadow_rays less the
+                            dark lights counted but skipped */
 } RtxStats;
 
 /* ---- entry points ---- */

@@ -1491,6 +1491,7 @@ int oracle_render(const char* ray_path, const char* cubemap_file, const RtxRende
       stats->camera_rays = tot[0];
       stats->secondary_rays = tot[1];
       stats->shadow_rays = tot[2];
+      stats->shadow_traced = tot[2];  // the restatement traces every shadow ray
       stats->rays = tot[0] + tot[1] + tot[2];
       stats->node_visits = tot[3];
       stats->object_tests = tot[4];

@@ -60,8 +60,15 @@ def main():
             tot[r["Counter_Name"]] += v
     fetch = tot.get("FETCH_SIZE", 0.0) * 1024 * 2
     write = tot.get("WRITE_SIZE", 0.0) * 1024
+    import hashlib
+    lib = os.path.join(ROOT, "cs378hgraphics-raytracer_amd", "lib", "librtx_hip.so")
+    bid = os.path.join(ROOT, "cs378hgraphics-raytracer_amd", "lib", "BUILD_ID")
     out = {
         "tag": tag, "flags": "-w 1920 -r 5 -O r -A 4", "n_gpus": 1,
+        # the build the counters were taken on (bench.py uses the file only
+        # for the same librtx_hip.so)
+        "lib_sha256": hashlib.sha256(open(lib, "rb").read()).hexdigest(),
+        "build_id": open(bid).read().strip() if os.path.exists(bid) else None,
         "unit_of_launch": "frame (all kernels of one frame; bench.py roofline is per frame)",
         "hbm_read_bytes_per_launch": fetch, "hbm_write_bytes_per_launch": write,
         "hbm_bytes_per_launch": fetch + write,
