@@ -156,11 +156,205 @@ __device__ __forceinline__ void flush_terms(LaneRef& LR, const FrameParams& F) {
   LR.wmask() = 0;
 }
 
+// pending-ray entry of lane g: pbuf[(e * 13 + f) * nlanes + g] (advance_lane)
+__device__ __forceinline__ void fused_put_entry(double* b, size_t nlanes, const dvec3& p, const dvec3& d, const dvec3& w,
+                                                const dvec3& k, int depth, int kind, int pos) {
+  b[0 * nlanes] = p.x; b[1 * nlanes] = p.y; b[2 * nlanes] = p.z;
+  b[3 * nlanes] = d.x; b[4 * nlanes] = d.y; b[5 * nlanes] = d.z;
+  b[6 * nlanes] = w.x; b[7 * nlanes] = w.y; b[8 * nlanes] = w.z;
+  b[9 * nlanes] = k.x; b[10 * nlanes] = k.y; b[11 * nlanes] = k.z;
+  b[12 * nlanes] = pend_code(pos, depth, kind);
+}
+__device__ __forceinline__ void fused_push(LaneRef& LR, double* pbuf, size_t nlanes, const dvec3& p, const dvec3& d,
+                                           const dvec3& w, const dvec3& k, int depth, int kind, int pos) {
+  fused_put_entry(pbuf + static_cast<size_t>(LR.top()) * 13 * nlanes + LR.g, nlanes, p, d, w, k, depth, kind, pos);
+  ++LR.top();
+}
+// child node at heap position cpos: its sub-tree on a fork slot, if one is
+// free (same buckets, same sums as on the own stack); false: the own stack
+template <bool FORK>
+__device__ __forceinline__ bool fused_fork_child(LaneRef& LR, const ForkCtx* fk, double* pbuf, size_t nlanes,
+                                                 const dvec3& p, const dvec3& d, const dvec3& w, const dvec3& k,
+                                                 int depth, int kind, int cpos) {
+  if (!FORK || cpos < 2 || fk->spare_n == 0) return false;
+  const unsigned int idx = atomicAdd(fk->fcnt, 1u);
+  if (idx >= fk->spare_n) return false;
+  const int T = fk->spare_base + static_cast<int>(idx);
+  LaneRef LT(LR.m, static_cast<size_t>(T));
+  fused_put_entry(pbuf + static_cast<size_t>(T), nlanes, p, d, w, k, depth, kind, cpos);
+  LT.top() = 1;
+  LT.acc() = mk3(0.0, 0.0, 0.0);
+  LT.nrays() = 0;
+  LT.camk() = 1;
+  LT.cam_end() = 1;
+  LT.pass() = 0;
+  LT.first_query() = 0;
+  LT.rec_on() = LR.rec_on();
+  LT.sample_slot() = LR.sample_slot();
+  LT.fpos() = cpos;
+  LT.wmask() = 0;
+  LT.st() = ST_POP;
+  fk->live_out[atomicAdd(fk->live_cnt, 1u)] = T;
+  return true;
+}
+
+// traceRay after scene->intersect (RayTracer.cpp:116-165) and
+// Material::shade (material.cpp:34-69) for the ray in pending entry `top`
+// with the closest hit (have, bt, bobj, bsub): the hit record, the colour
+// (now, or deferred until the walks' terms are in), the reflection /
+// refraction pushes.  Leaves the lane in ST_POP.  Run by the tail kernel
+// (INLINE: walks in this lane) and by trace_kernel<Q_CLOSEST, FUSED> right
+// where a query completes (walks appended to `we`).
+template <bool STATS, bool INLINE, bool FORK>
+__device__ __forceinline__ void shade_hit(LaneRef& LR, const DevScene& S, const FrameParams& F, Counters& C,
+                                          RtxHitRecord* __restrict__ hits, double* __restrict__ pbuf, size_t nlanes,
+                                          int pend_cap, const ForkCtx* fk, const WalkEmit* we, int* __restrict__ stk,
+                                          int lane, bool have, double bt, int bobj, int bsub) {
+  const RtxRenderParams& P = F.P;
+  const double* b = pbuf + static_cast<size_t>(LR.top()) * 13 * nlanes + LR.g;
+  const dvec3 rp = mk3(b[0 * nlanes], b[1 * nlanes], b[2 * nlanes]);
+  const dvec3 rd = mk3(b[3 * nlanes], b[4 * nlanes], b[5 * nlanes]);
+  dvec3 W = mk3(b[6 * nlanes], b[7 * nlanes], b[8 * nlanes]);
+  const int64_t code = static_cast<int64_t>(b[12 * nlanes]);
+  const int dk = static_cast<int>((code & ((int64_t(1) << 40) - 1)) - (int64_t(1) << 39));
+  const int pos = static_cast<int>(code >> 40);
+  const int rdepth = dk >= 0 ? dk / 4 : -((-dk + 3) / 4);
+  const int rkind = dk - rdepth * 4;
+  LR.st() = ST_POP;
+  if (LR.first_query()) {
+    LR.first_query() = false;
+    if (have) {
+      RtxHitRecord* hr = &hits[LR.sample_slot()];
+      const RtxObject& o = S.objs[bobj];
+      hr->object = o.orig_id;
+      hr->scene_leaf = o.leaf;
+      hr->t = bt;
+      if (o.type == RTX_OBJ_TRIMESH) {
+        const RtxMesh me = S.meshes[o.mesh];
+        const RtxFaceIds fi = S.fids[me.face_off + bsub];
+        hr->face = fi.orig_id;
+        hr->mesh_leaf = fi.leaf;
+      }
+    }
+  }
+  if (!have) {  // miss: the cube map's colour, else black (RayTracer.cpp:167-169; U3)
+    if (S.cube[0] >= 0) contrib_at(LR, F, pos, W * cube_color(S, rd));
+    return;
+  }
+  if (rkind != 0) {  // the parked kt factor of a child ray (RayTracer.cpp:140-158)
+    const dvec3 ktf = mk3(b[9 * nlanes], b[10 * nlanes], b[11 * nlanes]);
+    if (rkind == 1)
+      W = W * rtm::gmax3(rtm::gmin3(rtm::pow3(ktf, bt), rtm::splat3(1.0)), rtm::splat3(0.0));
+    else
+      W = W * rtm::pow3(ktf, bt);
+  }
+  const HitRef R = resolve_hit(S, rp, rd, bobj, bsub, nullptr, nullptr);
+  const dvec3 N = R.N;
+  const int flags = hit_flags(S, R);
+  if (STATS) C.shades++;
+  // Material::shade (material.cpp:34-69)
+  dvec3 i_out = hit_param(S, R, RTX_P_KE) + hit_param(S, R, RTX_P_KA) * mk3(S.ambient[0], S.ambient[1], S.ambient[2]);
+  {
+    const dvec3 kd = hit_param(S, R, RTX_P_KD), ks = hit_param(S, R, RTX_P_KS);
+    const double sh = hit_shininess(S, R);
+    const dvec3 X = rtm::ray_at(rp, rd, bt);
+    const dvec3 pb = X - rd * RTX_EPS_BACKUP;
+    unsigned int wm = 0;
+    int nr = 0;
+    for (int li = 0; li < S.n_lights; ++li) {
+      const RtxLight& L = S.lights[li];
+      const dvec3 l_i = light_dir(L, X);
+      const dvec3 l_r = (l_i - 2 * (rtm::dot(l_i, N)) * N);
+      double dt = rtm::dot(l_i, N);
+      if (flags & RTX_MF_TRANS) dt = fabs(dt);
+      const dvec3 d_comp = kd * rtm::gmax(0.0, dt);
+      const dvec3 s_comp = ks * rtm::splat3(rtm::rpow(rtm::gmax(0.0, rtm::dot(l_r, rd)), sh));
+      const dvec3 dscomp = d_comp + s_comp;
+      const double dattn = light_dist_atten(L, X);
+      if (STATS) C.shadow++;
+      ++nr;
+      // a zero colour factor with finite attenuations adds +0 (DESIGN.md:
+      // dark lights are counted, not traced)
+      const bool on = !(S.skip_dark && dscomp.x == 0.0 && dscomp.y == 0.0 && dscomp.z == 0.0);
+      const dvec3 sdir = light_dir(L, pb);
+      if (STATS && on) C.shadow_traced++;
+      if (INLINE) {
+        if (on) {
+          const dvec3 res = walk_inline<STATS>(S, L, pb, sdir, stk, lane, C);
+          i_out += dattn * res * ld3(L.color) * dscomp;
+        }
+      } else {
+        double qlim, qblk;
+        shadow_bounds(S, L, pb, true, qlim, qblk);
+        emit_walk(*we, on, static_cast<int>(LR.g), li, pb, sdir, qlim, qblk, dattn, dscomp);
+        if (on) wm |= 1u << li;
+      }
+    }
+    LR.nrays() += nr;
+    if (wm == 0) {
+      contrib_at(LR, F, pos, W * i_out);
+    } else {  // colorC = W * shade(...) once the terms are in (flush_terms)
+      LR.W() = W;
+      LR.i_out() = i_out;
+      LR.wmask() = static_cast<int>(wm);
+      LR.rpos() = pos;
+    }
+  }
+  // recursion (RayTracer.cpp:127-164), m_out = air; no adaptive termination
+  // on this path, so it does not wait for the colour
+  const int depth = rdepth - 1;
+  if (!((flags & RTX_MF_RECUR) && depth > 0)) return;
+  const bool leaving = rtm::dot(N, rd) >= 0;
+  const bool next_trans = leaving ? true : (flags & RTX_MF_TRANS) != 0;
+  const dvec3 normal = (leaving ? -1.0 : 1.0) * N;
+  const double c = -1 * rtm::dot(normal, rd);
+  const double eta =
+      next_trans ? (leaving ? hit_index(S, R) : S.air_index) / (leaving ? S.air_index : hit_index(S, R)) : 0;
+  const double radicand = 1 - eta * eta * (1 - c * c);
+  const bool tir = next_trans && radicand < 0;
+  // buckets of the children: their own heap positions when they are nodes
+  // (this ray is a node above the fork depth), else this ray's
+  const bool node = pos > 0 && P.depth - rdepth == ilog2i(pos);
+  const int node_refl = node && 2 * pos < F.fork_npos + 2 ? 2 * pos : 0;
+  const int node_refr = node && 2 * pos + 1 < F.fork_npos + 2 ? 2 * pos + 1 : 0;
+  // push refraction first so that reflection is traced first (the entry at
+  // `top` is this ray's own, read above: it is overwritten)
+  if (next_trans && !tir && LR.top() < pend_cap) {
+    const dvec3 tp = rtm::ray_at(rp, rd, bt + RTX_RAY_EPS);
+    const dvec3 td = eta * rd + (eta * c - sqrt(radicand)) * normal;
+    const dvec3 kf = leaving ? mk3(1.0, 1.0, 1.0) : hit_param(S, R, RTX_P_KT);
+    if (!fused_fork_child<FORK>(LR, fk, pbuf, nlanes, tp, td, W, kf, depth, 2, node_refr))
+      fused_push(LR, pbuf, nlanes, tp, td, W, kf, depth, 2, node_refr ? node_refr : pos);
+    if (STATS) C.secondary++;
+  }
+  if (((flags & RTX_MF_REFL) || tir) && LR.top() < pend_cap) {
+    const dvec3 rdir = rd + 2 * c * normal;
+    const dvec3 rs = rtm::ray_at(rp, rd, bt - RTX_RAY_EPS);
+    const dvec3 wr = W * hit_param(S, R, RTX_P_KR);
+    const dvec3 kf = leaving ? hit_param(S, R, RTX_P_KT) : mk3(1.0, 1.0, 1.0);
+    if (!fused_fork_child<FORK>(LR, fk, pbuf, nlanes, rs, rdir, wr, kf, depth, 1, node_refl))
+      fused_push(LR, pbuf, nlanes, rs, rdir, wr, kf, depth, 1, node_refl ? node_refl : pos);
+    if (STATS) C.secondary++;
+  }
+}
+
+// What trace_kernel<Q_CLOSEST, FUSED> needs to shade a completed query.
+struct ShadeArgs {
+  const FrameParams* Fp;
+  RtxHitRecord* hits;
+  double* pbuf;
+  int pend_cap;
+  QList qn;        // the group's next list (walk records)
+  int slot_off;    // the group's first slot
+  int* live_out;   // this iteration's live list (forked slots join it)
+  int out_cnt;     // its counter
+};
+
 // The fused state machine (CAM -> POP -> HIT): runs until the lane needs a
 // closest-hit query (Q_CLOSEST: the ray is pending-stack entry `top`), has to
-// wait for its terms (Q_WAIT) or its sample is finished (ST_IDLE).
-// INLINE: walks run in this lane (tail kernel); else they are appended to
-// the group's next list (we) and the hit's colour is deferred.
+// wait for its terms (Q_WAIT) or its sample is finished (ST_IDLE).  On the
+// batched iterations the hit is shaded by trace_kernel<Q_CLOSEST, FUSED>
+// (the lane comes back in ST_POP); INLINE (tail kernel) shades it here.
 template <bool STATS, bool INLINE, bool FORK>
 __device__ __forceinline__ void advance_fused(LaneRef& LR, const DevScene& S, const FrameParams& F, Counters& C,
                                               double* __restrict__ sbuf, RtxHitRecord* __restrict__ hits,
@@ -168,46 +362,11 @@ __device__ __forceinline__ void advance_fused(LaneRef& LR, const DevScene& S, co
                                               const ForkCtx* fk, const WalkEmit* we, int* __restrict__ stk,
                                               int lane) {
   const RtxRenderParams& P = F.P;
-  auto put_entry = [&](double* b, const dvec3& p, const dvec3& d, const dvec3& w, const dvec3& k, int depth, int kind,
-                       int pos) {
-    b[0 * nlanes] = p.x; b[1 * nlanes] = p.y; b[2 * nlanes] = p.z;
-    b[3 * nlanes] = d.x; b[4 * nlanes] = d.y; b[5 * nlanes] = d.z;
-    b[6 * nlanes] = w.x; b[7 * nlanes] = w.y; b[8 * nlanes] = w.z;
-    b[9 * nlanes] = k.x; b[10 * nlanes] = k.y; b[11 * nlanes] = k.z;
-    b[12 * nlanes] = pend_code(pos, depth, kind);
-  };
-  auto push = [&](const dvec3& p, const dvec3& d, const dvec3& w, const dvec3& k, int depth, int kind, int pos) {
-    put_entry(pbuf + static_cast<size_t>(LR.top()) * 13 * nlanes + LR.g, p, d, w, k, depth, kind, pos);
-    ++LR.top();
-  };
-  // child node at heap position cpos: its sub-tree on a fork slot, if one is
-  // free (same buckets, same sums as on the own stack)
-  auto fork_child = [&](const dvec3& p, const dvec3& d, const dvec3& w, const dvec3& k, int depth, int kind,
-                        int cpos) -> bool {
-    if (!FORK || cpos < 2 || fk->spare_n == 0) return false;
-    const unsigned int idx = atomicAdd(fk->fcnt, 1u);
-    if (idx >= fk->spare_n) return false;
-    const int T = fk->spare_base + static_cast<int>(idx);
-    LaneRef LT(LR.m, static_cast<size_t>(T));
-    put_entry(pbuf + static_cast<size_t>(T), p, d, w, k, depth, kind, cpos);
-    LT.top() = 1;
-    LT.acc() = mk3(0.0, 0.0, 0.0);
-    LT.nrays() = 0;
-    LT.camk() = 1;
-    LT.cam_end() = 1;
-    LT.pass() = 0;
-    LT.first_query() = 0;
-    LT.rec_on() = LR.rec_on();
-    LT.sample_slot() = LR.sample_slot();
-    LT.fpos() = cpos;
-    LT.wmask() = 0;
-    LT.st() = ST_POP;
-    fk->live_out[atomicAdd(fk->live_cnt, 1u)] = T;
-    return true;
-  };
   LR.qmode() = Q_NONE;
   while (LR.st() != ST_IDLE && LR.qmode() == Q_NONE) {
+#ifndef RTX_FUSED_NOREFRESH
     LR.refresh();
+#endif
     switch (LR.st()) {
       case ST_CAM: {
         // next camera ray of trace(x, y) (RayTracer.cpp:35-79)
@@ -291,7 +450,7 @@ __device__ __forceinline__ void advance_fused(LaneRef& LR, const DevScene& S, co
         LR.camk()++;
         if (STATS) C.camera++;
         LR.top() = 0;
-        push(rp, rd, mk3(1, 1, 1), mk3(1, 1, 1), P.depth, 0, F.fork_on ? 1 : 0);
+        fused_push(LR, pbuf, nlanes, rp, rd, mk3(1, 1, 1), mk3(1, 1, 1), P.depth, 0, F.fork_on ? 1 : 0);
         LR.st() = ST_POP;
         break;
       }
@@ -324,133 +483,14 @@ __device__ __forceinline__ void advance_fused(LaneRef& LR, const DevScene& S, co
         LR.st() = ST_HIT;
         break;
       }
-      case ST_HIT: {
-        // traceRay after scene->intersect (RayTracer.cpp:116-165) + shade
-        const double* b = pbuf + static_cast<size_t>(LR.top()) * 13 * nlanes + LR.g;
-        const dvec3 rp = mk3(b[0 * nlanes], b[1 * nlanes], b[2 * nlanes]);
-        const dvec3 rd = mk3(b[3 * nlanes], b[4 * nlanes], b[5 * nlanes]);
-        dvec3 W = mk3(b[6 * nlanes], b[7 * nlanes], b[8 * nlanes]);
-        const int64_t code = static_cast<int64_t>(b[12 * nlanes]);
-        const int dk = static_cast<int>((code & ((int64_t(1) << 40) - 1)) - (int64_t(1) << 39));
-        const int pos = static_cast<int>(code >> 40);
-        const int rdepth = dk >= 0 ? dk / 4 : -((-dk + 3) / 4);
-        const int rkind = dk - rdepth * 4;
-        const double bt = LR.bt();
-        const int bobj = LR.bobj(), bsub = LR.bsub();
-        if (LR.first_query()) {
-          LR.first_query() = false;
-          if (LR.bhave()) {
-            RtxHitRecord* hr = &hits[LR.sample_slot()];
-            const RtxObject& o = S.objs[bobj];
-            hr->object = o.orig_id;
-            hr->scene_leaf = o.leaf;
-            hr->t = bt;
-            if (o.type == RTX_OBJ_TRIMESH) {
-              const RtxMesh me = S.meshes[o.mesh];
-              const RtxFaceIds fi = S.fids[me.face_off + bsub];
-              hr->face = fi.orig_id;
-              hr->mesh_leaf = fi.leaf;
-            }
-          }
-        }
-        LR.st() = ST_POP;
-        if (!LR.bhave()) {  // miss: the cube map's colour, else black (RayTracer.cpp:167-169; U3)
-          if (S.cube[0] >= 0) contrib_at(LR, F, pos, W * cube_color(S, rd));
-          break;
-        }
-        if (rkind != 0) {  // the parked kt factor of a child ray (RayTracer.cpp:140-158)
-          const dvec3 ktf = mk3(b[9 * nlanes], b[10 * nlanes], b[11 * nlanes]);
-          if (rkind == 1)
-            W = W * rtm::gmax3(rtm::gmin3(rtm::pow3(ktf, bt), rtm::splat3(1.0)), rtm::splat3(0.0));
-          else
-            W = W * rtm::pow3(ktf, bt);
-        }
-        const HitRef R = resolve_hit(S, rp, rd, bobj, bsub, nullptr, nullptr);
-        const dvec3 N = R.N;
-        const int flags = hit_flags(S, R);
-        if (STATS) C.shades++;
-        // Material::shade (material.cpp:34-69)
-        dvec3 i_out = hit_param(S, R, RTX_P_KE) + hit_param(S, R, RTX_P_KA) * mk3(S.ambient[0], S.ambient[1], S.ambient[2]);
-        {
-          const dvec3 kd = hit_param(S, R, RTX_P_KD), ks = hit_param(S, R, RTX_P_KS);
-          const double sh = hit_shininess(S, R);
-          const dvec3 X = rtm::ray_at(rp, rd, bt);
-          const dvec3 pb = X - rd * RTX_EPS_BACKUP;
-          unsigned int wm = 0;
-          for (int li = 0; li < S.n_lights; ++li) {
-            const RtxLight& L = S.lights[li];
-            const dvec3 l_i = light_dir(L, X);
-            const dvec3 l_r = (l_i - 2 * (rtm::dot(l_i, N)) * N);
-            double dt = rtm::dot(l_i, N);
-            if (flags & RTX_MF_TRANS) dt = fabs(dt);
-            const dvec3 d_comp = kd * rtm::gmax(0.0, dt);
-            const dvec3 s_comp = ks * rtm::splat3(rtm::rpow(rtm::gmax(0.0, rtm::dot(l_r, rd)), sh));
-            const dvec3 dscomp = d_comp + s_comp;
-            const double dattn = light_dist_atten(L, X);
-            if (STATS) C.shadow++;
-            LR.nrays()++;
-            // a zero colour factor with finite attenuations adds +0 (DESIGN.md:
-            // dark lights are counted, not traced)
-            const bool on = !(S.skip_dark && dscomp.x == 0.0 && dscomp.y == 0.0 && dscomp.z == 0.0);
-            const dvec3 sdir = light_dir(L, pb);
-            if (STATS && on) C.shadow_traced++;
-            if (INLINE) {
-              if (on) {
-                const dvec3 res = walk_inline<STATS>(S, L, pb, sdir, stk, lane, C);
-                i_out += dattn * res * ld3(L.color) * dscomp;
-              }
-            } else {
-              double qlim, qblk;
-              shadow_bounds(S, L, pb, true, qlim, qblk);
-              emit_walk(*we, on, static_cast<int>(LR.g), li, pb, sdir, qlim, qblk, dattn, dscomp);
-              if (on) wm |= 1u << li;
-            }
-          }
-          if (wm == 0) {
-            contrib_at(LR, F, pos, W * i_out);
-          } else {  // colorC = W * shade(...) once the terms are in (flush_terms)
-            LR.W() = W;
-            LR.i_out() = i_out;
-            LR.wmask() = static_cast<int>(wm);
-            LR.rpos() = pos;
-          }
-        }
-        // recursion (RayTracer.cpp:127-164), m_out = air; no adaptive
-        // termination on this path, so it does not wait for the colour
-        const int depth = rdepth - 1;
-        if (!((flags & RTX_MF_RECUR) && depth > 0)) break;
-        const bool leaving = rtm::dot(N, rd) >= 0;
-        const bool next_trans = leaving ? true : (flags & RTX_MF_TRANS) != 0;
-        const dvec3 normal = (leaving ? -1.0 : 1.0) * N;
-        const double c = -1 * rtm::dot(normal, rd);
-        const double eta =
-            next_trans ? (leaving ? hit_index(S, R) : S.air_index) / (leaving ? S.air_index : hit_index(S, R)) : 0;
-        const double radicand = 1 - eta * eta * (1 - c * c);
-        const bool tir = next_trans && radicand < 0;
-        // buckets of the children: their own heap positions when they are
-        // nodes (this ray is a node above the fork depth), else this ray's
-        const bool node = pos > 0 && P.depth - rdepth == ilog2i(pos);
-        const int node_refl = node && 2 * pos < F.fork_npos + 2 ? 2 * pos : 0;
-        const int node_refr = node && 2 * pos + 1 < F.fork_npos + 2 ? 2 * pos + 1 : 0;
-        // push refraction first so that reflection is traced first (the
-        // entry at `top` is this ray's own, read above: it is overwritten)
-        if (next_trans && !tir && LR.top() < pend_cap) {
-          const dvec3 tp = rtm::ray_at(rp, rd, bt + RTX_RAY_EPS);
-          const dvec3 td = eta * rd + (eta * c - sqrt(radicand)) * normal;
-          const dvec3 kf = leaving ? mk3(1.0, 1.0, 1.0) : hit_param(S, R, RTX_P_KT);
-          if (!fork_child(tp, td, W, kf, depth, 2, node_refr)) push(tp, td, W, kf, depth, 2, node_refr ? node_refr : pos);
-          if (STATS) C.secondary++;
-        }
-        if (((flags & RTX_MF_REFL) || tir) && LR.top() < pend_cap) {
-          const dvec3 rdir = rd + 2 * c * normal;
-          const dvec3 rs = rtm::ray_at(rp, rd, bt - RTX_RAY_EPS);
-          const dvec3 wr = W * hit_param(S, R, RTX_P_KR);
-          const dvec3 kf = leaving ? hit_param(S, R, RTX_P_KT) : mk3(1.0, 1.0, 1.0);
-          if (!fork_child(rs, rdir, wr, kf, depth, 1, node_refl)) push(rs, rdir, wr, kf, depth, 1, node_refl ? node_refl : pos);
-          if (STATS) C.secondary++;
-        }
+      case ST_HIT:
+        // batched iterations: trace_kernel<Q_CLOSEST, FUSED> shades (never here)
+        if (INLINE)
+          shade_hit<STATS, INLINE, FORK>(LR, S, F, C, hits, pbuf, nlanes, pend_cap, fk, we, stk, lane, LR.bhave() != 0,
+                                         LR.bt(), LR.bobj(), LR.bsub());
+        else
+          LR.st() = ST_IDLE;
         break;
-      }
       default:
         LR.st() = ST_IDLE;
         break;
@@ -462,8 +502,11 @@ __device__ __forceinline__ void advance_fused(LaneRef& LR, const DevScene& S, co
 // hit's colour, then run the machine to the next closest query (appended to
 // q0 with ballot + popc + mbcnt, the ray read from the slot's pending stack)
 // while walks go to q1 as they are found.
+#ifndef RTX_FUSED_ADV_WAVES
+#define RTX_FUSED_ADV_WAVES RTX_ADV_WAVES
+#endif
 template <bool STATS, bool FORK>
-__global__ void __launch_bounds__(WG, RTX_ADV_WAVES)
+__global__ void __launch_bounds__(WG, RTX_FUSED_ADV_WAVES)
     advance_fused_kernel(DevScene S, const DevScene* __restrict__ Sg, const FrameParams* __restrict__ Fp, LaneMem lm,
                          double* __restrict__ sbuf, RtxHitRecord* __restrict__ hits, double* __restrict__ pbuf,
                          int pend_cap, QList q0, QList q1, unsigned int* __restrict__ counters,

@@ -1737,6 +1737,9 @@ struct ShadowBlocker {
 #ifndef RTX_REFILL
 #define RTX_REFILL 1
 #endif
+#if RTX_REFILL != 1
+#error "fused walks (trace_kernel FUSED) reset the walk state between claims: RTX_REFILL must be 1"
+#endif
 
 // Persistent traversal of one group's compacted query list.  A wave claims
 // 64 queries at a time (one atomic); lanes whose query ended take the next
@@ -1746,10 +1749,14 @@ struct ShadowBlocker {
 // a lane whose query completes runs the walk's next step (walk_hit) and
 // either queries again from the hit's key or writes the light's term to
 // wterm[light][slot].
-template <bool STATS, int MODE, bool FUSED = false>
+// FUSED Q_CLOSEST: a lane whose query completes shades the hit (shade_hit:
+// colour, walk records, reflection / refraction pushes) before it claims
+// the next query.
+template <bool STATS, int MODE, bool FUSED = false, bool FORK = false>
 __global__ void __launch_bounds__(WG, RTX_TRACE_WAVES)
     trace_kernel(DevScene S, const DevScene* __restrict__ Sg, QList Q, unsigned int* __restrict__ counters,
-                 LaneMem lm, int stack_cap, unsigned long long* __restrict__ stats, double* __restrict__ wterm) {
+                 LaneMem lm, int stack_cap, unsigned long long* __restrict__ stats, double* __restrict__ wterm,
+                 ShadeArgs SA) {
   extern __shared__ int lds_stack[];
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
@@ -1805,7 +1812,10 @@ __global__ void __launch_bounds__(WG, RTX_TRACE_WAVES)
   bool pend = false;  // FUSED: the lane's walk query completed, its walk step is due
   // FUSED: the walk step of a completed query — the next query of the walk
   // (its record keeps the walk's state and the new key) or the light's term
-  auto walk_phase = [&]() {
+  auto walk_phase = [&](bool have_in, double bt_in, int bo_in, int bs_in) {
+    bool w_have = have_in;
+    double w_bt = bt_in;
+    int w_bo = bo_in, w_bs = bs_in;
     while (pend) {
       const size_t k = kq;
       const int li = Q.iv[2 * cap + k];
@@ -1822,10 +1832,10 @@ __global__ void __launch_bounds__(WG, RTX_TRACE_WAVES)
         w.sattn = mk3(Q.d[QF_SAX * cap + k], Q.d[QF_SAY * cap + k], Q.d[QF_SAZ * cap + k]);
         w.last_t = Q.d[QF_LAST * cap + k];
       }
-      const double bt = T.bt;
-      const int bo = T.bobj, bs = T.bsub;
+      const double bt = w_bt;
+      const int bo = w_bo, bs = w_bs;
       dvec3 res;
-      if (walk_hit(S, L, pb, sdir, T.have, bt, bo, bs, w, res)) {
+      if (walk_hit(S, L, pb, sdir, w_have, bt, bo, bs, w, res)) {
         const size_t slot = static_cast<size_t>(Q.slot[k]);
         const dvec3 dsc = mk3(Q.d[QF_SCX * cap + k], Q.d[QF_SCY * cap + k], Q.d[QF_SCZ * cap + k]);
         const dvec3 term = Q.d[QF_DATTN * cap + k] * res * ld3(L.color) * dsc;
@@ -1847,11 +1857,36 @@ __global__ void __launch_bounds__(WG, RTX_TRACE_WAVES)
         shadow_bounds(S, L, pb, false, qlim, qblk);
         active = trav_init<STATS, MODE>(T, S, pb, sdir, bt, bo, bs, qlim, qblk, C);
         pend = !active;  // answered by the root test: the walk's next step
+        w_have = T.have;
+        w_bt = T.bt;
+        w_bo = T.bobj;
+        w_bs = T.bsub;
       }
     }
   };
   for (;;) {
-    if (FUSED) walk_phase();
+    if (FUSED) {
+      // Every lane is idle here (RTX_REFILL 1: the step loop below runs until
+      // no lane is active), so the walk state is dead: resetting it to
+      // constants tells the register allocator so, and the walk / shading
+      // step's temporaries reuse its registers instead of spilling around it.
+      const bool have = T.have;
+      const double bt = T.bt;
+      const int bo = T.bobj, bs = T.bsub;
+      trav_reset(T);
+      if (MODE == Q_NEXT) {
+        walk_phase(have, bt, bo, bs);
+      } else if (pend) {
+        const FrameParams& F = *SA.Fp;
+        const ForkCtx fk = {counters + CNT_FORK, SA.slot_off + F.wf_gsamp, static_cast<unsigned int>(F.wf_gs - F.wf_gsamp),
+                            SA.live_out, counters + SA.out_cnt};
+        const WalkEmit we = {SA.qn, counters + CNT_Q + CNT_LINE};
+        LaneRef LR(lm, static_cast<size_t>(Q.slot[kq]));
+        shade_hit<STATS, false, FORK>(LR, S, F, C, SA.hits, SA.pbuf, lm.n, SA.pend_cap, &fk, &we, nullptr, lane, have, bt,
+                                      bo, bs);
+        pend = false;
+      }
+    }
     unsigned long long idle = __ballot(!active);
     while (idle != 0ull && !exhausted) {
       if (qnext >= qend) {
@@ -1907,13 +1942,7 @@ __global__ void __launch_bounds__(WG, RTX_TRACE_WAVES)
     } while (static_cast<int>(__popcll(__ballot(active))) >= thresh);
   }
   if (STATS) {
-    int64_t v[3] = {C.nodes, C.objects, C.tris};
-#pragma unroll
-    for (int k = 0; k < 3; ++k) {
-      int64_t x = v[k];
-      for (int off = 32; off > 0; off >>= 1) x += __shfl_down(x, off);
-      if (lane == 0 && x) atomicAdd(&stats[3 + k], static_cast<unsigned long long>(x));
-    }
+    stats_add(C, stats, lane);  // traversal counts (and the shading's, FUSED Q_CLOSEST)
     if (lane == 0) {
       atomicAdd(&stats[8 + 2 * (MODE - 1)], static_cast<unsigned long long>(wsteps));
       atomicAdd(&stats[9 + 2 * (MODE - 1)], static_cast<unsigned long long>(lsteps));
@@ -2828,24 +2857,44 @@ rtx_status rtx_render(void* scene, const RtxRenderParams* params, uint8_t* rgb8,
         // the next-hit grid: fused walks can outnumber the live slots
         const int64_t tgn = fuse ? std::max<int64_t>(1, std::min<int64_t>(tgrid, (lb * int64_t(nrec_n) + WG - 1) / WG))
                                  : tg;
-        if (stats) {
-          hipLaunchKernelGGL((trace_kernel<true, Q_CLOSEST>), dim3(tg), dim3(WG), lds, sg, S, st->d_scene, q0,
-                             cnt, A, st->stack_cap, st->d_stats, nullptr);
-          if (fuse)
-            hipLaunchKernelGGL((trace_kernel<true, Q_NEXT, true>), dim3(tgn), dim3(WG), lds, sg, S, st->d_scene, q1,
-                               cnt, A, st->stack_cap, st->d_stats, st->d_wterm);
-          else
-            hipLaunchKernelGGL((trace_kernel<true, Q_NEXT>), dim3(tg), dim3(WG), lds, sg, S, st->d_scene, q1, cnt,
-                               A, st->stack_cap, st->d_stats, nullptr);
-        } else {
-          hipLaunchKernelGGL((trace_kernel<false, Q_CLOSEST>), dim3(tg), dim3(WG), lds, sg, S, st->d_scene, q0,
-                             cnt, A, st->stack_cap, st->d_stats, nullptr);
-          if (fuse)
-            hipLaunchKernelGGL((trace_kernel<false, Q_NEXT, true>), dim3(tgn), dim3(WG), lds, sg, S, st->d_scene, q1,
-                               cnt, A, st->stack_cap, st->d_stats, st->d_wterm);
-          else
-            hipLaunchKernelGGL((trace_kernel<false, Q_NEXT>), dim3(tg), dim3(WG), lds, sg, S, st->d_scene, q1, cnt,
-                               A, st->stack_cap, st->d_stats, nullptr);
+        ShadeArgs sa;
+        std::memset(&sa, 0, sizeof(sa));
+        if (fuse) {
+          sa.Fp = st->d_frame;
+          sa.hits = d_hits;
+          sa.pbuf = st->d_pbuf;
+          sa.pend_cap = pend_cap;
+          sa.qn = q1;
+          sa.slot_off = static_cast<int>(g * gslots);
+          sa.live_out = live_out;
+          sa.out_cnt = out_cnt;
+        }
+        dispatch2(stats, fork, [&](auto st_, auto fk_) {
+          constexpr bool ST_ = decltype(st_)::value, FK_ = decltype(fk_)::value;
+          if (fuse) {
+            hipLaunchKernelGGL((trace_kernel<ST_, Q_CLOSEST, true, FK_>), dim3(tg), dim3(WG), lds, sg, S, st->d_scene,
+                               q0, cnt, A, st->stack_cap, st->d_stats, st->d_wterm, sa);
+            hipLaunchKernelGGL((trace_kernel<ST_, Q_NEXT, true>), dim3(tgn), dim3(WG), lds, sg, S, st->d_scene, q1,
+                               cnt, A, st->stack_cap, st->d_stats, st->d_wterm, sa);
+          } else if (!FK_) {
+            hipLaunchKernelGGL((trace_kernel<ST_, Q_CLOSEST>), dim3(tg), dim3(WG), lds, sg, S, st->d_scene, q0, cnt, A,
+                               st->stack_cap, st->d_stats, nullptr, sa);
+            hipLaunchKernelGGL((trace_kernel<ST_, Q_NEXT>), dim3(tg), dim3(WG), lds, sg, S, st->d_scene, q1, cnt, A,
+                               st->stack_cap, st->d_stats, nullptr, sa);
+          }
+        });
+        if (!fuse && fork) {  // the sequential machine's trace kernels do not depend on forking
+          if (stats) {
+            hipLaunchKernelGGL((trace_kernel<true, Q_CLOSEST>), dim3(tg), dim3(WG), lds, sg, S, st->d_scene, q0, cnt,
+                               A, st->stack_cap, st->d_stats, nullptr, sa);
+            hipLaunchKernelGGL((trace_kernel<true, Q_NEXT>), dim3(tg), dim3(WG), lds, sg, S, st->d_scene, q1, cnt, A,
+                               st->stack_cap, st->d_stats, nullptr, sa);
+          } else {
+            hipLaunchKernelGGL((trace_kernel<false, Q_CLOSEST>), dim3(tg), dim3(WG), lds, sg, S, st->d_scene, q0, cnt,
+                               A, st->stack_cap, st->d_stats, nullptr, sa);
+            hipLaunchKernelGGL((trace_kernel<false, Q_NEXT>), dim3(tg), dim3(WG), lds, sg, S, st->d_scene, q1, cnt, A,
+                               st->stack_cap, st->d_stats, nullptr, sa);
+          }
         }
         HIP_TRY(hipGetLastError());
         if (it % check_every == check_every - 1) {

@@ -172,6 +172,18 @@ RT_HD bool trav_init(Trav& T, const DevScene& S, const dvec3& P, const dvec3& D,
   return true;
 }
 
+// Every field a constant (a walk no lane continues): lets the compiler see
+// the walk's registers as free between queries.
+RT_HD void trav_reset(Trav& T) {
+  T.P = T.D = T.lp = T.ld = mk3(0.0, 0.0, 0.0);
+  T.ri.inv = T.lri.inv = mk3(0.0, 0.0, 0.0);
+  T.ri.fast = T.lri.fast = true;
+  T.tp = T.tlimit = T.tlo = T.tblock = T.bt = T.len = T.mbest = 0.0;
+  T.rp = T.sq = T.bobj = T.bsub = T.sp = T.ref = T.mode = T.oc = T.oe = 0;
+  T.moi = T.mbase = T.mfoff = T.mnoff = T.mface = 0;
+  T.have = T.blocked = T.mhave = false;
+}
+
 // One unit of the walk; true when the query is complete.
 template <bool STATS, int QMODE, class Blocker>
 RT_HD bool trav_step(Trav& T, const DevScene& S, int* __restrict__ stk, const int lane, const Blocker& blocker,
