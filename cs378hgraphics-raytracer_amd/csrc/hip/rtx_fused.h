@@ -25,18 +25,18 @@
 
 #define Q_WAIT 3  // no query: the lane waits one iteration for its shadow terms
 
-// next-hit record of a fused walk, field-major in the group's next list
+// next-hit record of a fused walk, field-major in the group's next list.
+// The query ray is derived, not stored: the direction is light_dir(light,
+// origin) and the bounds are shadow_bounds' (what the emitter computes).
 enum {
-  QF_PX = 0, QF_PY, QF_PZ,     // walk origin: the shading point backed up (light.cpp:13, 28)
-  QF_DX, QF_DY, QF_DZ,         // toward the light
-  QF_TP, QF_TLIM, QF_TBLK,     // key of the last hit, query bounds (shadow_bounds)
+  QF_PX = 0, QF_PY, QF_PZ,           // walk origin: the shading point backed up (light.cpp:13, 28)
   QF_DATTN, QF_SCX, QF_SCY, QF_SCZ,  // distanceAttenuation, d_comp + s_comp
-  QF_WPX, QF_WPY, QF_WPZ,      // the walk's moved origin (light.cpp:37)
-  QF_SAX, QF_SAY, QF_SAZ,      // sattn so far
-  QF_LAST,                     // t of the last hit
+  QF_WPX, QF_WPY, QF_WPZ,            // after a hit: the walk's moved origin (light.cpp:37)
+  QF_SAX, QF_SAY, QF_SAZ,            //   sattn so far
+  QF_LAST,                           //   t of the last hit
   QF_D
 };
-#define QF_I 3  // ints: rp (last hit's object, -1 before the first), sq, light
+#define QF_I 2  // ints: 0 -1 before the walk's first hit (else the last hit's object), 1 light
 
 struct WalkState {
   dvec3 wpos, sattn;
@@ -104,8 +104,7 @@ struct WalkEmit {
 // per call per wave, offsets by mbcnt).  Called from divergent code: the
 // ballot covers the lanes executing it, the lowest of them claims.
 __device__ __forceinline__ void emit_walk(const WalkEmit& E, bool on, int slot, int li, const dvec3& pb,
-                                          const dvec3& sdir, double qlim, double qblk, double dattn,
-                                          const dvec3& dscomp) {
+                                          double dattn, const dvec3& dscomp) {
   const unsigned long long m = __ballot(on);
   if (!on) return;
   const int leader = __builtin_ctzll(m);
@@ -119,19 +118,12 @@ __device__ __forceinline__ void emit_walk(const WalkEmit& E, bool on, int slot, 
   d[QF_PX * cap + k] = pb.x;
   d[QF_PY * cap + k] = pb.y;
   d[QF_PZ * cap + k] = pb.z;
-  d[QF_DX * cap + k] = sdir.x;
-  d[QF_DY * cap + k] = sdir.y;
-  d[QF_DZ * cap + k] = sdir.z;
-  d[QF_TP * cap + k] = -RTX_INF;
-  d[QF_TLIM * cap + k] = qlim;
-  d[QF_TBLK * cap + k] = qblk;
   d[QF_DATTN * cap + k] = dattn;
   d[QF_SCX * cap + k] = dscomp.x;
   d[QF_SCY * cap + k] = dscomp.y;
   d[QF_SCZ * cap + k] = dscomp.z;
   E.q.iv[0 * cap + k] = -1;
-  E.q.iv[1 * cap + k] = -1;
-  E.q.iv[2 * cap + k] = li;
+  E.q.iv[1 * cap + k] = li;
   E.q.slot[k] = slot;
 }
 
@@ -284,9 +276,7 @@ __device__ __forceinline__ void shade_hit(LaneRef& LR, const DevScene& S, const 
           i_out += dattn * res * ld3(L.color) * dscomp;
         }
       } else {
-        double qlim, qblk;
-        shadow_bounds(S, L, pb, true, qlim, qblk);
-        emit_walk(*we, on, static_cast<int>(LR.g), li, pb, sdir, qlim, qblk, dattn, dscomp);
+        emit_walk(*we, on, static_cast<int>(LR.g), li, pb, dattn, dscomp);
         if (on) wm |= 1u << li;
       }
     }
@@ -519,6 +509,7 @@ __global__ void __launch_bounds__(WG, RTX_FUSED_ADV_WAVES)
   const int lane = threadIdx.x & 63;
   Counters C = {0, 0, 0, 0, 0, 0, 0};
   LaneRef L(lm, static_cast<size_t>(slot));
+  if (first) lane_init(L);
   int qm = Q_NONE;
   const ForkCtx fk = {counters + CNT_FORK, slot_off + F.wf_gsamp,
                       first ? 0u : static_cast<unsigned int>(F.wf_gs - F.wf_gsamp), live_out, counters + out_cnt};
@@ -550,11 +541,7 @@ __global__ void __launch_bounds__(WG, RTX_FUSED_ADV_WAVES)
       q0.d[3 * cap + k] = b[3 * n];
       q0.d[4 * cap + k] = b[4 * n];
       q0.d[5 * cap + k] = b[5 * n];
-      q0.d[6 * cap + k] = -RTX_INF;
-      q0.d[7 * cap + k] = RTX_INF;
-      q0.d[8 * cap + k] = -RTX_INF;
-      q0.iv[0 * cap + k] = -1;
-      q0.iv[1 * cap + k] = -1;
+      // (key and bounds of a closest query are constants: not stored)
     }
   }
   const bool live = valid && L.st() != ST_IDLE;  // a query pending or waiting for terms

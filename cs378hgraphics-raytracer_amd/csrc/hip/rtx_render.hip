@@ -433,6 +433,15 @@ struct LaneRef {
   __device__ __forceinline__ void refresh() { asm volatile("" : "+v"(g)::"memory"); }
 };
 
+// the fields a slot's first advance reads: idle, nothing claimed, outside a
+// discoverMat walk, no deferred colour
+__device__ __forceinline__ void lane_init(LaneRef& L) {
+  L.st() = ST_IDLE;
+  L.kdone() = 0;
+  L.dret() = DISC_NONE;
+  L.wmask() = 0;
+}
+
 // zero one lane's state (kernel start)
 __device__ __forceinline__ void lane_clear(const LaneMem& m, size_t g) {
   for (int k = 0; k < LI_COUNT; ++k) m.i[size_t(k) * m.n + g] = 0;
@@ -1483,6 +1492,7 @@ __device__ __forceinline__ void claim_sample(LaneRef& L, const FrameParams& F, R
     L.sx() = double(pi) / (double(P.width) * ssx);  // tracePixel (RayTracer.cpp:87-88)
     L.sy() = double(pj) / (double(P.height) * ssy);
     L.sample_slot() = static_cast<int>(oidx * F.spp + smp);
+    if (F.fork_on) F.fmask[L.sample_slot()] = 0u;  // no bucket written yet (forks come later)
     L.rec_on() = hits != nullptr;
     L.pass() = 0;
     L.camk() = cam0;
@@ -1513,6 +1523,7 @@ __global__ void __launch_bounds__(WG, RTX_ADV_WAVES) advance_kernel(DevScene S, 
   const int slot = first ? slot_off + tid : (valid ? live_in[tid] : slot_off);
   Counters C = {0, 0, 0, 0, 0, 0, 0};
   LaneRef L(lm, static_cast<size_t>(slot));
+  if (first) lane_init(L);
   int qm = Q_NONE;
   // fork slots: the group's slots past its sample slots (none in the
   // first iteration, which only starts camera rays)
@@ -1752,8 +1763,14 @@ struct ShadowBlocker {
 // FUSED Q_CLOSEST: a lane whose query completes shades the hit (shade_hit:
 // colour, walk records, reflection / refraction pushes) before it claims
 // the next query.
+#ifndef RTX_SHADE_WAVES
+#define RTX_SHADE_WAVES RTX_TRACE_WAVES
+#endif
+#ifndef RTX_WALK_WAVES
+#define RTX_WALK_WAVES RTX_TRACE_WAVES
+#endif
 template <bool STATS, int MODE, bool FUSED = false, bool FORK = false>
-__global__ void __launch_bounds__(WG, RTX_TRACE_WAVES)
+__global__ void __launch_bounds__(WG, !FUSED ? RTX_TRACE_WAVES : (MODE == Q_CLOSEST ? RTX_SHADE_WAVES : RTX_WALK_WAVES))
     trace_kernel(DevScene S, const DevScene* __restrict__ Sg, QList Q, unsigned int* __restrict__ counters,
                  LaneMem lm, int stack_cap, unsigned long long* __restrict__ stats, double* __restrict__ wterm,
                  ShadeArgs SA) {
@@ -1818,10 +1835,10 @@ __global__ void __launch_bounds__(WG, RTX_TRACE_WAVES)
     int w_bo = bo_in, w_bs = bs_in;
     while (pend) {
       const size_t k = kq;
-      const int li = Q.iv[2 * cap + k];
-      const RtxLight& L = S.lights[li];
+      const int li = Q.iv[1 * cap + k];
+      const RtxLight& L = Sg->lights[li];
       const dvec3 pb = mk3(Q.d[QF_PX * cap + k], Q.d[QF_PY * cap + k], Q.d[QF_PZ * cap + k]);
-      const dvec3 sdir = mk3(Q.d[QF_DX * cap + k], Q.d[QF_DY * cap + k], Q.d[QF_DZ * cap + k]);
+      const dvec3 sdir = light_dir(L, pb);  // as the emitter computed it
       WalkState w;
       if (Q.iv[0 * cap + k] < 0) {  // the walk's first hit (light.cpp:28-29)
         w.wpos = pb;
@@ -1835,7 +1852,7 @@ __global__ void __launch_bounds__(WG, RTX_TRACE_WAVES)
       const double bt = w_bt;
       const int bo = w_bo, bs = w_bs;
       dvec3 res;
-      if (walk_hit(S, L, pb, sdir, w_have, bt, bo, bs, w, res)) {
+      if (walk_hit(*Sg, L, pb, sdir, w_have, bt, bo, bs, w, res)) {
         const size_t slot = static_cast<size_t>(Q.slot[k]);
         const dvec3 dsc = mk3(Q.d[QF_SCX * cap + k], Q.d[QF_SCY * cap + k], Q.d[QF_SCZ * cap + k]);
         const dvec3 term = Q.d[QF_DATTN * cap + k] * res * ld3(L.color) * dsc;
@@ -1854,7 +1871,7 @@ __global__ void __launch_bounds__(WG, RTX_TRACE_WAVES)
         Q.d[QF_LAST * cap + k] = w.last_t;
         Q.iv[0 * cap + k] = bo;
         double qlim, qblk;
-        shadow_bounds(S, L, pb, false, qlim, qblk);
+        shadow_bounds(*Sg, L, pb, false, qlim, qblk);
         active = trav_init<STATS, MODE>(T, S, pb, sdir, bt, bo, bs, qlim, qblk, C);
         pend = !active;  // answered by the root test: the walk's next step
         w_have = T.have;
@@ -1882,8 +1899,10 @@ __global__ void __launch_bounds__(WG, RTX_TRACE_WAVES)
                             SA.live_out, counters + SA.out_cnt};
         const WalkEmit we = {SA.qn, counters + CNT_Q + CNT_LINE};
         LaneRef LR(lm, static_cast<size_t>(Q.slot[kq]));
-        shade_hit<STATS, false, FORK>(LR, S, F, C, SA.hits, SA.pbuf, lm.n, SA.pend_cap, &fk, &we, nullptr, lane, have, bt,
-                                      bo, bs);
+        // the scene through the device copy: indexing the by-value kernel
+        // argument (cube-map faces) would copy all of it to scratch
+        shade_hit<STATS, false, FORK>(LR, *Sg, F, C, SA.hits, SA.pbuf, lm.n, SA.pend_cap, &fk, &we, nullptr, lane, have,
+                                      bt, bo, bs);
         pend = false;
       }
     }
@@ -1907,10 +1926,22 @@ __global__ void __launch_bounds__(WG, RTX_TRACE_WAVES)
       const unsigned int take = avail < nidle ? avail : nidle;
       if (!active && !pend && rank < take) {
         kq = static_cast<size_t>(qnext) + rank;
-        const dvec3 P = mk3(Q.d[0 * cap + kq], Q.d[1 * cap + kq], Q.d[2 * cap + kq]);
-        const dvec3 D = mk3(Q.d[3 * cap + kq], Q.d[4 * cap + kq], Q.d[5 * cap + kq]);
-        active = trav_init<STATS, MODE>(T, S, P, D, Q.d[6 * cap + kq], Q.iv[0 * cap + kq], Q.iv[1 * cap + kq],
-                                  Q.d[7 * cap + kq], MODE == Q_NEXT ? Q.d[8 * cap + kq] : -RTX_INF, C);
+        if (!FUSED) {
+          const dvec3 P = mk3(Q.d[0 * cap + kq], Q.d[1 * cap + kq], Q.d[2 * cap + kq]);
+          const dvec3 D = mk3(Q.d[3 * cap + kq], Q.d[4 * cap + kq], Q.d[5 * cap + kq]);
+          active = trav_init<STATS, MODE>(T, S, P, D, Q.d[6 * cap + kq], Q.iv[0 * cap + kq], Q.iv[1 * cap + kq],
+                                          Q.d[7 * cap + kq], MODE == Q_NEXT ? Q.d[8 * cap + kq] : -RTX_INF, C);
+        } else if (MODE == Q_CLOSEST) {  // fused closest record: the ray only
+          const dvec3 P = mk3(Q.d[0 * cap + kq], Q.d[1 * cap + kq], Q.d[2 * cap + kq]);
+          const dvec3 D = mk3(Q.d[3 * cap + kq], Q.d[4 * cap + kq], Q.d[5 * cap + kq]);
+          active = trav_init<STATS, MODE>(T, S, P, D, -RTX_INF, -1, -1, RTX_INF, -RTX_INF, C);
+        } else {  // a walk's first query (continuations restart in walk_phase)
+          const RtxLight& L = Sg->lights[Q.iv[1 * cap + kq]];
+          const dvec3 pb = mk3(Q.d[QF_PX * cap + kq], Q.d[QF_PY * cap + kq], Q.d[QF_PZ * cap + kq]);
+          double qlim, qblk;
+          shadow_bounds(*Sg, L, pb, true, qlim, qblk);
+          active = trav_init<STATS, MODE>(T, S, pb, light_dir(L, pb), -RTX_INF, -1, -1, qlim, qblk, C);
+        }
         if (!active) {
           if (FUSED) pend = true;
           else finish();
@@ -2634,7 +2665,7 @@ rtx_status rtx_render(void* scene, const RtxRenderParams* params, uint8_t* rgb8,
     const size_t rec_c = sizeof(int) + QL_D * sizeof(double) + 2 * sizeof(int);
     const size_t rec_n = fuse ? sizeof(int) + QF_D * sizeof(double) + QF_I * sizeof(int) : rec_c;
     const size_t nrec_n = fuse ? std::max<size_t>(1, nl) : 1;
-    const size_t per_slot = lane_mem_bytes(1) + size_t(pend_cap) * 13 * sizeof(double) + rec_c + nrec_n * rec_n +
+    const size_t per_slot = lane_mem_bytes(1) - 512 + size_t(pend_cap) * 13 * sizeof(double) + rec_c + nrec_n * rec_n +
                             2 * sizeof(int) + nl * 3 * sizeof(double);
     {
       // memory budget: what the device has free plus the frame buffers this
@@ -2686,7 +2717,7 @@ rtx_status rtx_render(void* scene, const RtxRenderParams* params, uint8_t* rgb8,
         return rc;
       F.fbuf = st->d_fbuf;
       F.fmask = st->d_fmask;
-      HIP_TRY(hipMemsetAsync(st->d_fmask, 0, nsamp_out * sizeof(unsigned int), stream));
+      // fmask[sample] is cleared when the sample is claimed (claim_sample)
       if (hits) HIP_TRY(hipMemsetAsync(d_hits, 0xff, nsamp_out * sizeof(RtxHitRecord), stream));
     }
     const size_t ns = static_cast<size_t>(nslot64);
@@ -2756,17 +2787,17 @@ rtx_status rtx_render(void* scene, const RtxRenderParams* params, uint8_t* rgb8,
     // the forks that can still start): sizes the grids
     std::vector<int64_t> grid_bound(size_t(G), gslots);
     // tail switch: a group whose live slots fall to this many finishes in
-    // tail_kernel (RTX_TAIL; headline frame 92.6 / 91.0 / 99.5 ms and an
-    // 8-way shard 32.3 / 25.0 / 24.9 ms at 65k / 200k / 400k)
-    int64_t tail_slots = 200000;
+    // tail_kernel (RTX_TAIL; fused walks, headline frame: 64.0 / 62.4 / 62.0
+    // ms at 200k / 400k / 1M; sequential machine: 92.6 / 91.0 / 99.5 ms at
+    // 65k / 200k / 400k)
+    int64_t tail_slots = 1000000;
     const char* tail_env = getenv("RTX_TAIL");
     if (tail_env) tail_slots = atoll(tail_env);
     F.qchunk = 64;
     HIP_TRY(hipMemcpyAsync(st->d_frame, &F, sizeof(FrameParams), hipMemcpyHostToDevice, stream));
-    // every slot ST_IDLE, kdone = 0, outside a discoverMat walk (every other
-    // field is written before it is read; the int rows are field-major)
-    for (int f : {int(LI_st), int(LI_kdone), int(LI_dret), int(LI_wmask)})
-      HIP_TRY(hipMemsetAsync(A.i + size_t(f) * ns, 0, ns * sizeof(int), stream));
+    // every slot starts ST_IDLE, kdone = 0, outside a discoverMat walk, no
+    // deferred colour: set by the group's first advance_kernel, which visits
+    // all of its slots (every other field is written before it is read)
     HIP_TRY(hipMemsetAsync(st->d_counters, 0, 16 * CNT_PER_GROUP * sizeof(unsigned int), stream));
     const size_t lds_stacks = size_t(st->stack_cap) * 64 * sizeof(int) * WAVES_PER_WG;
 #ifdef RTX_LDS_STAGE
