@@ -1444,7 +1444,8 @@ struct QList {
 #define CNT_CLAIM (3 * CNT_LINE)
 #define CNT_ALIVE_B (5 * CNT_LINE)
 #define CNT_FORK (6 * CNT_LINE)  // fork slots taken this frame (not cleared per iteration)
-#define CNT_PER_GROUP (7 * CNT_LINE)
+#define CNT_DONE (7 * CNT_LINE)  // workgroups of the iteration's last kernel that finished
+#define CNT_PER_GROUP (8 * CNT_LINE)
 
 __device__ __forceinline__ unsigned int lane_prefix(unsigned long long mask) {
   return __builtin_amdgcn_mbcnt_hi(static_cast<unsigned int>(mask >> 32),
@@ -1773,7 +1774,7 @@ template <bool STATS, int MODE, bool FUSED = false, bool FORK = false>
 __global__ void __launch_bounds__(WG, !FUSED ? RTX_TRACE_WAVES : (MODE == Q_CLOSEST ? RTX_SHADE_WAVES : RTX_WALK_WAVES))
     trace_kernel(DevScene S, const DevScene* __restrict__ Sg, QList Q, unsigned int* __restrict__ counters,
                  LaneMem lm, int stack_cap, unsigned long long* __restrict__ stats, double* __restrict__ wterm,
-                 ShadeArgs SA) {
+                 ShadeArgs SA, int clr) {
   extern __shared__ int lds_stack[];
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
@@ -1977,6 +1978,22 @@ __global__ void __launch_bounds__(WG, !FUSED ? RTX_TRACE_WAVES : (MODE == Q_CLOS
     if (lane == 0) {
       atomicAdd(&stats[8 + 2 * (MODE - 1)], static_cast<unsigned long long>(wsteps));
       atomicAdd(&stats[9 + 2 * (MODE - 1)], static_cast<unsigned long long>(lsteps));
+    }
+  }
+  // clr >= 0 (the iteration's last launch): the last workgroup to finish
+  // clears the next iteration's counters (lines clr .. clr + 4: its live-slot
+  // count, query counts and claim cursors), so no memset launch has to wait
+  // for CU space between iterations
+  if (clr >= 0) {
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      __threadfence();
+      const unsigned int prev = atomicAdd(&counters[CNT_DONE], 1u);
+      if (prev == gridDim.x - 1) {
+        counters[CNT_DONE] = 0u;
+        for (int l = clr; l < clr + 5; ++l) counters[l * CNT_LINE] = 0u;
+        __threadfence();
+      }
     }
   }
 }
@@ -2865,7 +2882,11 @@ rtx_status rtx_render(void* scene, const RtxRenderParams* params, uint8_t* rgb8,
         const int out_cnt = odd ? CNT_ALIVE_B : CNT_ALIVE_A, in_cnt = odd ? CNT_ALIVE_A : CNT_ALIVE_B;
         int* live_out = live[size_t(g) * 2 + (odd ? 1 : 0)];
         const int* live_in = live[size_t(g) * 2 + (odd ? 0 : 1)];
-        HIP_TRY(hipMemsetAsync(cnt + (odd ? CNT_LINE : 0), 0, 5 * CNT_LINE * sizeof(unsigned int), sg));
+        // this iteration's counters were cleared by the last workgroup of the
+        // previous iteration's next-hit kernel (the frame-start memset for
+        // the first); this iteration's clears the next one's: even
+        // iterations use lines 0-4 (out-count A), odd ones lines 1-5 (B)
+        const int clr_next = odd ? 0 : 1;
         const int first = it == 0 ? 1 : 0;
         const int64_t lb = grid_bound[size_t(g)];
         const int64_t agrid = first ? per : std::max<int64_t>(1, std::min<int64_t>(per, (lb + WG - 1) / WG));
@@ -2904,27 +2925,27 @@ rtx_status rtx_render(void* scene, const RtxRenderParams* params, uint8_t* rgb8,
           constexpr bool ST_ = decltype(st_)::value, FK_ = decltype(fk_)::value;
           if (fuse) {
             hipLaunchKernelGGL((trace_kernel<ST_, Q_CLOSEST, true, FK_>), dim3(tg), dim3(WG), lds, sg, S, st->d_scene,
-                               q0, cnt, A, st->stack_cap, st->d_stats, st->d_wterm, sa);
+                               q0, cnt, A, st->stack_cap, st->d_stats, st->d_wterm, sa, -1);
             hipLaunchKernelGGL((trace_kernel<ST_, Q_NEXT, true>), dim3(tgn), dim3(WG), lds, sg, S, st->d_scene, q1,
-                               cnt, A, st->stack_cap, st->d_stats, st->d_wterm, sa);
+                               cnt, A, st->stack_cap, st->d_stats, st->d_wterm, sa, clr_next);
           } else if (!FK_) {
             hipLaunchKernelGGL((trace_kernel<ST_, Q_CLOSEST>), dim3(tg), dim3(WG), lds, sg, S, st->d_scene, q0, cnt, A,
-                               st->stack_cap, st->d_stats, nullptr, sa);
+                               st->stack_cap, st->d_stats, nullptr, sa, -1);
             hipLaunchKernelGGL((trace_kernel<ST_, Q_NEXT>), dim3(tg), dim3(WG), lds, sg, S, st->d_scene, q1, cnt, A,
-                               st->stack_cap, st->d_stats, nullptr, sa);
+                               st->stack_cap, st->d_stats, nullptr, sa, clr_next);
           }
         });
         if (!fuse && fork) {  // the sequential machine's trace kernels do not depend on forking
           if (stats) {
             hipLaunchKernelGGL((trace_kernel<true, Q_CLOSEST>), dim3(tg), dim3(WG), lds, sg, S, st->d_scene, q0, cnt,
-                               A, st->stack_cap, st->d_stats, nullptr, sa);
+                               A, st->stack_cap, st->d_stats, nullptr, sa, -1);
             hipLaunchKernelGGL((trace_kernel<true, Q_NEXT>), dim3(tg), dim3(WG), lds, sg, S, st->d_scene, q1, cnt, A,
-                               st->stack_cap, st->d_stats, nullptr, sa);
+                               st->stack_cap, st->d_stats, nullptr, sa, clr_next);
           } else {
             hipLaunchKernelGGL((trace_kernel<false, Q_CLOSEST>), dim3(tg), dim3(WG), lds, sg, S, st->d_scene, q0, cnt,
-                               A, st->stack_cap, st->d_stats, nullptr, sa);
+                               A, st->stack_cap, st->d_stats, nullptr, sa, -1);
             hipLaunchKernelGGL((trace_kernel<false, Q_NEXT>), dim3(tg), dim3(WG), lds, sg, S, st->d_scene, q1, cnt, A,
-                               st->stack_cap, st->d_stats, nullptr, sa);
+                               st->stack_cap, st->d_stats, nullptr, sa, clr_next);
           }
         }
         HIP_TRY(hipGetLastError());

@@ -15,6 +15,8 @@
 #include "rtx.h"
 #include "rtx_host.h"
 
+int rtx_cli_multi_gpu(const rtxh::CliOptions& o, void* host_scene);  // multi_gpu.cpp
+
 // raw dump of an extension output (--dump-f64 / --dump-hits); false after
 // printing why it could not be written
 static bool dump_raw(const std::string& path, const void* data, size_t elem, size_t n) {
@@ -44,6 +46,16 @@ int main(int argc, char** argv) {
   }
   if (!o.cubemap.empty() && rtx_host_cubemap(hs, o.cubemap.c_str()) != RTX_OK)
     std::cerr << rtx_host_last_error() << std::endl;  // smartLoadCubemap: render on without one
+  if (o.gpus > 0) {  // one process per GPU, RCCL gather (multi_gpu.cpp); no HIP call before the fork
+    if (!o.dump_f64.empty() || !o.dump_hits.empty()) {
+      std::cerr << "--dump-f64 / --dump-hits are single-GPU options" << std::endl;
+      rtx_host_free(hs);
+      return 1;
+    }
+    const int mrc = rtx_cli_multi_gpu(o, hs);
+    rtx_host_free(hs);
+    return mrc;
+  }
   RtxHostInfo info;
   rtx_host_info(hs, &info);
   RtxSceneDesc desc;

@@ -44,7 +44,9 @@ struct CliOptions {
   std::string cubemap;
   std::string ray_name, img_name;
   // extensions
-  int device = 0;
+  int device = 0;      // first GPU (ranks use device + rank)
+  int gpus = 0;        // > 0: tile-shard the frame over this many GPUs (multi_gpu.cpp)
+  int tile = 32;       // shard tile size with --gpus
   bool stats = false;
   std::string dump_f64, dump_hits;
 };
@@ -63,6 +65,8 @@ inline void cli_usage(const char* prog, const CliOptions& o) {
             << "  -B <?>      a: adaptive AA threshold, d: DoF samples\n"
             << "  -C <?>      d: aperture size\n"
             << "  --device N  GPU index (extension)   --stats  print JSON stats (extension)\n"
+            << "  --gpus N    one process per GPU, 32x32 tiles dealt over N GPUs, RCCL gather (extension)\n"
+            << "  --tile T    tile size with --gpus (default 32)\n"
             << "  --dump-f64 FILE / --dump-hits FILE  raw float64 RGB / hit records (extension)\n";
 }
 
@@ -137,6 +141,8 @@ inline int cli_parse(int argc, char** argv, CliOptions& o) {
                                      {"stats", no_argument, nullptr, 1001},
                                      {"dump-f64", required_argument, nullptr, 1002},
                                      {"dump-hits", required_argument, nullptr, 1003},
+                                     {"gpus", required_argument, nullptr, 1004},
+                                     {"tile", required_argument, nullptr, 1005},
                                      {nullptr, 0, nullptr, 0}};
   const char* jsonfile = nullptr;
   char prev = 0;
@@ -199,6 +205,8 @@ inline int cli_parse(int argc, char** argv, CliOptions& o) {
       case 1001: o.stats = true; break;
       case 1002: o.dump_f64 = optarg; break;
       case 1003: o.dump_hits = optarg; break;
+      case 1004: o.gpus = std::atoi(optarg); break;
+      case 1005: o.tile = std::atoi(optarg); break;
       case 'h':
         cli_usage(argv[0], o);
         return 1;
