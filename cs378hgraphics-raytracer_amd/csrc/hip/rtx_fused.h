@@ -129,7 +129,7 @@ __device__ __forceinline__ void emit_walk(const WalkEmit& E, bool on, int slot, 
 
 // colour c into bucket pos of the lane's sample (the root's bucket is acc)
 __device__ __forceinline__ void contrib_at(LaneRef& LR, const FrameParams& F, int pos, const dvec3& c) {
-  if (F.fork_on && pos >= 2) bucket_add(F, LR.sample_slot(), pos, c);
+  if (F.fork_on && pos >= 2) bucket_add(F, LR.bunit(), pos, c);
   else LR.acc() += c;
 }
 
@@ -183,6 +183,7 @@ __device__ __forceinline__ bool fused_fork_child(LaneRef& LR, const ForkCtx* fk,
   LT.first_query() = 0;
   LT.rec_on() = LR.rec_on();
   LT.sample_slot() = LR.sample_slot();
+  LT.bunit() = LR.bunit();
   LT.fpos() = cpos;
   LT.wmask() = 0;
   LT.st() = ST_POP;
@@ -371,21 +372,21 @@ __device__ __forceinline__ void advance_fused(LaneRef& LR, const DevScene& S, co
             LR.st() = ST_IDLE;
             break;
           }
-          if (F.fork_on) {  // the root's sum; reduce_kernel adds the buckets, then clamps
-            double* out = sbuf + static_cast<int64_t>(LR.sample_slot()) * 3;
-            out[0] = LR.acc().x;
-            out[1] = LR.acc().y;
-            out[2] = LR.acc().z;
-            if (LR.rec_on()) atomicAdd(&hits[LR.sample_slot()].nrays, LR.nrays() + 1);
-            LR.st() = ST_IDLE;
-            break;
-          }
           if (F.cam_split) {  // one camera ray of a DoF sample: its own sum (reduce_kernel scales, clamps)
             const int64_t u = static_cast<int64_t>(LR.sample_slot()) * F.ncam + (LR.cam_end() - 1);
             sbuf[u * 3 + 0] = LR.acc().x;
             sbuf[u * 3 + 1] = LR.acc().y;
             sbuf[u * 3 + 2] = LR.acc().z;
             if (LR.rec_on()) atomicAdd(&hits[LR.sample_slot()].nrays, LR.nrays() + (LR.cam_end() == 1 ? 1 : 0));
+            LR.st() = ST_IDLE;
+            break;
+          }
+          if (F.fork_on) {  // the root's sum; reduce_kernel adds the buckets, then clamps
+            double* out = sbuf + static_cast<int64_t>(LR.sample_slot()) * 3;
+            out[0] = LR.acc().x;
+            out[1] = LR.acc().y;
+            out[2] = LR.acc().z;
+            if (LR.rec_on()) atomicAdd(&hits[LR.sample_slot()].nrays, LR.nrays() + 1);
             LR.st() = ST_IDLE;
             break;
           }

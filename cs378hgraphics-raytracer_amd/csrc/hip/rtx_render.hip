@@ -361,7 +361,7 @@ struct Pending {
 // with it.  LaneRef gives a lane's fields as accessors (LR.st(), LR.acc(), ...).
 #define LANE_INT_FIELDS(X) X(st) X(sample_slot) X(rec_on) X(pass) X(camk) X(nrays) X(top) X(rdepth) X(rkind) \
   X(first_query) X(cam_end) X(sobj) X(ssub) X(m_flags) X(li) X(pick) X(qmode) X(qrp) X(qsq) X(kdone) X(bobj) X(bsub) X(bhave) \
-  X(dret) X(dpass) X(dpush) X(dhead) X(dtot) X(dlast) X(dopq) X(mo_trans) X(wobj) X(wsub) X(fpos) X(rpos) X(wmask)
+  X(dret) X(dpass) X(dpush) X(dhead) X(dtot) X(dlast) X(dopq) X(mo_trans) X(wobj) X(wsub) X(fpos) X(rpos) X(wmask) X(bunit)
 #define LANE_DBL_FIELDS(X) X(sx) X(sy) X(st_t) X(m_sh) X(dattn) X(last_t) X(qtp) X(bt) X(mo_idx) X(wt) X(wtr)
 #define LANE_VEC_FIELDS(X) X(acc) X(rp) X(rd) X(W) X(N) X(i_out) X(dscomp) X(m_kd) X(m_ks) X(area_sum) X(sdir) \
   X(wpos) X(sattn) X(dpos) X(ddir) X(dkt) X(didx) X(mo_kt)
@@ -676,7 +676,7 @@ __device__ __forceinline__ void advance_lane(LaneRef& LR, const DevScene& S, con
   // colour of the current ray (bucket LR.rpos()): the root's bucket is the
   // lane's acc, a node's bucket its fbuf entry
   auto contrib = [&](const dvec3& c) {
-    if (F.fork_on && LR.rpos() >= 2) bucket_add(F, LR.sample_slot(), LR.rpos(), c);
+    if (F.fork_on && LR.rpos() >= 2) bucket_add(F, LR.bunit(), LR.rpos(), c);
     else LR.acc() += c;
   };
   // child node at heap position cpos: its sub-tree on a fork slot, if one is
@@ -699,6 +699,7 @@ __device__ __forceinline__ void advance_lane(LaneRef& LR, const DevScene& S, con
     LT.first_query() = 0;
     LT.rec_on() = LR.rec_on();
     LT.sample_slot() = LR.sample_slot();
+    LT.bunit() = LR.bunit();
     LT.fpos() = cpos;
     LT.dret() = DISC_NONE;
     LT.st() = ST_POP;
@@ -770,18 +771,6 @@ __device__ __forceinline__ void advance_lane(LaneRef& LR, const DevScene& S, con
             LR.st() = ST_IDLE;
             break;
           }
-          if (F.fork_on) {
-            // the root's sum; reduce_kernel adds the forked sub-trees' sums,
-            // then clamps (no DoF / anaglyph with forking); the record's ray
-            // count starts at -1 (0xff fill)
-            double* out = sbuf + static_cast<int64_t>(LR.sample_slot()) * 3;
-            out[0] = LR.acc().x;
-            out[1] = LR.acc().y;
-            out[2] = LR.acc().z;
-            if (LR.rec_on()) atomicAdd(&hits[LR.sample_slot()].nrays, LR.nrays() + 1);
-            LR.st() = ST_IDLE;
-            break;
-          }
           if (F.cam_split) {
             // one camera ray of a DoF sample (RayTracer.cpp:47-75): its own
             // sum; reduce_kernel adds the sample's rays in order, scales and
@@ -793,6 +782,18 @@ __device__ __forceinline__ void advance_lane(LaneRef& LR, const DevScene& S, con
             // per-sample ray count over the sample's units; the record starts
             // at -1 (0xff fill), the first ray's unit adds the 1 back
             if (LR.rec_on()) atomicAdd(&hits[LR.sample_slot()].nrays, LR.nrays() + (LR.cam_end() == 1 ? 1 : 0));
+            LR.st() = ST_IDLE;
+            break;
+          }
+          if (F.fork_on) {
+            // the root's sum; reduce_kernel adds the forked sub-trees' sums,
+            // then clamps (no anaglyph with forking; DoF splits above); the record's ray
+            // count starts at -1 (0xff fill)
+            double* out = sbuf + static_cast<int64_t>(LR.sample_slot()) * 3;
+            out[0] = LR.acc().x;
+            out[1] = LR.acc().y;
+            out[2] = LR.acc().z;
+            if (LR.rec_on()) atomicAdd(&hits[LR.sample_slot()].nrays, LR.nrays() + 1);
             LR.st() = ST_IDLE;
             break;
           }
@@ -1493,7 +1494,9 @@ __device__ __forceinline__ void claim_sample(LaneRef& L, const FrameParams& F, R
     L.sx() = double(pi) / (double(P.width) * ssx);  // tracePixel (RayTracer.cpp:87-88)
     L.sy() = double(pj) / (double(P.height) * ssy);
     L.sample_slot() = static_cast<int>(oidx * F.spp + smp);
-    if (F.fork_on) F.fmask[L.sample_slot()] = 0u;  // no bucket written yet (forks come later)
+    // the buckets' owner: the sample, or with the DoF split its camera ray
+    L.bunit() = F.cam_split ? L.sample_slot() * F.ncam + cam0 : L.sample_slot();
+    if (F.fork_on) F.fmask[L.bunit()] = 0u;  // no bucket written yet (forks come later)
     L.rec_on() = hits != nullptr;
     L.pass() = 0;
     L.camk() = cam0;
@@ -2024,12 +2027,25 @@ __global__ void __launch_bounds__(WG) reduce_kernel(const FrameParams* __restric
     // DoF split: a sample = its camera rays' sums added in order, then
     // trace()'s scale and clamp (RayTracer.cpp:73-77)
     const double* s = sbuf + o * F.spp * F.ncam * 3;
-    for (int q = 0; q < F.spp; ++q) {
-      dvec3 ret = mk3(s[q * F.ncam * 3 + 0], s[q * F.ncam * 3 + 1], s[q * F.ncam * 3 + 2]);
-      for (int k = 1; k < F.ncam; ++k) {
-        const double* r = s + (q * F.ncam + k) * 3;
-        ret += mk3(r[0], r[1], r[2]);
+    // a camera ray's sum: its root's plus (forking) its buckets in heap order
+    auto unit_sum = [&](int q, int k) {
+      const double* r = s + (q * F.ncam + k) * 3;
+      dvec3 u = mk3(r[0], r[1], r[2]);
+      if (F.fork_on) {
+        const int64_t uid = (o * F.spp + q) * F.ncam + k;
+        unsigned int m = F.fmask[uid];
+        while (m) {
+          const int b = __builtin_ctz(m);
+          m &= m - 1;
+          const double* f = F.fbuf + (uid * F.fork_npos + b) * 3;
+          u += mk3(f[0], f[1], f[2]);
+        }
       }
+      return u;
+    };
+    for (int q = 0; q < F.spp; ++q) {
+      dvec3 ret = unit_sum(q, 0);
+      for (int k = 1; k < F.ncam; ++k) ret += unit_sum(q, k);
       ret *= (1.0 / (F.P.dof_div + 1.0));
       acc += rtm::gclamp3(ret, 0.0, 1.0);
     }
@@ -2668,7 +2684,9 @@ rtx_status rtx_render(void* scene, const RtxRenderParams* params, uint8_t* rgb8,
     int fork_depth = 3;
     const char* fd_env = getenv("RTX_FORK_DEPTH");
     if (fd_env && atoi(fd_env) > 0) fork_depth = std::min(4, atoi(fd_env));
-    bool fork_ok = !(fork_env && atoi(fork_env) == 0) && !F.cam_split && !params->dof && !params->anaglyph;
+    // (DoF: with the camera-ray split each camera ray owns its buckets)
+    bool fork_ok = !(fork_env && atoi(fork_env) == 0) && !params->anaglyph && (!params->dof || F.cam_split);
+    const size_t nunit_out = size_t(npix) * F.spp * (F.cam_split ? F.ncam : 1);  // bucket owners
     // fused shadow walks (rtx_fused.h): every light a point or directional
     // light, no overlapping media, no adaptive termination (RTX_FUSE=0: the
     // sequential machine)
@@ -2694,7 +2712,7 @@ rtx_status rtx_render(void* scene, const RtxRenderParams* params, uint8_t* rgb8,
       const size_t sbuf_need = size_t(npix) * F.spp * 3 * sizeof(double);
       const size_t avail = freeb + held > sbuf_need ? (freeb + held - sbuf_need) / 10 * 8 : 0;
       const size_t npos = (size_t(1) << (fork_depth + 1)) - 2;
-      const size_t bucket_need = fork_ok ? size_t(npix) * F.spp * (npos * 3 * sizeof(double) + sizeof(unsigned)) : 0;
+      const size_t bucket_need = fork_ok ? nunit_out * (npos * 3 * sizeof(double) + sizeof(unsigned)) : 0;
       if (bucket_need > avail / 2) fork_ok = false;  // buckets would crowd out the slots: plain accumulation
       const size_t slot_budget = std::min<size_t>(size_t(96) << 30, avail - (fork_ok ? bucket_need : 0));
       const int64_t cap = static_cast<int64_t>(slot_budget / per_slot);
@@ -2727,9 +2745,9 @@ rtx_status rtx_render(void* scene, const RtxRenderParams* params, uint8_t* rgb8,
     if (fork_ok) {
       const size_t nsamp_out = size_t(npix) * F.spp;
       if ((rc = ensure(reinterpret_cast<void**>(&st->d_fbuf), &st->fbuf_bytes,
-                       nsamp_out * F.fork_npos * 3 * sizeof(double))) != RTX_OK)
+                       nunit_out * F.fork_npos * 3 * sizeof(double))) != RTX_OK)
         return rc;
-      if ((rc = ensure(reinterpret_cast<void**>(&st->d_fmask), &st->fmask_bytes, nsamp_out * sizeof(unsigned int))) !=
+      if ((rc = ensure(reinterpret_cast<void**>(&st->d_fmask), &st->fmask_bytes, nunit_out * sizeof(unsigned int))) !=
           RTX_OK)
         return rc;
       F.fbuf = st->d_fbuf;

@@ -3,7 +3,7 @@
 GPU: rank r of N renders tiles t % N == r (what bench.py --gpus N runs on
 each GPU).  The slowest shard's time bounds the N-GPU frame (plus the RCCL
 gather of a few MB).  Prints one JSON line per N.
-usage (GPU box): python tools/shard_probe.py [N ...]"""
+usage (GPU box): python tools/shard_probe.py [--flags "-w 1920 ..."] [N ...]"""
 import json
 import os
 import sys
@@ -18,8 +18,12 @@ def main():
     import torch
 
     pkg = bench.load_package()
-    ns = [int(a) for a in sys.argv[1:]] or [1, 2, 4, 8]
-    opts = pkg.RenderOptions.from_cli("-w 1920 -r 5 -O r -A 4".split())
+    args = sys.argv[1:]
+    flags = "-w 1920 -r 5 -O r -A 4"
+    if args and args[0] == "--flags":
+        flags, args = args[1], args[2:]
+    ns = [int(a) for a in args] or [1, 2, 4, 8]
+    opts = pkg.RenderOptions.from_cli(flags.split())
     host = pkg.HostScene(os.path.join(ROOT, "scenes", "trimesh2.ray"))
     dev = pkg.DeviceScene(host, 0)
     h = host.height_for(opts.width)
@@ -38,7 +42,8 @@ def main():
             torch.cuda.synchronize()
             times.append((time.perf_counter() - t0) / 3 * 1e3)
         full = 1e3 if n == 1 else None
-        print(json.dumps({"n": n, "shard_ms": [round(t, 2) for t in times], "max_ms": round(max(times), 2)}),
+        print(json.dumps({"flags": flags, "n": n, "shard_ms": [round(t, 2) for t in times],
+                          "max_ms": round(max(times), 2)}),
               flush=True)
 
 
