@@ -55,13 +55,16 @@ PATHS = {"wavefront": {}, "mega": {"RTX_MEGAKERNEL": "1"}, "wavefront_1g": {"RTX
          "wavefront_256": {"RTX_SLOTS": "256"},
          "wavefront_nofork": {"RTX_FORK": "0"}, "wavefront_fork4": {"RTX_FORK_DEPTH": "4"},
          # tail_kernel takes over right after the first batched iteration
-         "wavefront_tail": {"RTX_TAIL": "1000000000"}}
+         "wavefront_tail": {"RTX_TAIL": "1000000000"},
+         # the sequential state machine on frames that default to fused walks
+         # (rtx_fused.h; the sequential one still runs area lights, -O o, -O c)
+         "wavefront_seq": {"RTX_FUSE": "0"}}
 
 
 @pytest.fixture(params=list(PATHS), ids=list(PATHS))
 def render_path(request):
     saved = {k: os.environ.get(k) for k in ("RTX_MEGAKERNEL", "RTX_SLOTS", "RTX_GROUPS", "RTX_TAIL", "RTX_FORK",
-                                     "RTX_FORK_DEPTH")}
+                                     "RTX_FORK_DEPTH", "RTX_FUSE")}
     for k in saved:
         os.environ.pop(k, None)
     os.environ.update(PATHS[request.param])
