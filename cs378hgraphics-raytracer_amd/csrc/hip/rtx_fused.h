@@ -20,7 +20,8 @@
 //     at the start of the lane's next step, before anything else reaches the
 //     sample's sum, so the sum's order — and every bit of it — is the
 //     sequential machine's (the terms are added to i_out in light order).
-// The tail kernel runs the same machine with the walks inline (INLINE).
+// The tail kernel runs the same machine, each lane walking its own records
+// (tail_fused_kernel).
 #pragma once
 
 #define Q_WAIT 3  // no query: the lane waits one iteration for its shadow terms
@@ -72,32 +73,12 @@ __device__ __forceinline__ bool walk_hit(const DevScene& S, const RtxLight& L, c
   return false;
 }
 
-// A whole walk in the calling lane (tail kernel): successive next-hit
-// queries from the list start.
-template <bool STATS>
-__device__ __forceinline__ dvec3 walk_inline(const DevScene& S, const RtxLight& L, const dvec3& pb, const dvec3& sdir,
-                                             int* __restrict__ stk, int lane, Counters& C) {
-  WalkState w = {pb, mk3(1.0, 1.0, 1.0), 0.0};
-  double tp = -RTX_INF;
-  int rp = -1, sq = -1;
-  for (;;) {
-    double qlim, qblk;
-    shadow_bounds(S, L, pb, rp < 0, qlim, qblk);
-    double bt;
-    int bo, bs;
-    const bool have = traverse<STATS>(S, Q_NEXT, pb, sdir, tp, rp, sq, qlim, bt, bo, bs, stk, lane, C);
-    dvec3 res;
-    if (walk_hit(S, L, pb, sdir, have, bt, bo, bs, w, res)) return res;
-    tp = bt;
-    rp = bo;
-    sq = bs;
-  }
-}
-
 // the group's next-hit list and its append counter
 struct WalkEmit {
   QList q;
   unsigned int* cnt;
+  int fixed_base;  // >= 0 (tail kernel): record (slot - fixed_base) * n_lights + light, no append
+  int n_lights;
 };
 
 // Append a walk record for the lanes with `on` (wave-aggregated: one atomic
@@ -105,14 +86,20 @@ struct WalkEmit {
 // ballot covers the lanes executing it, the lowest of them claims.
 __device__ __forceinline__ void emit_walk(const WalkEmit& E, bool on, int slot, int li, const dvec3& pb,
                                           double dattn, const dvec3& dscomp) {
-  const unsigned long long m = __ballot(on);
-  if (!on) return;
-  const int leader = __builtin_ctzll(m);
-  const int lane = threadIdx.x & 63;
-  unsigned int base = 0;
-  if (lane == leader) base = atomicAdd(E.cnt, static_cast<unsigned int>(__popcll(m)));
-  base = __shfl(base, leader);
-  const size_t k = base + lane_prefix(m);
+  size_t k;
+  if (E.fixed_base >= 0) {
+    if (!on) return;
+    k = static_cast<size_t>(slot - E.fixed_base) * E.n_lights + li;
+  } else {
+    const unsigned long long m = __ballot(on);
+    if (!on) return;
+    const int leader = __builtin_ctzll(m);
+    const int lane = threadIdx.x & 63;
+    unsigned int base = 0;
+    if (lane == leader) base = atomicAdd(E.cnt, static_cast<unsigned int>(__popcll(m)));
+    base = __shfl(base, leader);
+    k = base + lane_prefix(m);
+  }
   const size_t cap = E.q.cap;
   double* d = E.q.d;
   d[QF_PX * cap + k] = pb.x;
@@ -194,15 +181,16 @@ __device__ __forceinline__ bool fused_fork_child(LaneRef& LR, const ForkCtx* fk,
 // traceRay after scene->intersect (RayTracer.cpp:116-165) and
 // Material::shade (material.cpp:34-69) for the ray in pending entry `top`
 // with the closest hit (have, bt, bobj, bsub): the hit record, the colour
-// (now, or deferred until the walks' terms are in), the reflection /
-// refraction pushes.  Leaves the lane in ST_POP.  Run by the tail kernel
-// (INLINE: walks in this lane) and by trace_kernel<Q_CLOSEST, FUSED> right
-// where a query completes (walks appended to `we`).
-template <bool STATS, bool INLINE, bool FORK>
+// (now, or deferred until the walks' terms are in), the walk records, the
+// reflection / refraction pushes.  Leaves the lane in ST_POP.  Run by
+// trace_kernel<Q_CLOSEST, FUSED> right where a query completes (walks
+// appended to the group's next list) and by the tail kernel (walks at the
+// slot's own record positions, walked by the same lane).
+template <bool STATS, bool FORK>
 __device__ __forceinline__ void shade_hit(LaneRef& LR, const DevScene& S, const FrameParams& F, Counters& C,
                                           RtxHitRecord* __restrict__ hits, double* __restrict__ pbuf, size_t nlanes,
-                                          int pend_cap, const ForkCtx* fk, const WalkEmit* we, int* __restrict__ stk,
-                                          int lane, bool have, double bt, int bobj, int bsub) {
+                                          int pend_cap, const ForkCtx* fk, const WalkEmit* we, bool have, double bt,
+                                          int bobj, int bsub) {
   const RtxRenderParams& P = F.P;
   const double* b = pbuf + static_cast<size_t>(LR.top()) * 13 * nlanes + LR.g;
   const dvec3 rp = mk3(b[0 * nlanes], b[1 * nlanes], b[2 * nlanes]);
@@ -269,17 +257,9 @@ __device__ __forceinline__ void shade_hit(LaneRef& LR, const DevScene& S, const 
       // a zero colour factor with finite attenuations adds +0 (DESIGN.md:
       // dark lights are counted, not traced)
       const bool on = !(S.skip_dark && dscomp.x == 0.0 && dscomp.y == 0.0 && dscomp.z == 0.0);
-      const dvec3 sdir = light_dir(L, pb);
       if (STATS && on) C.shadow_traced++;
-      if (INLINE) {
-        if (on) {
-          const dvec3 res = walk_inline<STATS>(S, L, pb, sdir, stk, lane, C);
-          i_out += dattn * res * ld3(L.color) * dscomp;
-        }
-      } else {
-        emit_walk(*we, on, static_cast<int>(LR.g), li, pb, dattn, dscomp);
-        if (on) wm |= 1u << li;
-      }
+      emit_walk(*we, on, static_cast<int>(LR.g), li, pb, dattn, dscomp);
+      if (on) wm |= 1u << li;
     }
     LR.nrays() += nr;
     if (wm == 0) {
@@ -341,17 +321,15 @@ struct ShadeArgs {
   int out_cnt;     // its counter
 };
 
-// The fused state machine (CAM -> POP -> HIT): runs until the lane needs a
+// The fused state machine (CAM -> POP): runs until the lane needs a
 // closest-hit query (Q_CLOSEST: the ray is pending-stack entry `top`), has to
-// wait for its terms (Q_WAIT) or its sample is finished (ST_IDLE).  On the
-// batched iterations the hit is shaded by trace_kernel<Q_CLOSEST, FUSED>
-// (the lane comes back in ST_POP); INLINE (tail kernel) shades it here.
-template <bool STATS, bool INLINE, bool FORK>
+// wait for its terms (Q_WAIT) or its sample is finished (ST_IDLE).  The hit
+// is shaded by whoever runs the query (trace_kernel<Q_CLOSEST, FUSED>, the
+// tail kernel): the lane comes back in ST_POP.
+template <bool STATS, bool FORK>
 __device__ __forceinline__ void advance_fused(LaneRef& LR, const DevScene& S, const FrameParams& F, Counters& C,
                                               double* __restrict__ sbuf, RtxHitRecord* __restrict__ hits,
-                                              double* __restrict__ pbuf, size_t nlanes, int pend_cap,
-                                              const ForkCtx* fk, const WalkEmit* we, int* __restrict__ stk,
-                                              int lane) {
+                                              double* __restrict__ pbuf, size_t nlanes, int pend_cap) {
   const RtxRenderParams& P = F.P;
   LR.qmode() = Q_NONE;
   while (LR.st() != ST_IDLE && LR.qmode() == Q_NONE) {
@@ -474,14 +452,6 @@ __device__ __forceinline__ void advance_fused(LaneRef& LR, const DevScene& S, co
         LR.st() = ST_HIT;
         break;
       }
-      case ST_HIT:
-        // batched iterations: trace_kernel<Q_CLOSEST, FUSED> shades (never here)
-        if (INLINE)
-          shade_hit<STATS, INLINE, FORK>(LR, S, F, C, hits, pbuf, nlanes, pend_cap, fk, we, stk, lane, LR.bhave() != 0,
-                                         LR.bt(), LR.bobj(), LR.bsub());
-        else
-          LR.st() = ST_IDLE;
-        break;
       default:
         LR.st() = ST_IDLE;
         break;
@@ -512,16 +482,13 @@ __global__ void __launch_bounds__(WG, RTX_FUSED_ADV_WAVES)
   LaneRef L(lm, static_cast<size_t>(slot));
   if (first) lane_init(L);
   int qm = Q_NONE;
-  const ForkCtx fk = {counters + CNT_FORK, slot_off + F.wf_gsamp,
-                      first ? 0u : static_cast<unsigned int>(F.wf_gs - F.wf_gsamp), live_out, counters + out_cnt};
-  const WalkEmit we = {q1, counters + CNT_Q + CNT_LINE};
   if (valid && (L.st() != ST_IDLE || slot_unit(F, slot, L.kdone()) >= 0)) {
     flush_terms(L, F);
     L.qmode() = Q_NONE;
     for (;;) {
       claim_sample(L, F, hits, slot);
       if (L.st() == ST_IDLE) break;
-      advance_fused<STATS, false, FORK>(L, *Sg, F, C, sbuf, hits, pbuf, lm.n, pend_cap, &fk, &we, nullptr, lane);
+      advance_fused<STATS, FORK>(L, *Sg, F, C, sbuf, hits, pbuf, lm.n, pend_cap);
       if (L.qmode() != Q_NONE) break;
     }
     qm = L.qmode();
@@ -558,8 +525,11 @@ __global__ void __launch_bounds__(WG, RTX_FUSED_ADV_WAVES)
   }
 }
 
-// Tail of a fused frame (see tail_kernel): each slot runs its own chain,
-// walks inline.
+// Tail of a fused frame (see tail_kernel): each slot runs its own chain —
+// closest query, shading, its walks one after the other — with one
+// traversal call site, so the kernel keeps the sequential tail's register
+// budget.  The walk records go to the group's next list at the slot's own
+// positions (the batched iterations are over, the list is free).
 template <bool STATS>
 __global__ void __launch_bounds__(WG) tail_fused_kernel(DevScene S, const DevScene* __restrict__ Sg,
                                                          const FrameParams* __restrict__ Fp, LaneMem lm,
@@ -567,7 +537,8 @@ __global__ void __launch_bounds__(WG) tail_fused_kernel(DevScene S, const DevSce
                                                          double* __restrict__ pbuf, int pend_cap,
                                                          const unsigned int* __restrict__ counters,
                                                          const int* __restrict__ live_in, int in_cnt, int stack_cap,
-                                                         unsigned long long* __restrict__ stats) {
+                                                         unsigned long long* __restrict__ stats, QList qn,
+                                                         int slot_off) {
   extern __shared__ int lds_stack[];
   const FrameParams& F = *Fp;
   const int lane = threadIdx.x & 63;
@@ -577,24 +548,80 @@ __global__ void __launch_bounds__(WG) tail_fused_kernel(DevScene S, const DevSce
   const bool valid = tid < static_cast<int>(counters[in_cnt]);
   const int slot = valid ? live_in[tid] : 0;
   LaneRef L(lm, static_cast<size_t>(slot));
-  if (valid) {
-    flush_terms(L, F);
-    for (;;) {
+  const DevScene& SS = *Sg;
+  const WalkEmit we = {qn, nullptr, slot_off, SS.n_lights};
+  const size_t cap = qn.cap;
+  unsigned int todo = 0;  // lights whose walk is still to run (records at the slot's positions)
+  int wl = -1;            // the light being walked; w: its state
+  WalkState w = {mk3(0.0, 0.0, 0.0), mk3(0.0, 0.0, 0.0), 0.0};
+  dvec3 pb = mk3(0.0, 0.0, 0.0), sdir = pb;
+  double tp = -RTX_INF;
+  int rp = -1, sq = -1;
+  bool live = valid;
+  if (valid) flush_terms(L, F);
+  while (live) {
+    int qm;
+    dvec3 qP, qD;
+    double qlim = RTX_INF;
+    if (todo) {
+      if (wl < 0) {  // start the next walk (light order)
+        wl = __builtin_ctz(todo);
+        const size_t k = static_cast<size_t>(slot - slot_off) * SS.n_lights + wl;
+        pb = mk3(qn.d[QF_PX * cap + k], qn.d[QF_PY * cap + k], qn.d[QF_PZ * cap + k]);
+        sdir = light_dir(SS.lights[wl], pb);
+        w.wpos = pb;
+        w.sattn = mk3(1.0, 1.0, 1.0);
+        w.last_t = 0.0;
+        tp = -RTX_INF;
+        rp = -1;
+        sq = -1;
+      }
+      double qblk;
+      shadow_bounds(SS, SS.lights[wl], pb, rp < 0, qlim, qblk);
+      qm = Q_NEXT;
+      qP = pb;
+      qD = sdir;
+    } else {
+      flush_terms(L, F);
       L.qmode() = Q_NONE;
       claim_sample(L, F, hits, slot);
       if (L.st() == ST_IDLE) break;
-      advance_fused<STATS, true, false>(L, *Sg, F, C, sbuf, hits, pbuf, lm.n, pend_cap, nullptr, nullptr, stk, lane);
-      if (L.qmode() != Q_CLOSEST) continue;
+      advance_fused<STATS, false>(L, SS, F, C, sbuf, hits, pbuf, lm.n, pend_cap);
+      if (L.qmode() != Q_CLOSEST) {
+        live = L.st() != ST_IDLE;
+        continue;
+      }
+      qm = Q_CLOSEST;
       const double* b = pbuf + static_cast<size_t>(L.top()) * 13 * lm.n + slot;
-      const dvec3 qP = mk3(b[0 * lm.n], b[1 * lm.n], b[2 * lm.n]);
-      const dvec3 qD = mk3(b[3 * lm.n], b[4 * lm.n], b[5 * lm.n]);
-      double bt;
-      int bobj, bsub;
-      const bool have = traverse<STATS>(S, Q_CLOSEST, qP, qD, -RTX_INF, -1, -1, RTX_INF, bt, bobj, bsub, stk, lane, C);
-      L.bt() = bt;
-      L.bobj() = bobj;
-      L.bsub() = bsub;
-      L.bhave() = have ? 1 : 0;
+      qP = mk3(b[0 * lm.n], b[1 * lm.n], b[2 * lm.n]);
+      qD = mk3(b[3 * lm.n], b[4 * lm.n], b[5 * lm.n]);
+      tp = -RTX_INF;
+      rp = -1;
+      sq = -1;
+    }
+    double bt;
+    int bobj, bsub;
+    const bool have = traverse<STATS>(S, qm, qP, qD, tp, rp, sq, qlim, bt, bobj, bsub, stk, lane, C);
+    if (qm == Q_NEXT) {
+      dvec3 res;
+      if (walk_hit(SS, SS.lights[wl], pb, sdir, have, bt, bobj, bsub, w, res)) {
+        const size_t k = static_cast<size_t>(slot - slot_off) * SS.n_lights + wl;
+        const dvec3 dsc = mk3(qn.d[QF_SCX * cap + k], qn.d[QF_SCY * cap + k], qn.d[QF_SCZ * cap + k]);
+        const dvec3 term = qn.d[QF_DATTN * cap + k] * res * ld3(SS.lights[wl].color) * dsc;
+        double* o = F.wterm + (static_cast<size_t>(wl) * lm.n + slot) * 3;
+        o[0] = term.x;
+        o[1] = term.y;
+        o[2] = term.z;
+        todo &= todo - 1;
+        wl = -1;
+      } else {
+        tp = bt;
+        rp = bobj;
+        sq = bsub;
+      }
+    } else {
+      shade_hit<STATS, false>(L, SS, F, C, hits, pbuf, lm.n, pend_cap, nullptr, &we, have, bt, bobj, bsub);
+      todo = static_cast<unsigned int>(L.wmask());
     }
   }
   if (STATS) {

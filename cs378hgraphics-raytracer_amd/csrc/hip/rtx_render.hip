@@ -1901,12 +1901,11 @@ __global__ void __launch_bounds__(WG, !FUSED ? RTX_TRACE_WAVES : (MODE == Q_CLOS
         const FrameParams& F = *SA.Fp;
         const ForkCtx fk = {counters + CNT_FORK, SA.slot_off + F.wf_gsamp, static_cast<unsigned int>(F.wf_gs - F.wf_gsamp),
                             SA.live_out, counters + SA.out_cnt};
-        const WalkEmit we = {SA.qn, counters + CNT_Q + CNT_LINE};
+        const WalkEmit we = {SA.qn, counters + CNT_Q + CNT_LINE, -1, 0};
         LaneRef LR(lm, static_cast<size_t>(Q.slot[kq]));
         // the scene through the device copy: indexing the by-value kernel
         // argument (cube-map faces) would copy all of it to scratch
-        shade_hit<STATS, false, FORK>(LR, *Sg, F, C, SA.hits, SA.pbuf, lm.n, SA.pend_cap, &fk, &we, nullptr, lane, have,
-                                      bt, bo, bs);
+        shade_hit<STATS, FORK>(LR, *Sg, F, C, SA.hits, SA.pbuf, lm.n, SA.pend_cap, &fk, &we, have, bt, bo, bs);
         pend = false;
       }
     }
@@ -2878,10 +2877,12 @@ rtx_status rtx_render(void* scene, const RtxRenderParams* params, uint8_t* rgb8,
           if (fuse) {
             if (stats)
               hipLaunchKernelGGL((tail_fused_kernel<true>), dim3(grid), dim3(WG), lds, sg, S, st->d_scene, st->d_frame,
-                                 A, sb, d_hits, st->d_pbuf, pend_cap, cnt, live_in, in_cnt, st->stack_cap, st->d_stats);
+                                 A, sb, d_hits, st->d_pbuf, pend_cap, cnt, live_in, in_cnt, st->stack_cap, st->d_stats,
+                                 ql[size_t(g) * 2 + 1], static_cast<int>(g * gslots));
             else
               hipLaunchKernelGGL((tail_fused_kernel<false>), dim3(grid), dim3(WG), lds, sg, S, st->d_scene, st->d_frame,
-                                 A, sb, d_hits, st->d_pbuf, pend_cap, cnt, live_in, in_cnt, st->stack_cap, st->d_stats);
+                                 A, sb, d_hits, st->d_pbuf, pend_cap, cnt, live_in, in_cnt, st->stack_cap, st->d_stats,
+                                 ql[size_t(g) * 2 + 1], static_cast<int>(g * gslots));
           } else {
             dispatch2(stats, media, [&](auto st_, auto md_) {
               hipLaunchKernelGGL((tail_kernel<decltype(st_)::value, decltype(md_)::value>), dim3(grid), dim3(WG), lds,
