@@ -557,9 +557,8 @@ __global__ void __launch_bounds__(WG) tail_fused_kernel(DevScene S, const DevSce
   dvec3 pb = mk3(0.0, 0.0, 0.0), sdir = pb;
   double tp = -RTX_INF;
   int rp = -1, sq = -1;
-  bool live = valid;
   if (valid) flush_terms(L, F);
-  while (live) {
+  while (valid) {
     int qm;
     dvec3 qP, qD;
     double qlim = RTX_INF;
@@ -587,10 +586,7 @@ __global__ void __launch_bounds__(WG) tail_fused_kernel(DevScene S, const DevSce
       claim_sample(L, F, hits, slot);
       if (L.st() == ST_IDLE) break;
       advance_fused<STATS, false>(L, SS, F, C, sbuf, hits, pbuf, lm.n, pend_cap);
-      if (L.qmode() != Q_CLOSEST) {
-        live = L.st() != ST_IDLE;
-        continue;
-      }
+      if (L.qmode() != Q_CLOSEST) continue;  // the sample is done: claim the next one
       qm = Q_CLOSEST;
       const double* b = pbuf + static_cast<size_t>(L.top()) * 13 * lm.n + slot;
       qP = mk3(b[0 * lm.n], b[1 * lm.n], b[2 * lm.n]);
