@@ -2827,6 +2827,11 @@ rtx_status rtx_render(void* scene, const RtxRenderParams* params, uint8_t* rgb8,
     int64_t tail_slots = 1000000;
     const char* tail_env = getenv("RTX_TAIL");
     if (tail_env) tail_slots = atoll(tail_env);
+    // RTX_TAIL_ITER=k (A/B): the tail kernel takes over at batched iteration
+    // k whatever the live count
+    int tail_iter = 0;
+    const char* ti_env = getenv("RTX_TAIL_ITER");
+    if (ti_env) tail_iter = atoi(ti_env);
     F.qchunk = 64;
     HIP_TRY(hipMemcpyAsync(st->d_frame, &F, sizeof(FrameParams), hipMemcpyHostToDevice, stream));
     // every slot starts ST_IDLE, kdone = 0, outside a discoverMat walk, no
@@ -2874,7 +2879,7 @@ rtx_status rtx_render(void* scene, const RtxRenderParams* params, uint8_t* rgb8,
         unsigned int* cnt = st->d_counters + CNT_PER_GROUP * g;
         const QList& q0 = ql[size_t(g) * 2];
         const QList& q1 = ql[size_t(g) * 2 + 1];
-        if (it > 0 && live_bound[size_t(g)] <= tail_slots) {
+        if (it > 0 && (live_bound[size_t(g)] <= tail_slots || (tail_iter > 0 && it >= tail_iter))) {
           // few slots left: finish them in one persistent launch
           const bool odd = (it & 1) != 0;  // this iteration would read the list the last one wrote
           const int in_cnt = odd ? CNT_ALIVE_A : CNT_ALIVE_B;
