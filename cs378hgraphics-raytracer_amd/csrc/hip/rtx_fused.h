@@ -597,7 +597,7 @@ __global__ void __launch_bounds__(WG) tail_fused_kernel(DevScene S, const DevSce
     }
     double bt;
     int bobj, bsub;
-    const bool have = traverse<STATS>(S, qm, qP, qD, tp, rp, sq, qlim, bt, bobj, bsub, stk, lane, C);
+    const bool have = traverse_any<STATS>(S, qm, qP, qD, tp, rp, sq, qlim, bt, bobj, bsub, stk, lane, C);
     if (qm == Q_NEXT) {
       dvec3 res;
       if (walk_hit(SS, SS.lights[wl], pb, sdir, have, bt, bobj, bsub, w, res)) {

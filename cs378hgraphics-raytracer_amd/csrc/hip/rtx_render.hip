@@ -1643,7 +1643,7 @@ __global__ void __launch_bounds__(WG) tail_kernel(DevScene S, const DevScene* __
       }
       double bt;
       int bobj, bsub;
-      const bool have = traverse<STATS>(S, qm, qP, qD, L.qtp(), L.qrp(), L.qsq(), qlim, bt, bobj, bsub, stk, lane, C);
+      const bool have = traverse_any<STATS>(S, qm, qP, qD, L.qtp(), L.qrp(), L.qsq(), qlim, bt, bobj, bsub, stk, lane, C);
       L.bt() = bt;
       L.bobj() = bobj;
       L.bsub() = bsub;

@@ -63,7 +63,14 @@ struct Trav {
   double len, mbest;
   int moi, mbase, mfoff, mnoff, mface;
   bool mhave;
+  bool closest;  // the query's mode (read by the Q_ANY instantiations)
 };
+
+// QMODE Q_ANY: one instantiation for both query kinds, the mode read from
+// the Trav — for kernels whose lanes mix closest and next-hit queries (the
+// tail), so a wave steps them together instead of running the two loops
+// one after the other.
+#define Q_ANY 0
 
 // Plain ordered queries (closest hits, the host harness, the megakernel).
 struct NoBlocker {
@@ -146,8 +153,9 @@ RT_HD bool trav_init(Trav& T, const DevScene& S, const dvec3& P, const dvec3& D,
   T.bsub = INT_MAX;
   T.have = false;
   T.blocked = false;
+  if (QMODE != Q_ANY) T.closest = QMODE == Q_CLOSEST;  // Q_ANY: set by the caller first
   if (S.n_snodes == 0) return false;
-  T.tlo = QMODE == Q_CLOSEST ? -RTX_INF : tp - S.margin;
+  T.tlo = QMODE == Q_CLOSEST ? -RTX_INF : tp - S.margin;  // Q_ANY: tp = -inf for a closest query
   T.ri = ray_inv(D);
   if (STATS) C.nodes++;
   double a, b;
@@ -181,14 +189,14 @@ RT_HD void trav_reset(Trav& T) {
   T.tp = T.tlimit = T.tlo = T.tblock = T.bt = T.len = T.mbest = 0.0;
   T.rp = T.sq = T.bobj = T.bsub = T.sp = T.ref = T.mode = T.oc = T.oe = 0;
   T.moi = T.mbase = T.mfoff = T.mnoff = T.mface = 0;
-  T.have = T.blocked = T.mhave = false;
+  T.have = T.blocked = T.mhave = T.closest = false;
 }
 
 // One unit of the walk; true when the query is complete.
 template <bool STATS, int QMODE, class Blocker>
 RT_HD bool trav_step(Trav& T, const DevScene& S, int* __restrict__ stk, const int lane, const Blocker& blocker,
                      Counters& C) {
-  constexpr bool closest = QMODE == Q_CLOSEST;
+  const bool closest = QMODE == Q_CLOSEST || (QMODE == Q_ANY && T.closest);
   const double tp = T.tp, tlimit = T.tlimit, tlo = T.tlo;
   const int rp = T.rp, sq = T.sq;
   double& bt = T.bt;
@@ -512,6 +520,23 @@ RT_HD bool traverse(const DevScene& S, const int qmode, const dvec3& P, const dv
   return T.have;
 }
 
+
+// One query to completion, either kind, one traversal loop (Q_ANY).
+template <bool STATS>
+RT_HD bool traverse_any(const DevScene& S, const int qmode, const dvec3& P, const dvec3& D, const double tp,
+                        const int rp, const int sq, const double tlimit, double& bt, int& bobj, int& bsub,
+                        int* __restrict__ stk, const int lane, Counters& C) {
+  Trav T;
+  const NoBlocker nb;
+  T.closest = qmode == Q_CLOSEST;
+  if (trav_init<STATS, Q_ANY>(T, S, P, D, T.closest ? -RTX_INF : tp, rp, sq, tlimit, -RTX_INF, C))
+    while (!trav_step<STATS, Q_ANY>(T, S, stk, lane, nb, C)) {
+    }
+  bt = T.bt;
+  bobj = T.bobj;
+  bsub = T.bsub;
+  return T.have;
+}
 
 // float bounds of a double box rounded outward (the record holds a superset)
 inline float round_down_f(double x) {

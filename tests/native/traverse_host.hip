@@ -86,6 +86,19 @@ int trav_host_run(const RtxSceneDesc* d, int32_t qmode, int32_t n, const double*
       int bobj, bsub;
       const bool have = traverse<true>(H.S, qmode, p, dd, tp, rp, sq, qmode == Q_CLOSEST ? RTX_INF : tlimit[k], bt,
                                        bobj, bsub, stk.data(), 0, C);
+      // the runtime-mode instantiation (tail kernels, megakernel) must agree
+      // bit for bit; a disagreement poisons the answer (object -999)
+      double bt2;
+      int bobj2, bsub2;
+      Counters C2 = C;
+      const bool have2 = traverse_any<true>(H.S, qmode, p, dd, tp, rp, sq,
+                                            qmode == Q_CLOSEST ? RTX_INF : tlimit[k], bt2, bobj2, bsub2, stk.data(), 0,
+                                            C2);
+      if (have2 != have || (have && (bt2 != bt || bobj2 != bobj || bsub2 != bsub))) {
+        object[size_t(k) * kk + j] = -999;
+        ++cnt;
+        break;
+      }
       if (!have) break;
       const RtxObject& o = d->objects[bobj];
       t[size_t(k) * kk + j] = bt;
