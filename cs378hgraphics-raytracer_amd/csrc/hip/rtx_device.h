@@ -48,9 +48,9 @@ using rtm::mk3;
 // objects whose world box does — Geometry::intersect re-tests it).  Internal
 // boxes therefore only steer the walk, and any test that never rejects a
 // box the exact one accepts is as good.  The records store them as floats
-// rounded outward (a superset box) tested conservatively (box_cons); the
-// exact test runs where it decides a result: on each object's world box and
-// on the leaf box of every face hit that would enter the answer (leaf_ok).
+// rounded outward (a superset box) tested conservatively in float
+// (box_cons32); the exact test runs where it decides a result: on each
+// object's world box and on the leaf box of every face hit that would enter the answer (leaf_ok).
 // child[k] >= 0: index of the child's record; child[k] < 0: the child is a
 // leaf, ~child[k] = first_item << 2 | count (count 1..3, kdTree.h:6).  Item
 // ranks (DFS-leaf order) are unchanged, so the winner of the lexicographic
@@ -214,33 +214,78 @@ RT_HD bool box_test(const double* lo, const double* hi, const dvec3& o, const dv
   return slab(lo, hi, o, d, a, b);
 }
 
-// Conservative slab on a record entry (float box, superset of the exact
-// one): never rejects a box the exact test accepts, and returns a lower bound
-// of the entry distance and an upper bound of the exit, so pruning with them
-// is safe.  Same reciprocal margins as box_test, minus the exact fallback.
-RT_HD bool box_cons(const DevNode4& nd, int k, const dvec3& o, const dvec3& d, const RayInv& ri, double& a,
-                    double& b) {
-  const double lo[3] = {nd.lo[0][k], nd.lo[1][k], nd.lo[2][k]};
-  const double hi[3] = {nd.hi[0][k], nd.hi[1][k], nd.hi[2][k]};
-  if (!ri.fast) return slab(lo, hi, o, d, a, b);
-  double tmin = -1.0e308, tmax = 1.0e308;
+// the next float toward +inf (finite f; nextafterf has no device version)
+RT_HD float f_succ(float f) {
+  if (f == 0.0f) return 0x1p-149f;
+  const uint32_t u = __builtin_bit_cast(uint32_t, f);
+  return __builtin_bit_cast(float, f > 0.0f ? u + 1u : u - 1u);
+}
+// a float >= x / <= x (x itself when representable)
+RT_HD float f_up(double x) {
+  float f = static_cast<float>(x);
+  if (static_cast<double>(f) < x) f = f_succ(f);
+  return f;
+}
+RT_HD float f_down(double x) {
+  float f = static_cast<float>(x);
+  if (static_cast<double>(f) > x) f = -f_succ(-f);
+  return f;
+}
+
+// Float copy of a ray for the record tests (box_cons32): origin and
+// reciprocal direction rounded to float, and an absolute bound `err` of the
+// error of every per-axis slab distance computed from them in float.  An axis
+// with d == 0 has a NaN origin: its distances are NaN and fminf / fmaxf
+// (IEEE minNum / maxNum) drop them — the axis is skipped, as bbox.cc skips it.
+//   t = fl(fl(lo - fl(o)) * fl(1/d)) = (lo - o)/d + (o - fl(o))/d, times
+//   (1 + eta) with |eta| <= 3.01 * 2^-24, so |t - t_exact| <= 1.01 |o / d|
+//   2^-24 + 3.1 2^-24 |t|.  err = 2^-22 max_q |o_q / d_q| and the relative
+//   2^-21 |t| applied to the result cover that with room (and the 2^-52
+//   relative error of the double slab the exact test computes).
+struct RayF {
+  float ox, oy, oz, ix, iy, iz;
+  float err;  // inf: 1/d overflowed in float — every record entry is hit
+};
+
+RT_HD RayF ray_f(const dvec3& o, const dvec3& d, const RayInv& ri) {
+  RayF r;
+  const float qnan = __builtin_nanf("");
+  double e = 0.0;
+  float* ov[3] = {&r.ox, &r.oy, &r.oz};
+  float* iv[3] = {&r.ix, &r.iy, &r.iz};
 #pragma unroll
-  for (int q = 0; q < 3; ++q) {
-    if (rtm::get(d, q) == 0.0) continue;
-    const double iv = rtm::get(ri.inv, q), oa = rtm::get(o, q);
-    const double t1 = (lo[q] - oa) * iv;
-    const double t2 = (hi[q] - oa) * iv;
-    tmin = fmax(tmin, fmin(t1, t2));
-    tmax = fmin(tmax, fmax(t1, t2));
+  for (int a = 0; a < 3; ++a) {
+    const double da = rtm::get(d, a), oa = rtm::get(o, a);
+    if (da == 0.0) {
+      *ov[a] = qnan;
+      *iv[a] = 0.0f;
+      continue;
+    }
+    const double inv = rtm::get(ri.inv, a);  // 1 / da (ray_inv)
+    *ov[a] = static_cast<float>(oa);
+    *iv[a] = static_cast<float>(inv);
+    const double ea = fabs(oa * inv);
+    e = ea > e ? ea : e;
+    if (!(fabs(inv) < 3.0e38)) e = __builtin_inf();  // 1/d overflows in float
   }
-  const double e1 = 1e-15 * fabs(tmin) + 1e-300, e2 = 1e-15 * fabs(tmax) + 1e-300;
-  // certain miss.  No 1e-8 cut on the exit here (bbox.cc:66-67): a box of
-  // the device's own trees may be tighter than the reference leaf around a
-  // hit with t < 1e-8; leaf_ok applies the reference's cut exactly.
-  if (tmin - e1 > tmax + e2 || tmax + e2 < 0.0) return false;
-  a = tmin - e1;
-  b = tmax + e2;
-  return true;
+  const double eb = e * 0x1p-22;
+  r.err = f_up(eb);
+  return r;
+}
+
+// Conservative slab of a record entry in float (see RayF): never rejects a
+// box the exact test accepts; a <= the exact entry distance, b >= the exit.
+RT_HD bool box_cons32(const DevNode4& nd, int k, const RayF& r, float& a, float& b) {
+  const float t1x = (nd.lo[0][k] - r.ox) * r.ix, t2x = (nd.hi[0][k] - r.ox) * r.ix;
+  const float t1y = (nd.lo[1][k] - r.oy) * r.iy, t2y = (nd.hi[1][k] - r.oy) * r.iy;
+  const float t1z = (nd.lo[2][k] - r.oz) * r.iz, t2z = (nd.hi[2][k] - r.oz) * r.iz;
+  const float tmin = fmaxf(fmaxf(fminf(t1x, t2x), fminf(t1y, t2y)), fminf(t1z, t2z));
+  const float tmax = fminf(fminf(fmaxf(t1x, t2x), fmaxf(t1y, t2y)), fmaxf(t1z, t2z));
+  // (a NaN bound — inf - inf with err = inf — becomes the unbounded one)
+  a = fmaxf(tmin - (r.err + fabsf(tmin) * 0x1p-21f), -__builtin_inff());
+  b = fminf(tmax + (r.err + fabsf(tmax) * 0x1p-21f), __builtin_inff());
+  // (no 1e-8 cut on the exit, as box_cons; leaf_ok applies the reference's)
+  return !(a > b) && !(b < 0.0f);
 }
 
 // ------------------------------------------------------------------ textures

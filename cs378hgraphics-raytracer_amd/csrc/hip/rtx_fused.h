@@ -155,10 +155,9 @@ template <bool FORK>
 __device__ __forceinline__ bool fused_fork_child(LaneRef& LR, const ForkCtx* fk, double* pbuf, size_t nlanes,
                                                  const dvec3& p, const dvec3& d, const dvec3& w, const dvec3& k,
                                                  int depth, int kind, int cpos) {
-  if (!FORK || cpos < 2 || fk->spare_n == 0) return false;
-  const unsigned int idx = atomicAdd(fk->fcnt, 1u);
-  if (idx >= fk->spare_n) return false;
-  const int T = fk->spare_base + static_cast<int>(idx);
+  if (!FORK) return false;
+  const int T = fork_claim(fk, cpos >= 2 && fk->spare_n != 0);
+  if (T < 0) return false;
   LaneRef LT(LR.m, static_cast<size_t>(T));
   fused_put_entry(pbuf + static_cast<size_t>(T), nlanes, p, d, w, k, depth, kind, cpos);
   LT.top() = 1;
@@ -174,7 +173,7 @@ __device__ __forceinline__ bool fused_fork_child(LaneRef& LR, const ForkCtx* fk,
   LT.fpos() = cpos;
   LT.wmask() = 0;
   LT.st() = ST_POP;
-  fk->live_out[atomicAdd(fk->live_cnt, 1u)] = T;
+  fork_join(fk, T);
   return true;
 }
 
@@ -186,17 +185,33 @@ __device__ __forceinline__ bool fused_fork_child(LaneRef& LR, const ForkCtx* fk,
 // trace_kernel<Q_CLOSEST, FUSED> right where a query completes (walks
 // appended to the group's next list) and by the tail kernel (walks at the
 // slot's own record positions, walked by the same lane).
+// The ray of a closest query: pending-stack entry `top` (or, for a sample's
+// first camera ray in the first iteration, regenerated: cam_first_ray).
+struct QRay {
+  dvec3 p, d, W;
+  int64_t code;
+};
+__device__ __forceinline__ QRay qray_at(const LaneRef& LR, const double* __restrict__ pbuf, size_t nlanes) {
+  const double* b = pbuf + static_cast<size_t>(LR.top()) * 13 * nlanes + LR.g;
+  QRay r;
+  r.p = mk3(b[0 * nlanes], b[1 * nlanes], b[2 * nlanes]);
+  r.d = mk3(b[3 * nlanes], b[4 * nlanes], b[5 * nlanes]);
+  r.W = mk3(b[6 * nlanes], b[7 * nlanes], b[8 * nlanes]);
+  r.code = static_cast<int64_t>(b[12 * nlanes]);
+  return r;
+}
+
 template <bool STATS, bool FORK>
 __device__ __forceinline__ void shade_hit(LaneRef& LR, const DevScene& S, const FrameParams& F, Counters& C,
                                           RtxHitRecord* __restrict__ hits, double* __restrict__ pbuf, size_t nlanes,
-                                          int pend_cap, const ForkCtx* fk, const WalkEmit* we, bool have, double bt,
-                                          int bobj, int bsub) {
+                                          int pend_cap, const ForkCtx* fk, const WalkEmit* we, const QRay& qr,
+                                          bool have, double bt, int bobj, int bsub) {
   const RtxRenderParams& P = F.P;
   const double* b = pbuf + static_cast<size_t>(LR.top()) * 13 * nlanes + LR.g;
-  const dvec3 rp = mk3(b[0 * nlanes], b[1 * nlanes], b[2 * nlanes]);
-  const dvec3 rd = mk3(b[3 * nlanes], b[4 * nlanes], b[5 * nlanes]);
-  dvec3 W = mk3(b[6 * nlanes], b[7 * nlanes], b[8 * nlanes]);
-  const int64_t code = static_cast<int64_t>(b[12 * nlanes]);
+  const dvec3 rp = qr.p;
+  const dvec3 rd = qr.d;
+  dvec3 W = qr.W;
+  const int64_t code = qr.code;
   const int dk = static_cast<int>((code & ((int64_t(1) << 40) - 1)) - (int64_t(1) << 39));
   const int pos = static_cast<int>(code >> 40);
   const int rdepth = dk >= 0 ? dk / 4 : -((-dk + 3) / 4);
@@ -319,7 +334,83 @@ struct ShadeArgs {
   int slot_off;    // the group's first slot
   int* live_out;   // this iteration's live list (forked slots join it)
   int out_cnt;     // its counter
+  int cam_n;       // > 0: the first iteration — query k is the first camera
+                   // ray of the group's slot k (cam_first_claim), k < cam_n
 };
+
+// Camera ray k of the sample at (sx, sy), eye pass `pass` (trace(),
+// RayTracer.cpp:35-79: k = 0 the pinhole ray, k >= 1 the DoF lens rays).
+__device__ __forceinline__ void camera_ray(const FrameParams& F, int pass, int k, double sx, double sy, dvec3& rp,
+                                           dvec3& rd) {
+  const RtxRenderParams& P = F.P;
+  const RtxCamera& cam = F.cam;
+  const dvec3 eye = pass ? ld3(cam.eye) + mk3(0.25, 0.0, 0.0) : ld3(cam.eye);
+  const double x = sx - 0.5, y = sy - 0.5;
+  const dvec3 cdir = rtm::normalize(ld3(cam.look) + x * ld3(cam.u) + y * ld3(cam.v));
+  rp = eye;
+  rd = cdir;
+  if (k > 0) {
+    const double fd = rtm::gmax(P.dof_fd, 1.0);
+    const dvec3 fp_n = -cdir;
+    const dvec3 fp_pt = rtm::ray_at(eye, cdir, fd);
+    double t = rtm::dot(fp_n, cdir);
+    t = rtm::dot(fp_pt - eye, fp_n) / t;
+    const dvec3 dest = rtm::ray_at(eye, cdir, t);
+    rp = eye + ld3(&F.offv[(k - 1) * 3]);
+    rd = rtm::normalize(dest - rp);
+  }
+}
+// ST_CAM's next camera ray: the ray, the hit-record default of a sample's
+// first ray, camk advanced
+__device__ __forceinline__ void cam_start(LaneRef& LR, const FrameParams& F, RtxHitRecord* __restrict__ hits,
+                                          dvec3& rp, dvec3& rd) {
+  const int k = LR.camk();
+  camera_ray(F, LR.pass(), k, LR.sx(), LR.sy(), rp, rd);
+  if (k == 0) {
+    LR.first_query() = LR.rec_on() && LR.pass() == 0;
+    if (LR.first_query()) {  // default record: miss (also what depth < 0 leaves)
+      RtxHitRecord* hr = &hits[LR.sample_slot()];
+      hr->object = hr->face = hr->scene_leaf = hr->mesh_leaf = -1;
+      hr->t = 1000.0;
+      hr->pad = 0;
+    }
+  } else {
+    LR.first_query() = false;
+  }
+  LR.camk() = k + 1;
+}
+
+// First iteration of a fused frame (trace_kernel<Q_CLOSEST, FUSED> with
+// cam_n > 0): the kernel claims the slot's first sample itself and queries
+// its first camera ray straight away — what advance_fused (claim, ST_CAM,
+// ST_POP) would have done, without the pending-stack entry and the query
+// record round trip.  False: the slot has no sample (left idle).
+// (out of line: inlined into the persistent closest-hit kernel its registers
+// add to the traversal's peak)
+template <bool STATS>
+__device__ __noinline__ bool cam_first_claim(LaneRef& LR, const FrameParams& F, Counters& C,
+                                             RtxHitRecord* __restrict__ hits, int slot, QRay& qr) {
+  lane_init(LR);
+  claim_sample(LR, F, hits, slot);
+  if (LR.st() == ST_IDLE) return false;
+  cam_start(LR, F, hits, qr.p, qr.d);
+  if (STATS) C.camera++;
+  qr.W = mk3(1.0, 1.0, 1.0);
+  qr.code = static_cast<int64_t>(pend_code(F.fork_on ? 1 : 0, F.P.depth, 0));
+  LR.top() = 0;     // the ray's own entry (never written: shading overwrites it with the children)
+  LR.nrays()++;     // ST_POP
+  LR.qmode() = Q_CLOSEST;
+  LR.st() = ST_HIT;
+  return true;
+}
+// its ray again at shading time (the walk's registers are reused meanwhile)
+__device__ __forceinline__ QRay cam_first_ray(const LaneRef& LR, const FrameParams& F) {
+  QRay qr;
+  camera_ray(F, LR.pass(), LR.camk() - 1, LR.sx(), LR.sy(), qr.p, qr.d);
+  qr.W = mk3(1.0, 1.0, 1.0);
+  qr.code = static_cast<int64_t>(pend_code(F.fork_on ? 1 : 0, F.P.depth, 0));
+  return qr;
+}
 
 // The fused state machine (CAM -> POP): runs until the lane needs a
 // closest-hit query (Q_CLOSEST: the ray is pending-stack entry `top`), has to
@@ -392,31 +483,8 @@ __device__ __forceinline__ void advance_fused(LaneRef& LR, const DevScene& S, co
           LR.st() = ST_IDLE;
           break;
         }
-        const RtxCamera& cam = F.cam;
-        const dvec3 eye = LR.pass() ? ld3(cam.eye) + mk3(0.25, 0.0, 0.0) : ld3(cam.eye);
-        const double x = LR.sx() - 0.5, y = LR.sy() - 0.5;
-        const dvec3 cdir = rtm::normalize(ld3(cam.look) + x * ld3(cam.u) + y * ld3(cam.v));
-        dvec3 rp = eye, rd = cdir;
-        if (LR.camk() == 0) {
-          LR.first_query() = LR.rec_on() && LR.pass() == 0;
-          if (LR.first_query()) {  // default record: miss (also what depth < 0 leaves)
-            RtxHitRecord* hr = &hits[LR.sample_slot()];
-            hr->object = hr->face = hr->scene_leaf = hr->mesh_leaf = -1;
-            hr->t = 1000.0;
-            hr->pad = 0;
-          }
-        } else {
-          const double fd = rtm::gmax(P.dof_fd, 1.0);
-          const dvec3 fp_n = -cdir;
-          const dvec3 fp_pt = rtm::ray_at(eye, cdir, fd);
-          double t = rtm::dot(fp_n, cdir);
-          t = rtm::dot(fp_pt - eye, fp_n) / t;
-          const dvec3 dest = rtm::ray_at(eye, cdir, t);
-          rp = eye + ld3(&F.offv[(LR.camk() - 1) * 3]);
-          rd = rtm::normalize(dest - rp);
-          LR.first_query() = false;
-        }
-        LR.camk()++;
+        dvec3 rp, rd;
+        cam_start(LR, F, hits, rp, rd);
         if (STATS) C.camera++;
         LR.top() = 0;
         fused_push(LR, pbuf, nlanes, rp, rd, mk3(1, 1, 1), mk3(1, 1, 1), P.depth, 0, F.fork_on ? 1 : 0);
@@ -475,12 +543,15 @@ __global__ void __launch_bounds__(WG, RTX_FUSED_ADV_WAVES)
                          int* __restrict__ live_out, int first, int in_cnt, int out_cnt) {
   const FrameParams& F = *Fp;
   const int tid = blockIdx.x * WG + threadIdx.x;
-  const bool valid = first || tid < static_cast<int>(counters[in_cnt]);
-  const int slot = first ? slot_off + tid : (valid ? live_in[tid] : slot_off);
+  // first: 1 every slot of the group, initialised here; 2 every slot (the
+  // iteration after the first closest-hit launch claimed the samples, which
+  // keeps no live list); 0 the live list
+  const bool valid = first == 1 || (first == 2 ? tid < F.wf_gs : tid < static_cast<int>(counters[in_cnt]));
+  const int slot = first ? slot_off + (valid ? tid : 0) : (valid ? live_in[tid] : slot_off);
   const int lane = threadIdx.x & 63;
   Counters C = {0, 0, 0, 0, 0, 0, 0};
   LaneRef L(lm, static_cast<size_t>(slot));
-  if (first) lane_init(L);
+  if (first == 1) lane_init(L);
   int qm = Q_NONE;
   if (valid && (L.st() != ST_IDLE || slot_unit(F, slot, L.kdone()) >= 0)) {
     flush_terms(L, F);
@@ -616,7 +687,8 @@ __global__ void __launch_bounds__(WG) tail_fused_kernel(DevScene S, const DevSce
         sq = bsub;
       }
     } else {
-      shade_hit<STATS, false>(L, SS, F, C, hits, pbuf, lm.n, pend_cap, nullptr, &we, have, bt, bobj, bsub);
+      shade_hit<STATS, false>(L, SS, F, C, hits, pbuf, lm.n, pend_cap, nullptr, &we, qray_at(L, pbuf, lm.n), have, bt,
+                              bobj, bsub);
       todo = static_cast<unsigned int>(L.wmask());
     }
   }

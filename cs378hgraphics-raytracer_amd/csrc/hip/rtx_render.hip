@@ -617,6 +617,42 @@ struct ForkCtx {
   unsigned int* live_cnt;
 };
 
+// lanes of the wave below the calling lane in `mask` (mbcnt)
+__device__ __forceinline__ unsigned int lane_prefix(unsigned long long mask) {
+  return __builtin_amdgcn_mbcnt_hi(static_cast<unsigned int>(mask >> 32),
+                                   __builtin_amdgcn_mbcnt_lo(static_cast<unsigned int>(mask), 0u));
+}
+
+// A fork slot for each calling lane with `want`, or -1 (none left / not
+// wanted).  Wave-aggregated — one atomic on the group's fork counter per call
+// per wave, offsets by mbcnt — and called from divergent code: the ballot
+// covers the lanes executing it.  (Per-lane atomics on the one counter
+// serialised in L2: the shading step of a shard's first iteration forks
+// hundreds of thousands of sub-trees.)
+__device__ __forceinline__ int fork_claim(const ForkCtx* fk, bool want) {
+  const unsigned long long m = __ballot(want);
+  if (m == 0ull) return -1;
+  const int leader = __builtin_ctzll(m);
+  unsigned int base = 0;
+  if (static_cast<int>(threadIdx.x & 63) == leader) base = atomicAdd(fk->fcnt, static_cast<unsigned int>(__popcll(m)));
+  base = __shfl(base, leader);
+  if (!want) return -1;
+  const unsigned int idx = base + lane_prefix(m);
+  return idx < fk->spare_n ? fk->spare_base + static_cast<int>(idx) : -1;
+}
+// append fork slot T (lanes with T >= 0) to the iteration's live list,
+// wave-aggregated like fork_claim
+__device__ __forceinline__ void fork_join(const ForkCtx* fk, int T) {
+  const unsigned long long m = __ballot(T >= 0);
+  if (m == 0ull) return;
+  const int leader = __builtin_ctzll(m);
+  unsigned int base = 0;
+  if (static_cast<int>(threadIdx.x & 63) == leader)
+    base = atomicAdd(fk->live_cnt, static_cast<unsigned int>(__popcll(m)));
+  base = __shfl(base, leader);
+  if (T >= 0) fk->live_out[base + lane_prefix(m)] = T;
+}
+
 // pending-ray entry field 12: bucket (the ray's heap position if it is a
 // node, else its nearest node ancestor's; 0 without buckets), depth and kind
 // (0 camera, 1 reflection, 2 refraction), exact in a double
@@ -684,10 +720,9 @@ __device__ __forceinline__ void advance_lane(LaneRef& LR, const DevScene& S, con
   // the own stack
   auto fork_child = [&](const dvec3& p, const dvec3& d, const dvec3& w, const dvec3& k, int depth, int kind,
                         int cpos) -> bool {
-    if (!FORK || cpos < 2 || fk->spare_n == 0) return false;
-    const unsigned int idx = atomicAdd(fk->fcnt, 1u);
-    if (idx >= fk->spare_n) return false;
-    const int T = fk->spare_base + static_cast<int>(idx);
+    if (!FORK) return false;
+    const int T = fork_claim(fk, cpos >= 2 && fk->spare_n != 0);
+    if (T < 0) return false;
     LaneRef LT(LR.m, static_cast<size_t>(T));
     put_entry(pbuf + static_cast<size_t>(T), p, d, w, k, depth, kind, cpos);
     LT.top() = 1;
@@ -703,7 +738,7 @@ __device__ __forceinline__ void advance_lane(LaneRef& LR, const DevScene& S, con
     LT.fpos() = cpos;
     LT.dret() = DISC_NONE;
     LT.st() = ST_POP;
-    fk->live_out[atomicAdd(fk->live_cnt, 1u)] = T;
+    fork_join(fk, T);
     return true;
   };
   // traceRay's reflection / refraction (RayTracer.cpp:127-164); m_out =
@@ -1448,11 +1483,6 @@ struct QList {
 #define CNT_DONE (7 * CNT_LINE)  // workgroups of the iteration's last kernel that finished
 #define CNT_PER_GROUP (8 * CNT_LINE)
 
-__device__ __forceinline__ unsigned int lane_prefix(unsigned long long mask) {
-  return __builtin_amdgcn_mbcnt_hi(static_cast<unsigned int>(mask >> 32),
-                                   __builtin_amdgcn_mbcnt_lo(static_cast<unsigned int>(mask), 0u));
-}
-
 // A slot's next statically dealt work unit, or -1: none left, or a fork
 // slot.  Runs of 64 consecutive units (one wave's worth of neighbouring
 // samples) are dealt to the groups round-robin, so every group gets a share
@@ -1806,7 +1836,8 @@ __global__ void __launch_bounds__(WG, !FUSED ? RTX_TRACE_WAVES : (MODE == Q_CLOS
     S.mhot = lds_nodes + ns;
   }
 #endif
-  const unsigned int nq = counters[CNT_Q + (MODE - 1) * CNT_LINE];
+  const bool cam = FUSED && MODE == Q_CLOSEST && SA.cam_n > 0;  // first iteration: claims + camera rays here
+  const unsigned int nq = cam ? static_cast<unsigned int>(SA.cam_n) : counters[CNT_Q + (MODE - 1) * CNT_LINE];
   unsigned int* claim = counters + CNT_CLAIM + (MODE - 1) * CNT_LINE;
 #ifdef RTX_EARLYOUT
   using Blk = typename std::conditional<MODE == Q_NEXT, ShadowBlocker, NoBlocker>::type;
@@ -1902,10 +1933,11 @@ __global__ void __launch_bounds__(WG, !FUSED ? RTX_TRACE_WAVES : (MODE == Q_CLOS
         const ForkCtx fk = {counters + CNT_FORK, SA.slot_off + F.wf_gsamp, static_cast<unsigned int>(F.wf_gs - F.wf_gsamp),
                             SA.live_out, counters + SA.out_cnt};
         const WalkEmit we = {SA.qn, counters + CNT_Q + CNT_LINE, -1, 0};
-        LaneRef LR(lm, static_cast<size_t>(Q.slot[kq]));
+        LaneRef LR(lm, static_cast<size_t>(cam ? SA.slot_off + static_cast<int>(kq) : Q.slot[kq]));
+        const QRay qr = cam ? cam_first_ray(LR, F) : qray_at(LR, SA.pbuf, lm.n);
         // the scene through the device copy: indexing the by-value kernel
         // argument (cube-map faces) would copy all of it to scratch
-        shade_hit<STATS, FORK>(LR, *Sg, F, C, SA.hits, SA.pbuf, lm.n, SA.pend_cap, &fk, &we, have, bt, bo, bs);
+        shade_hit<STATS, FORK>(LR, *Sg, F, C, SA.hits, SA.pbuf, lm.n, SA.pend_cap, &fk, &we, qr, have, bt, bo, bs);
         pend = false;
       }
     }
@@ -1929,11 +1961,18 @@ __global__ void __launch_bounds__(WG, !FUSED ? RTX_TRACE_WAVES : (MODE == Q_CLOS
       const unsigned int take = avail < nidle ? avail : nidle;
       if (!active && !pend && rank < take) {
         kq = static_cast<size_t>(qnext) + rank;
+        bool noq = false;
         if (!FUSED) {
           const dvec3 P = mk3(Q.d[0 * cap + kq], Q.d[1 * cap + kq], Q.d[2 * cap + kq]);
           const dvec3 D = mk3(Q.d[3 * cap + kq], Q.d[4 * cap + kq], Q.d[5 * cap + kq]);
           active = trav_init<STATS, MODE>(T, S, P, D, Q.d[6 * cap + kq], Q.iv[0 * cap + kq], Q.iv[1 * cap + kq],
                                           Q.d[7 * cap + kq], MODE == Q_NEXT ? Q.d[8 * cap + kq] : -RTX_INF, C);
+        } else if (MODE == Q_CLOSEST && cam) {  // claim the slot's first sample, its first camera ray
+          const int slot = SA.slot_off + static_cast<int>(kq);
+          LaneRef LR(lm, static_cast<size_t>(slot));
+          QRay qr;
+          noq = !cam_first_claim<STATS>(LR, *SA.Fp, C, SA.hits, slot, qr);
+          if (!noq) active = trav_init<STATS, MODE>(T, S, qr.p, qr.d, -RTX_INF, -1, -1, RTX_INF, -RTX_INF, C);
         } else if (MODE == Q_CLOSEST) {  // fused closest record: the ray only
           const dvec3 P = mk3(Q.d[0 * cap + kq], Q.d[1 * cap + kq], Q.d[2 * cap + kq]);
           const dvec3 D = mk3(Q.d[3 * cap + kq], Q.d[4 * cap + kq], Q.d[5 * cap + kq]);
@@ -1946,7 +1985,7 @@ __global__ void __launch_bounds__(WG, !FUSED ? RTX_TRACE_WAVES : (MODE == Q_CLOS
           active = trav_init<STATS, MODE>(T, S, pb, light_dir(L, pb), -RTX_INF, -1, -1, qlim, qblk, C);
         }
         if (!active) {
-          if (FUSED) pend = true;
+          if (FUSED) pend = !noq;  // (a slot without a sample: nothing to shade)
           else finish();
         }
       }
@@ -1998,6 +2037,16 @@ __global__ void __launch_bounds__(WG, !FUSED ? RTX_TRACE_WAVES : (MODE == Q_CLOS
       }
     }
   }
+}
+
+// Slots [first, first + n) start idle (lane_init): on a frame whose first
+// closest-hit launch claims the samples (cam_first_claim), the slots it does
+// not claim — spare (fork) slots and sample slots without a first sample.
+__global__ void __launch_bounds__(WG) lane_init_kernel(LaneMem lm, int first, int n) {
+  const int t = blockIdx.x * WG + threadIdx.x;
+  if (t >= n) return;
+  LaneRef L(lm, static_cast<size_t>(first + t));
+  lane_init(L);
 }
 
 // Per-pixel ordered reduction of the sample buffer (RayTracer.cpp:288-298:
@@ -2833,6 +2882,26 @@ rtx_status rtx_render(void* scene, const RtxRenderParams* params, uint8_t* rgb8,
     const char* ti_env = getenv("RTX_TAIL_ITER");
     if (ti_env) tail_iter = atoi(ti_env);
     F.qchunk = 64;
+    // First iteration without an advance launch (fused frames): the closest-
+    // hit launch claims each sample slot's first sample and queries its first
+    // camera ray itself (cam_first_claim).  cam_n[g]: the group's sample
+    // slots with a first unit (slot_unit(kdone 0) is increasing in the slot,
+    // so they are a prefix).  RTX_CAM_FIRST=0: the advance launch (A/B).
+    bool cam_first = fuse && params->depth >= 0;
+    {
+      const char* e = getenv("RTX_CAM_FIRST");
+      if (e && atoi(e) == 0) cam_first = false;
+    }
+    std::vector<int> cam_n(size_t(G), 0);
+    for (int g = 0; g < G && cam_first; ++g) {
+      int64_t c = 0;
+      for (int64_t b = 0; b * 64 < gsamp; ++b) {
+        const int64_t base = (b * G + g) * 64;
+        if (base >= F.n_samples) break;
+        c += std::min<int64_t>(std::min<int64_t>(64, gsamp - b * 64), F.n_samples - base);
+      }
+      cam_n[size_t(g)] = static_cast<int>(c);
+    }
     HIP_TRY(hipMemcpyAsync(st->d_frame, &F, sizeof(FrameParams), hipMemcpyHostToDevice, stream));
     // every slot starts ST_IDLE, kdone = 0, outside a discoverMat walk, no
     // deferred colour: set by the group's first advance_kernel, which visits
@@ -2879,7 +2948,10 @@ rtx_status rtx_render(void* scene, const RtxRenderParams* params, uint8_t* rgb8,
         unsigned int* cnt = st->d_counters + CNT_PER_GROUP * g;
         const QList& q0 = ql[size_t(g) * 2];
         const QList& q1 = ql[size_t(g) * 2 + 1];
-        if (it > 0 && (live_bound[size_t(g)] <= tail_slots || (tail_iter > 0 && it >= tail_iter))) {
+        // (after a claiming first launch, iteration 1 visits every slot by
+        // index and writes the first live list: no tail before iteration 2)
+        if (it > (cam_first ? 1 : 0) &&
+            (live_bound[size_t(g)] <= tail_slots || (tail_iter > 0 && it >= tail_iter))) {
           // few slots left: finish them in one persistent launch
           const bool odd = (it & 1) != 0;  // this iteration would read the list the last one wrote
           const int in_cnt = odd ? CNT_ALIVE_A : CNT_ALIVE_B;
@@ -2918,11 +2990,20 @@ rtx_status rtx_render(void* scene, const RtxRenderParams* params, uint8_t* rgb8,
         // the first); this iteration's clears the next one's: even
         // iterations use lines 0-4 (out-count A), odd ones lines 1-5 (B)
         const int clr_next = odd ? 0 : 1;
-        const int first = it == 0 ? 1 : 0;
+        // advance mode: 1 init + every slot, 2 every slot (after a claiming
+        // first launch), 0 the live list
+        const int first = it == 0 ? 1 : (cam_first && it == 1 ? 2 : 0);
         const int64_t lb = grid_bound[size_t(g)];
         const int64_t agrid = first ? per : std::max<int64_t>(1, std::min<int64_t>(per, (lb + WG - 1) / WG));
         const int64_t tg = std::max<int64_t>(1, std::min<int64_t>(tgrid, (lb + WG - 1) / WG));
-        if (fuse) {
+        const bool cam_it = cam_first && it == 0;
+        if (cam_it) {
+          // the slots the first launch does not claim start idle
+          const int n0 = static_cast<int>(gslots) - cam_n[size_t(g)];
+          if (n0 > 0)
+            hipLaunchKernelGGL(lane_init_kernel, dim3((n0 + WG - 1) / WG), dim3(WG), 0, sg, A,
+                               static_cast<int>(g * gslots) + cam_n[size_t(g)], n0);
+        } else if (fuse) {
           dispatch2(stats, fork, [&](auto st_, auto fk_) {
             hipLaunchKernelGGL((advance_fused_kernel<decltype(st_)::value, decltype(fk_)::value>), dim3(agrid),
                                dim3(WG), 0, sg, S, st->d_scene, st->d_frame, A, sb, d_hits, st->d_pbuf, pend_cap, q0,
@@ -2951,6 +3032,7 @@ rtx_status rtx_render(void* scene, const RtxRenderParams* params, uint8_t* rgb8,
           sa.slot_off = static_cast<int>(g * gslots);
           sa.live_out = live_out;
           sa.out_cnt = out_cnt;
+          sa.cam_n = cam_it ? cam_n[size_t(g)] : 0;
         }
         dispatch2(stats, fork, [&](auto st_, auto fk_) {
           constexpr bool ST_ = decltype(st_)::value, FK_ = decltype(fk_)::value;

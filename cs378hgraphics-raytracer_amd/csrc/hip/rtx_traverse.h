@@ -47,7 +47,9 @@ namespace rtxd {
 // whole walk: T.blocked, shadow attenuation 0.
 struct Trav {
   dvec3 P, D;
-  RayInv ri;
+  RayInv ri;  // exact-fallback reciprocal: the root and the objects' world boxes
+  RayF rf;    // float tests of the records being walked: the scene's, or in
+              // mode 2 the mesh's (local frame); reset when the mesh is done
   double tp, tlimit, tlo, tblock;
   int rp, sq;
   // answer so far
@@ -59,7 +61,6 @@ struct Trav {
   int sp, ref, mode, oc, oe;
   // mesh context (local frame of object moi)
   dvec3 lp, ld;
-  RayInv lri;
   double len, mbest;
   int moi, mbase, mfoff, mnoff, mface;
   bool mhave;
@@ -93,17 +94,19 @@ RT_HD bool leaf_ok(const Trav& T, const DevScene& S, int f) {
 // other hits farthest first, so the walk stays near-first.  False if no
 // entry was hit (the caller pops).
 template <bool STATS>
-RT_HD bool visit4(const DevNode4& nd, const dvec3& o, const dvec3& d, const RayInv& ri, const double hi,
-                  const double lo, int* __restrict__ stk, const int lane, int& sp, int& ref, Counters& C) {
-  const double NOHIT = __builtin_inf();
-  double a0 = NOHIT, a1 = NOHIT, a2 = NOHIT, a3 = NOHIT;
+RT_HD bool visit4(const DevNode4& nd, const RayF& rf, const double hi, const double lo, int* __restrict__ stk,
+                  const int lane, int& sp, int& ref, Counters& C) {
+  const float NOHIT = __builtin_inff();
+  // prune bounds widened to floats (hi up, lo down): pruning stays safe
+  const float hf = f_up(hi), lf = f_down(lo);
+  float a0 = NOHIT, a1 = NOHIT, a2 = NOHIT, a3 = NOHIT;
   int r0 = 0, r1 = 0, r2 = 0, r3 = 0;
   const int cnt = nd.count;
-  auto test = [&](int k, double& ak, int& rk) {
+  auto test = [&](int k, float& ak, int& rk) {
     if (k < cnt) {
       if (STATS) C.nodes++;
-      double ta, tb;
-      if (box_cons(nd, k, o, d, ri, ta, tb) && !(ta > hi) && !(tb < lo)) {
+      float ta, tb;
+      if (box_cons32(nd, k, rf, ta, tb) && !(ta > hf) && !(tb < lf)) {
         ak = ta;
         rk = nd.child[k];
       }
@@ -114,9 +117,9 @@ RT_HD bool visit4(const DevNode4& nd, const dvec3& o, const dvec3& d, const RayI
   test(2, a2, r2);
   test(3, a3, r3);
   // sorting network on (entry distance, ref)
-  auto cs = [](double& x, int& rx, double& y, int& ry) {
+  auto cs = [](float& x, int& rx, float& y, int& ry) {
     const bool s = y < x;
-    const double lo_ = s ? y : x, hi_ = s ? x : y;
+    const float lo_ = s ? y : x, hi_ = s ? x : y;
     const int rlo = s ? ry : rx, rhi = s ? rx : ry;
     x = lo_;
     y = hi_;
@@ -157,6 +160,7 @@ RT_HD bool trav_init(Trav& T, const DevScene& S, const dvec3& P, const dvec3& D,
   if (S.n_snodes == 0) return false;
   T.tlo = QMODE == Q_CLOSEST ? -RTX_INF : tp - S.margin;  // Q_ANY: tp = -inf for a closest query
   T.ri = ray_inv(D);
+  T.rf = ray_f(P, D, T.ri);
   if (STATS) C.nodes++;
   double a, b;
   if (!box_test(S.sroot.lo, S.sroot.hi, P, D, T.ri, a, b) || a > T.bt + S.margin || b < T.tlo) return false;
@@ -167,8 +171,6 @@ RT_HD bool trav_init(Trav& T, const DevScene& S, const dvec3& P, const dvec3& D,
   T.oe = 0;
   T.lp = mk3(0, 0, 0);
   T.ld = mk3(0, 0, 0);
-  T.lri.inv = mk3(0, 0, 0);
-  T.lri.fast = true;
   T.len = 1.0;
   T.mbest = RTX_INF;
   T.moi = 0;
@@ -184,8 +186,9 @@ RT_HD bool trav_init(Trav& T, const DevScene& S, const dvec3& P, const dvec3& D,
 // the walk's registers as free between queries.
 RT_HD void trav_reset(Trav& T) {
   T.P = T.D = T.lp = T.ld = mk3(0.0, 0.0, 0.0);
-  T.ri.inv = T.lri.inv = mk3(0.0, 0.0, 0.0);
-  T.ri.fast = T.lri.fast = true;
+  T.ri.inv = mk3(0.0, 0.0, 0.0);
+  T.ri.fast = true;
+  T.rf = RayF{0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   T.tp = T.tlimit = T.tlo = T.tblock = T.bt = T.len = T.mbest = 0.0;
   T.rp = T.sq = T.bobj = T.bsub = T.sp = T.ref = T.mode = T.oc = T.oe = 0;
   T.moi = T.mbase = T.mfoff = T.mnoff = T.mface = 0;
@@ -207,7 +210,7 @@ RT_HD bool trav_step(Trav& T, const DevScene& S, int* __restrict__ stk, const in
   int& ref = T.ref;
   if (T.mode == 0) {
     if (ref >= 0) {
-      if (visit4<STATS>(S.snode4[ref], T.P, T.D, T.ri, bt + S.margin, tlo, stk, lane, sp, ref, C)) return false;
+      if (visit4<STATS>(S.snode4[ref], T.rf, bt + S.margin, tlo, stk, lane, sp, ref, C)) return false;
       if (sp == 0) return true;
       --sp;
       ref = stk[sp * 64 + lane];
@@ -241,7 +244,7 @@ RT_HD bool trav_step(Trav& T, const DevScene& S, int* __restrict__ stk, const in
           if (box_test(mr.lo, mr.hi, pos, dir, mri, ma, mb) && !(ma > whi) && !(mb < lo)) {
             T.lp = pos;
             T.ld = dir;
-            T.lri = mri;
+            T.rf = ray_f(pos, dir, mri);
             T.len = ln;
             T.moi = oi;
             T.mbase = sp;
@@ -430,7 +433,7 @@ RT_HD bool trav_step(Trav& T, const DevScene& S, int* __restrict__ stk, const in
   if (closest && T.mhave) hi = rtm::gmin(hi, T.mbest + S.lmargin);
   const double lo = closest ? -RTX_INF : tlo * len * (1.0 - 1e-12) - S.lmargin;
   if (ref >= 0) {
-    if (visit4<STATS>((ref < S.n_mhot ? S.mhot : S.mnode4)[ref], T.lp, T.ld, T.lri, hi, lo, stk, lane, sp, ref, C))
+    if (visit4<STATS>((ref < S.n_mhot ? S.mhot : S.mnode4)[ref], T.rf, hi, lo, stk, lane, sp, ref, C))
       return false;
   } else {
     const int code = ~ref;
@@ -478,6 +481,7 @@ RT_HD bool trav_step(Trav& T, const DevScene& S, int* __restrict__ stk, const in
     return false;
   }
   // mesh finished: Trimesh::intersectLocal's result enters Scene::intersect
+  T.rf = ray_f(T.P, T.D, T.ri);
   if (closest && T.mhave) {
     const double tw = T.mbest / len;
     if (!have || tw < bt || (tw == bt && T.moi < bobj)) {
