@@ -234,57 +234,67 @@ RT_HD float f_down(double x) {
 
 // Float copy of a ray for the record tests (box_cons32): origin and
 // reciprocal direction rounded to float, and an absolute bound `err` of the
-// error of every per-axis slab distance computed from them in float.  An axis
-// with d == 0 has a NaN origin: its distances are NaN and fminf / fmaxf
-// (IEEE minNum / maxNum) drop them — the axis is skipped, as bbox.cc skips it.
+// error of every per-axis slab distance computed from them in float:
 //   t = fl(fl(lo - fl(o)) * fl(1/d)) = (lo - o)/d + (o - fl(o))/d, times
 //   (1 + eta) with |eta| <= 3.01 * 2^-24, so |t - t_exact| <= 1.01 |o / d|
 //   2^-24 + 3.1 2^-24 |t|.  err = 2^-22 max_q |o_q / d_q| and the relative
 //   2^-21 |t| applied to the result cover that with room (and the 2^-52
 //   relative error of the double slab the exact test computes).
+// An axis with d == 0 (or 1/d past the float range) is an inside test
+// instead: inv = +inf, the entry side's origin rounded up past o and the
+// exit side's down (olo > o > ohi strictly), so its slab is (-inf, +inf)
+// when lo <= o <= hi and empty otherwise.  That is NOT bbox.cc's rule (it
+// skips the axis) but the conservative one for the device's own trees: their
+// boxes only steer the walk and must contain every hit point, and a hit of
+// such a ray has P.x == o.x exactly (DESIGN.md "Float record tests").
+// Skipping the axis made every such ray — the image column whose direction
+// has x == 0 — visit thousands of records.
 struct RayF {
-  float ox, oy, oz, ix, iy, iz;
-  float err;  // inf: 1/d overflowed in float — every record entry is hit
+  float olo[3], ohi[3], inv[3];
+  float err;
 };
 
 RT_HD RayF ray_f(const dvec3& o, const dvec3& d, const RayInv& ri) {
   RayF r;
-  const float qnan = __builtin_nanf("");
   double e = 0.0;
-  float* ov[3] = {&r.ox, &r.oy, &r.oz};
-  float* iv[3] = {&r.ix, &r.iy, &r.iz};
 #pragma unroll
   for (int a = 0; a < 3; ++a) {
     const double da = rtm::get(d, a), oa = rtm::get(o, a);
-    if (da == 0.0) {
-      *ov[a] = qnan;
-      *iv[a] = 0.0f;
+    const double inv = rtm::get(ri.inv, a);  // 1 / da (ray_inv), 0 for da == 0
+    if (da == 0.0 || !(fabs(inv) < 3.0e38)) {
+      const double dl = fabs(oa) * 0x1p-23 + 1e-30;
+      r.olo[a] = f_up(oa + dl);
+      r.ohi[a] = f_down(oa - dl);
+      r.inv[a] = __builtin_inff();
       continue;
     }
-    const double inv = rtm::get(ri.inv, a);  // 1 / da (ray_inv)
-    *ov[a] = static_cast<float>(oa);
-    *iv[a] = static_cast<float>(inv);
+    r.olo[a] = r.ohi[a] = static_cast<float>(oa);
+    r.inv[a] = static_cast<float>(inv);
     const double ea = fabs(oa * inv);
     e = ea > e ? ea : e;
-    if (!(fabs(inv) < 3.0e38)) e = __builtin_inf();  // 1/d overflows in float
   }
-  const double eb = e * 0x1p-22;
-  r.err = f_up(eb);
+  r.err = f_up(e * 0x1p-22);
   return r;
 }
 
 // Conservative slab of a record entry in float (see RayF): never rejects a
-// box the exact test accepts; a <= the exact entry distance, b >= the exit.
+// box containing a hit point of the ray; a <= the entry distance, b >= the
+// exit distance.
 RT_HD bool box_cons32(const DevNode4& nd, int k, const RayF& r, float& a, float& b) {
-  const float t1x = (nd.lo[0][k] - r.ox) * r.ix, t2x = (nd.hi[0][k] - r.ox) * r.ix;
-  const float t1y = (nd.lo[1][k] - r.oy) * r.iy, t2y = (nd.hi[1][k] - r.oy) * r.iy;
-  const float t1z = (nd.lo[2][k] - r.oz) * r.iz, t2z = (nd.hi[2][k] - r.oz) * r.iz;
+  const float t1x = (nd.lo[0][k] - r.olo[0]) * r.inv[0], t2x = (nd.hi[0][k] - r.ohi[0]) * r.inv[0];
+  const float t1y = (nd.lo[1][k] - r.olo[1]) * r.inv[1], t2y = (nd.hi[1][k] - r.ohi[1]) * r.inv[1];
+  const float t1z = (nd.lo[2][k] - r.olo[2]) * r.inv[2], t2z = (nd.hi[2][k] - r.ohi[2]) * r.inv[2];
   const float tmin = fmaxf(fmaxf(fminf(t1x, t2x), fminf(t1y, t2y)), fminf(t1z, t2z));
   const float tmax = fminf(fminf(fmaxf(t1x, t2x), fmaxf(t1y, t2y)), fmaxf(t1z, t2z));
-  // (a NaN bound — inf - inf with err = inf — becomes the unbounded one)
-  a = fmaxf(tmin - (r.err + fabsf(tmin) * 0x1p-21f), -__builtin_inff());
-  b = fminf(tmax + (r.err + fabsf(tmax) * 0x1p-21f), __builtin_inff());
-  // (no 1e-8 cut on the exit, as box_cons; leaf_ok applies the reference's)
+  // (err is finite; an infinite bound stays infinite, a miss stays a miss)
+  a = tmin - (r.err + fabsf(tmin) * 0x1p-21f);
+  b = tmax + (r.err + fabsf(tmax) * 0x1p-21f);
+  // inf - inf (an inside-test axis): the infinite bound itself — entry at
+  // +inf or exit at -inf, a miss either way
+  if (!(a == a)) a = tmin;
+  if (!(b == b)) b = tmax;
+  // (no 1e-8 cut on the exit, as the double slab had none here; leaf_ok
+  // applies the reference's)
   return !(a > b) && !(b < 0.0f);
 }
 

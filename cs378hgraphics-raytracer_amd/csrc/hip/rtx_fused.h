@@ -336,6 +336,8 @@ struct ShadeArgs {
   int out_cnt;     // its counter
   int cam_n;       // > 0: the first iteration — query k is the first camera
                    // ray of the group's slot k (cam_first_claim), k < cam_n
+  int leaf_k;      // object / leaf units wait while >= leaf_k lanes are at a
+                   // record (trace_kernel; 65: never)
 };
 
 // Camera ray k of the sample at (sx, sy), eye pass `pass` (trace(),

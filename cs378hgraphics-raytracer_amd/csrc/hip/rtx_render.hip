@@ -1995,11 +1995,18 @@ __global__ void __launch_bounds__(WG, !FUSED ? RTX_TRACE_WAVES : (MODE == Q_CLOS
     if (__ballot(active || pend) == 0ull) break;  // nothing claimed and nothing left
     const int thresh = exhausted ? 1 : RTX_REFILL;
     do {
+      // Postponed costly units (Aila & Laine's while-while, one call site):
+      // while at least leaf_k lanes of the wave are at a 4-wide record, only
+      // those lanes step, so most steps run the record test alone instead of
+      // the record test AND the object / face tests of a mixed wave.  A
+      // lane's own sequence of units is unchanged (results identical).
+      const unsigned long long at_rec = __ballot(active && trav_at_record(T));
+      const bool go = active && (static_cast<int>(__popcll(at_rec)) < SA.leaf_k || trav_at_record(T));
       if (STATS) {  // SIMD efficiency of the walk (RTX_DEBUG report)
         wsteps++;
-        lsteps += __popcll(__ballot(active));
+        lsteps += __popcll(__ballot(go));
       }
-      if (active) {
+      if (go) {
         if (STATS) qsteps++;
         if (trav_step<STATS, MODE>(T, S, stk, lane, blk, C)) {
           if (FUSED) pend = true;
@@ -2931,9 +2938,29 @@ rtx_status rtx_render(void* scene, const RtxRenderParams* params, uint8_t* rgb8,
       if (e && atoi(e) > 1) tgrid = std::max<int64_t>(1, tgrid / atoi(e));
     }
     if (tgrid > per) tgrid = per;
+    // the fused kernels' own residency (their launch bounds differ:
+    // RTX_SHADE_WAVES / RTX_WALK_WAVES)
+    int64_t tgrid_c = tgrid, tgrid_n = tgrid;
+    if (fuse) {
+      int pc = 0, pn = 0;
+      HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(
+          &pc, reinterpret_cast<const void*>(trace_kernel<false, Q_CLOSEST, true, true>), WG, lds));
+      HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(
+          &pn, reinterpret_cast<const void*>(trace_kernel<false, Q_NEXT, true>), WG, lds));
+      tgrid_c = std::min<int64_t>(per, std::max<int64_t>(1, tgrid * std::max(1, pc) / per_cu));
+      tgrid_n = std::min<int64_t>(per, std::max<int64_t>(1, tgrid * std::max(1, pn) / per_cu));
+    }
     const char* dbg_env = getenv("RTX_DEBUG");
     const bool dbg = dbg_env && atoi(dbg_env) != 0;
+    const int dbg_level = dbg_env ? atoi(dbg_env) : 0;
     const int check_every = 4;
+    // costly traversal units wait while this many lanes of a wave are at a
+    // 4-wide record (trace_kernel; RTX_LEAF_K, 1..65, 65: never wait)
+    int leaf_k = 16;
+    {
+      const char* e = getenv("RTX_LEAF_K");
+      if (e && atoi(e) > 0) leaf_k = std::min(65, atoi(e));
+    }
     hipEvent_t e0, e1;
     if ((rc = get_event(&e0)) != RTX_OK || (rc = get_event(&e1)) != RTX_OK) return rc;
     HIP_TRY(hipEventRecord(e0, stream));
@@ -2995,7 +3022,7 @@ rtx_status rtx_render(void* scene, const RtxRenderParams* params, uint8_t* rgb8,
         const int first = it == 0 ? 1 : (cam_first && it == 1 ? 2 : 0);
         const int64_t lb = grid_bound[size_t(g)];
         const int64_t agrid = first ? per : std::max<int64_t>(1, std::min<int64_t>(per, (lb + WG - 1) / WG));
-        const int64_t tg = std::max<int64_t>(1, std::min<int64_t>(tgrid, (lb + WG - 1) / WG));
+        const int64_t tg = std::max<int64_t>(1, std::min<int64_t>(fuse ? tgrid_c : tgrid, (lb + WG - 1) / WG));
         const bool cam_it = cam_first && it == 0;
         if (cam_it) {
           // the slots the first launch does not claim start idle
@@ -3019,10 +3046,11 @@ rtx_status rtx_render(void* scene, const RtxRenderParams* params, uint8_t* rgb8,
           });
         }
         // the next-hit grid: fused walks can outnumber the live slots
-        const int64_t tgn = fuse ? std::max<int64_t>(1, std::min<int64_t>(tgrid, (lb * int64_t(nrec_n) + WG - 1) / WG))
+        const int64_t tgn = fuse ? std::max<int64_t>(1, std::min<int64_t>(tgrid_n, (lb * int64_t(nrec_n) + WG - 1) / WG))
                                  : tg;
         ShadeArgs sa;
         std::memset(&sa, 0, sizeof(sa));
+        sa.leaf_k = leaf_k;
         if (fuse) {
           sa.Fp = st->d_frame;
           sa.hits = d_hits;
@@ -3037,10 +3065,50 @@ rtx_status rtx_render(void* scene, const RtxRenderParams* params, uint8_t* rgb8,
         dispatch2(stats, fork, [&](auto st_, auto fk_) {
           constexpr bool ST_ = decltype(st_)::value, FK_ = decltype(fk_)::value;
           if (fuse) {
+            // (inside the dispatch lambda: no HIP_TRY returns here; debug only)
+            hipEvent_t d0 = nullptr, d1 = nullptr;
+            if (dbg_level >= 2) {  // RTX_DEBUG=2: every iteration's queries and closest-hit time (synchronous)
+              (void)(hipStreamSynchronize(sg));
+              if (stats) (void)(hipMemset(st->d_stats + 12, 0, 4 * sizeof(unsigned long long)));
+              (void)(hipEventCreate(&d0));
+              (void)(hipEventCreate(&d1));
+              (void)(hipEventRecord(d0, sg));
+            }
             hipLaunchKernelGGL((trace_kernel<ST_, Q_CLOSEST, true, FK_>), dim3(tg), dim3(WG), lds, sg, S, st->d_scene,
                                q0, cnt, A, st->stack_cap, st->d_stats, st->d_wterm, sa, -1);
+            if (dbg_level >= 2) {
+              unsigned int hc[CNT_PER_GROUP];
+              unsigned long long hs[4] = {0, 0, 0, 0};
+              float ms = 0.f;
+              (void)(hipEventRecord(d1, sg));
+              (void)(hipStreamSynchronize(sg));
+              (void)(hipEventElapsedTime(&ms, d0, d1));
+              (void)(hipMemcpy(hc, cnt, sizeof(hc), hipMemcpyDeviceToHost));
+              if (stats) (void)(hipMemcpy(hs, st->d_stats + 12, sizeof(hs), hipMemcpyDeviceToHost));
+              fprintf(stderr,
+                      "rtx group %d iter %d: closest %u walks %u forks %u | closest-hit launch %.3f ms, max steps "
+                      "%llu, queries over 100 steps %llu\n",
+                      g, it, cam_it ? static_cast<unsigned>(cam_n[size_t(g)]) : hc[CNT_Q], hc[CNT_Q + CNT_LINE],
+                      hc[CNT_FORK], ms, hs[0], hs[2]);
+              (void)(hipEventDestroy(d0));
+              (void)(hipEventDestroy(d1));
+            }
+            if (dbg_level >= 2) {
+              (void)(hipEventCreate(&d0));
+              (void)(hipEventCreate(&d1));
+              (void)(hipEventRecord(d0, sg));
+            }
             hipLaunchKernelGGL((trace_kernel<ST_, Q_NEXT, true>), dim3(tgn), dim3(WG), lds, sg, S, st->d_scene, q1,
                                cnt, A, st->stack_cap, st->d_stats, st->d_wterm, sa, clr_next);
+            if (dbg_level >= 2) {
+              float ms = 0.f;
+              (void)(hipEventRecord(d1, sg));
+              (void)(hipStreamSynchronize(sg));
+              (void)(hipEventElapsedTime(&ms, d0, d1));
+              fprintf(stderr, "rtx group %d iter %d: walk launch %.3f ms\n", g, it, ms);
+              (void)(hipEventDestroy(d0));
+              (void)(hipEventDestroy(d1));
+            }
           } else if (!FK_) {
             hipLaunchKernelGGL((trace_kernel<ST_, Q_CLOSEST>), dim3(tg), dim3(WG), lds, sg, S, st->d_scene, q0, cnt, A,
                                st->stack_cap, st->d_stats, nullptr, sa, -1);

@@ -195,6 +195,11 @@ RT_HD void trav_reset(Trav& T) {
   T.have = T.blocked = T.mhave = T.closest = false;
 }
 
+// The lane's next unit is a 4-wide record (scene or mesh): the cheap step.
+// Objects (mode 1: world-box test, transform to the mesh frame) and mesh
+// leaves (exact face tests) are the costly ones.
+RT_HD bool trav_at_record(const Trav& T) { return T.mode != 1 && T.ref >= 0; }
+
 // One unit of the walk; true when the query is complete.
 template <bool STATS, int QMODE, class Blocker>
 RT_HD bool trav_step(Trav& T, const DevScene& S, int* __restrict__ stk, const int lane, const Blocker& blocker,
@@ -208,14 +213,28 @@ RT_HD bool trav_step(Trav& T, const DevScene& S, int* __restrict__ stk, const in
   bool& have = T.have;
   int& sp = T.sp;
   int& ref = T.ref;
-  if (T.mode == 0) {
-    if (ref >= 0) {
-      if (visit4<STATS>(S.snode4[ref], T.rf, bt + S.margin, tlo, stk, lane, sp, ref, C)) return false;
+  // a 4-wide record, scene (mode 0) or mesh (mode 2, local frame): one call
+  // site for both, so a wave with lanes at both levels runs it once (and the
+  // kernel carries one inlined copy)
+  const bool mesh = T.mode == 2;
+  if (T.mode != 1 && ref >= 0) {
+    double hi = bt + S.margin, lo = tlo;
+    if (mesh) {
+      const double len = T.len;
+      hi = (bt + S.margin) * len * (1.0 + 1e-12);
+      if (closest && T.mhave) hi = rtm::gmin(hi, T.mbest + S.lmargin);
+      lo = closest ? -RTX_INF : tlo * len * (1.0 - 1e-12) - S.lmargin;
+    }
+    const DevNode4* recs = !mesh ? S.snode4 : (ref < S.n_mhot ? S.mhot : S.mnode4);
+    if (visit4<STATS>(recs[ref], T.rf, hi, lo, stk, lane, sp, ref, C)) return false;
+    if (!mesh) {
       if (sp == 0) return true;
       --sp;
       ref = stk[sp * 64 + lane];
       return false;
     }
+  }
+  if (T.mode == 0) {
     const int code = ~ref;
     T.oc = code >> 2;
     T.oe = T.oc + (code & 3);
@@ -426,16 +445,11 @@ RT_HD bool trav_step(Trav& T, const DevScene& S, int* __restrict__ stk, const in
     }
     return false;
   }
-  // mode == 2: mesh BVH of object moi, local frame
+  // mode == 2: mesh BVH of object moi, local frame (a record missed above,
+  // or a leaf)
   const double len = T.len;
   const double whi = (bt + S.margin) * len * (1.0 + 1e-12);
-  double hi = whi;
-  if (closest && T.mhave) hi = rtm::gmin(hi, T.mbest + S.lmargin);
-  const double lo = closest ? -RTX_INF : tlo * len * (1.0 - 1e-12) - S.lmargin;
-  if (ref >= 0) {
-    if (visit4<STATS>((ref < S.n_mhot ? S.mhot : S.mnode4)[ref], T.rf, hi, lo, stk, lane, sp, ref, C))
-      return false;
-  } else {
+  if (ref < 0) {
     const int code = ~ref;
     const int f0 = code >> 2, f1 = f0 + (code & 3);
     // a face whose plane hit lies beyond this bound cannot win (closest:

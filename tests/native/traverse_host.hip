@@ -118,4 +118,29 @@ int trav_host_run(const RtxSceneDesc* d, int32_t qmode, int32_t n, const double*
   return 0;
 }
 
+// Per-ray traversal cost of closest queries (record entries, object tests,
+// face tests): which rays make the long queries (tools/ray_cost_probe.py).
+int trav_host_cost(const RtxSceneDesc* d, int32_t n, const double* P, const double* D, int64_t* nodes,
+                   int64_t* objs, int64_t* tris, int32_t* object) {
+  HostScene H;
+  if (!make_scene(d, H)) {
+    g_err = "malformed BVH";
+    return -1;
+  }
+  std::vector<int> stk(size_t(H.stack_cap + 4) * 64, 0);
+  for (int32_t k = 0; k < n; ++k) {
+    Counters C = {0, 0, 0, 0, 0, 0, 0};
+    double bt;
+    int bobj, bsub;
+    const bool have = traverse<true>(H.S, Q_CLOSEST, mk3(P[3 * k], P[3 * k + 1], P[3 * k + 2]),
+                                     mk3(D[3 * k], D[3 * k + 1], D[3 * k + 2]), -RTX_INF, -1, -1, RTX_INF, bt, bobj,
+                                     bsub, stk.data(), 0, C);
+    nodes[k] = C.nodes;
+    objs[k] = C.objects;
+    tris[k] = C.tris;
+    object[k] = have ? d->objects[bobj].orig_id : -1;
+  }
+  return 0;
+}
+
 }  // extern "C"

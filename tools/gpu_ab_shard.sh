@@ -1,0 +1,18 @@
+#!/bin/bash
+# A/B of configurations on the full headline frame and its 8-way shards
+# (tools/shard_probe.py, same box).  Each argument is one configuration:
+# env assignments separated by ','; "lib=NAME" selects
+# lib/variants/librtx_hip_NAME.so (tools/build_variants.sh); "" = default.
+set -o pipefail
+cd "$GRAFT_REPO_ROOT"
+mkdir -p gpurun_out
+for cfg in "$@"; do
+  envs=""
+  for a in $(echo "$cfg" | tr ',' ' '); do
+    case $a in
+      lib=*) envs="$envs RTX_HIP_LIB=$GRAFT_REPO_ROOT/cs378hgraphics-raytracer_amd/lib/variants/librtx_hip_${a#lib=}.so" ;;
+      *) envs="$envs $a" ;;
+    esac
+  done
+  env $envs timeout -k 10 200 python tools/shard_probe.py 1 8 | sed "s|^|[$cfg] |" || exit 1
+done
