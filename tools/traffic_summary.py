@@ -83,8 +83,10 @@ def main():
         out["sq_fractions"] = {k: tot.get(k, 0.0) / sq for k in ("SQ_WAIT_ANY", "SQ_WAIT_INST_ANY",
                                                                   "SQ_ACTIVE_INST_ANY", "SQ_ACTIVE_INST_VALU")}
     os.makedirs(os.path.join(ROOT, "profiles"), exist_ok=True)
-    for name in (f"traffic_{tag}.json", "traffic_latest.json"):
-        with open(os.path.join(ROOT, "profiles", name), "w") as f:
+    os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
+    for path in (os.path.join("profiles", f"traffic_{tag}.json"), os.path.join("profiles", "traffic_latest.json"),
+                 os.path.join("gpurun_out", f"traffic_{tag}.json")):  # (gpurun_out/ comes back from the box)
+        with open(os.path.join(ROOT, path), "w") as f:
             json.dump(out, f, indent=1)
     print(json.dumps({k: out[k] for k in ("hbm_read_bytes_per_launch", "hbm_write_bytes_per_launch",
                                           "l2_hit_rate")}), out.get("sq_fractions"))
