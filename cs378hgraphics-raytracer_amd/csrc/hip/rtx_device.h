@@ -298,6 +298,33 @@ RT_HD bool box_cons32(const DevNode4& nd, int k, const RayF& r, float& a, float&
   return !(a > b) && !(b < 0.0f);
 }
 
+// box_cons32 for entries 2p and 2p + 1 at once: the slab arithmetic on
+// float pairs (packed v_pk_add_f32 / v_pk_mul_f32 on gfx950), the same
+// operations element by element.  Returns the pair's (a, b); the caller
+// applies the hit rule !(a > b) && !(b < 0).
+typedef float rtx_f2 __attribute__((ext_vector_type(2)));
+RT_HD void box_cons32x2(const DevNode4& nd, int p, const RayF& r, rtx_f2& a, rtx_f2& b) {
+  rtx_f2 tmin, tmax;
+#pragma unroll
+  for (int q = 0; q < 3; ++q) {
+    const rtx_f2 lo = {nd.lo[q][2 * p], nd.lo[q][2 * p + 1]};
+    const rtx_f2 hi = {nd.hi[q][2 * p], nd.hi[q][2 * p + 1]};
+    const rtx_f2 t1 = (lo - r.olo[q]) * r.inv[q];
+    const rtx_f2 t2 = (hi - r.ohi[q]) * r.inv[q];
+    const rtx_f2 n = __builtin_elementwise_min(t1, t2), f = __builtin_elementwise_max(t1, t2);
+    tmin = q == 0 ? n : __builtin_elementwise_max(tmin, n);
+    tmax = q == 0 ? f : __builtin_elementwise_min(tmax, f);
+  }
+  const rtx_f2 err = {r.err, r.err};
+  a = tmin - (err + __builtin_elementwise_abs(tmin) * 0x1p-21f);
+  b = tmax + (err + __builtin_elementwise_abs(tmax) * 0x1p-21f);
+#pragma unroll
+  for (int e = 0; e < 2; ++e) {  // inf - inf: the infinite bound itself (see box_cons32)
+    if (!(a[e] == a[e])) a[e] = tmin[e];
+    if (!(b[e] == b[e])) b[e] = tmax[e];
+  }
+}
+
 // ------------------------------------------------------------------ textures
 // TextureMap::getMappedValue / getPixelAt (material.cpp:84-138)
 __device__ __forceinline__ dvec3 tex_pixel(const DevScene& S, const RtxTexture& t, int x, int y) {

@@ -102,6 +102,27 @@ RT_HD bool visit4(const DevNode4& nd, const RayF& rf, const double hi, const dou
   float a0 = NOHIT, a1 = NOHIT, a2 = NOHIT, a3 = NOHIT;
   int r0 = 0, r1 = 0, r2 = 0, r3 = 0;
   const int cnt = nd.count;
+#ifdef RTX_PACKED_RECORDS
+  // Opt-in: two entries per packed float pair (box_cons32x2; entries past
+  // `count` are empty boxes, which the slab rule does not reject: masked
+  // here).  Measured 47.7 / 48.9 ms against 46.4 / 47.1 for the scalar
+  // tests on the headline frame: fewer instructions, more spills (192 B).
+  auto pair = [&](int p, float& ax, int& rx, float& ay, int& ry) {
+    rtx_f2 ta, tb;
+    box_cons32x2(nd, p, rf, ta, tb);
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      const int k = 2 * p + e;
+      if (STATS && k < cnt) C.nodes++;
+      if (k < cnt && !(ta[e] > tb[e]) && !(tb[e] < 0.0f) && !(ta[e] > hf) && !(tb[e] < lf)) {
+        (e ? ay : ax) = ta[e];
+        (e ? ry : rx) = nd.child[k];
+      }
+    }
+  };
+  pair(0, a0, r0, a1, r1);
+  pair(1, a2, r2, a3, r3);
+#else
   auto test = [&](int k, float& ak, int& rk) {
     if (k < cnt) {
       if (STATS) C.nodes++;
@@ -116,6 +137,7 @@ RT_HD bool visit4(const DevNode4& nd, const RayF& rf, const double hi, const dou
   test(1, a1, r1);
   test(2, a2, r2);
   test(3, a3, r3);
+#endif
   // sorting network on (entry distance, ref)
   auto cs = [](float& x, int& rx, float& y, int& ry) {
     const bool s = y < x;
