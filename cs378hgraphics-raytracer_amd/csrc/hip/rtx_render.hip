@@ -2883,11 +2883,15 @@ rtx_status rtx_render(void* scene, const RtxRenderParams* params, uint8_t* rgb8,
     int64_t tail_slots = 1000000;
     const char* tail_env = getenv("RTX_TAIL");
     if (tail_env) tail_slots = atoll(tail_env);
-    // RTX_TAIL_ITER=k (A/B): the tail kernel takes over at batched iteration
-    // k whatever the live count
-    int tail_iter = 0;
+    // RTX_TAIL_ITER=k: the tail kernel takes over at batched iteration k
+    // whatever the live count (0: by the live count only).  Default 5: the
+    // full frames have nothing left by then (46.4 vs 46.4 ms headline, 62.7
+    // vs 63.4 C4) while a shard's stragglers finish without 1-2 more
+    // launch pairs bounded by their slowest query (8-way shard 9.7 vs 10.4
+    // ms, C4's 12.1 vs 12.4; iteration 4: full frames 0.5-1.5 ms slower)
+    int tail_iter = 5;
     const char* ti_env = getenv("RTX_TAIL_ITER");
-    if (ti_env) tail_iter = atoi(ti_env);
+    if (ti_env) tail_iter = std::max(0, atoi(ti_env));
     F.qchunk = 64;
     // First iteration without an advance launch (fused frames): the closest-
     // hit launch claims each sample slot's first sample and queries its first

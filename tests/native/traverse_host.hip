@@ -118,6 +118,29 @@ int trav_host_run(const RtxSceneDesc* d, int32_t qmode, int32_t n, const double*
   return 0;
 }
 
+// The float record test (box_cons32, as visit4 runs it) on n (ray, box)
+// pairs: box k = (lo[6k..6k+3), hi[6k+3..6k+6)) in double, stored the way the
+// records store it (rounded outward to float); ok[k] = 1 when the entry
+// passes.  The test harness compares with an exact geometric slab.
+int rec_test_host(int32_t n, const double* P, const double* D, const double* box, int32_t* ok, float* a_out) {
+  for (int32_t k = 0; k < n; ++k) {
+    const dvec3 p = mk3(P[3 * k], P[3 * k + 1], P[3 * k + 2]);
+    const dvec3 d = mk3(D[3 * k], D[3 * k + 1], D[3 * k + 2]);
+    const RayF rf = ray_f(p, d, ray_inv(d));
+    DevNode4 nd;
+    std::memset(&nd, 0, sizeof(nd));
+    for (int q = 0; q < 3; ++q) {
+      nd.lo[q][0] = round_down_f(box[6 * k + q]);
+      nd.hi[q][0] = round_up_f(box[6 * k + 3 + q]);
+    }
+    nd.count = 1;
+    float a, b;
+    ok[k] = box_cons32(nd, 0, rf, a, b) ? 1 : 0;
+    a_out[k] = a;
+  }
+  return 0;
+}
+
 // Per-ray traversal cost of closest queries (record entries, object tests,
 // face tests): which rays make the long queries (tools/ray_cost_probe.py).
 int trav_host_cost(const RtxSceneDesc* d, int32_t n, const double* P, const double* D, int64_t* nodes,

@@ -1,0 +1,101 @@
+"""The float record test (box_cons32, rtx_device.h; DESIGN.md "Float record
+tests") never rejects a box that contains a point of the ray at t >= 0: the
+requirement for the device's own BVH records, whose boxes only steer the walk
+(the exact tests decide candidacy: objects' world boxes and leaf_ok).
+
+Checked against an exact rational slab (fractions.Fraction) on adversarial
+(ray, box) pairs: boxes that just touch the ray (the ray passes through a
+face or an edge of the box, within a few ulps), rays with zero direction
+components (the inside test: the box must be hit iff o lies in the slab),
+large origins (the float rounding of o dominates), and near-parallel rays.
+Runs the device code compiled for the host (tests/native/traverse_host.hip)."""
+import ctypes as C
+from fractions import Fraction as Fr
+
+import numpy as np
+
+from test_traverse_host import _harness
+
+
+def exact_hit(o, d, lo, hi):
+    """Does the ray o + t d, t >= 0, meet the closed box [lo, hi]?  Exact."""
+    tmin, tmax = Fr(0), None
+    for a in range(3):
+        oa, da, la, ha = Fr(o[a]), Fr(d[a]), Fr(lo[a]), Fr(hi[a])
+        if da == 0:
+            if oa < la or oa > ha:
+                return False
+            continue
+        t1, t2 = (la - oa) / da, (ha - oa) / da
+        if t1 > t2:
+            t1, t2 = t2, t1
+        tmin = max(tmin, t1)
+        tmax = t2 if tmax is None else min(tmax, t2)
+        if tmin > tmax:
+            return False
+    return True
+
+
+def _cases(rng, n):
+    P, D, B = [], [], []
+    for k in range(n):
+        kind = k % 5
+        scale = [1.0, 1e3, 1e6, 0.01, 50.0][k % 5]
+        o = rng.normal(size=3) * scale
+        d = rng.normal(size=3)
+        if kind == 1:  # zero components
+            d[rng.integers(0, 3)] = 0.0
+            if k % 2:
+                d[rng.integers(0, 3)] = 0.0
+        if kind == 2:  # near-parallel to an axis plane
+            d[rng.integers(0, 3)] *= 1e-9
+        if abs(d).max() == 0.0:
+            d[0] = 1.0
+        d /= np.linalg.norm(d)
+        # a point on the ray (or just off it), a box with a face through it
+        t = abs(rng.normal()) * scale + 1e-3
+        x = o + t * d
+        ext = abs(rng.normal(size=3)) * scale * 0.1 + 1e-9
+        lo, hi = x - ext * rng.random(3), x + ext * rng.random(3)
+        ax = rng.integers(0, 3)
+        eps = rng.choice([0.0, 1e-16, -1e-16, 1e-13, -1e-13, 1e-9, -1e-9]) * max(abs(x[ax]), 1.0)
+        if rng.random() < 0.5:
+            lo[ax] = x[ax] + eps  # the ray grazes the box's lower face
+        else:
+            hi[ax] = x[ax] + eps
+        if kind == 1:  # zero axes: origin exactly on / just off the slab boundary
+            za = np.nonzero(d == 0.0)[0]
+            for a in za:
+                lo[a] = o[a] + rng.choice([0.0, 1e-15, -1e-15]) * max(abs(o[a]), 1.0)
+                hi[a] = max(hi[a], lo[a])
+        lo, hi = np.minimum(lo, hi), np.maximum(lo, hi)
+        P.append(o)
+        D.append(d)
+        B.append(np.concatenate([lo, hi]))
+    return np.array(P), np.array(D), np.array(B)
+
+
+def test_float_record_test_is_conservative(pkg):
+    L = _harness(pkg)
+    L.rec_test_host.argtypes = [C.c_int32] + [C.c_void_p] * 5
+    rng = np.random.default_rng(2024)
+    n = 6000
+    P, D, B = _cases(rng, n)
+    ok = np.zeros(n, np.int32)
+    a = np.zeros(n, np.float32)
+    assert L.rec_test_host(n, P.ctypes.data, D.ctypes.data, B.ctypes.data, ok.ctypes.data, a.ctypes.data) == 0
+    hits = 0
+    for k in range(n):
+        if exact_hit(P[k], D[k], B[k, :3], B[k, 3:]):
+            hits += 1
+            assert ok[k] == 1, f"case {k}: exact hit rejected (o={P[k]!r}, d={D[k]!r}, box={B[k]!r})"
+    assert hits > n // 3  # the cases really sit on the boundary of hitting
+    # and the float test still culls: boxes clearly off the ray are rejected
+    far = B.copy()
+    far[:, :3] += 10.0 * (abs(B[:, 3:] - B[:, :3]).max(axis=1, keepdims=True) + 1.0) * np.sign(D + 1e-300) * -1
+    far[:, 3:] = far[:, :3] + (B[:, 3:] - B[:, :3])
+    ok2 = np.zeros(n, np.int32)
+    assert L.rec_test_host(n, P.ctypes.data, D.ctypes.data, far.ctypes.data, ok2.ctypes.data, a.ctypes.data) == 0
+    culled = sum(1 for k in range(n) if not exact_hit(P[k], D[k], far[k, :3], far[k, 3:]) and ok2[k] == 0)
+    missed = sum(1 for k in range(n) if not exact_hit(P[k], D[k], far[k, :3], far[k, 3:]))
+    assert missed > 0 and culled >= 0.9 * missed

@@ -15,4 +15,7 @@ for cfg in "$@"; do
     esac
   done
   env $envs timeout -k 10 200 python tools/shard_probe.py 1 8 | sed "s|^|[$cfg] |" || exit 1
+  if [ -n "$AB_C4" ]; then
+    env $envs timeout -k 10 200 python tools/shard_probe.py --flags "-w 1920 -r 5 -O d -A 2.5 -B 16 -C 0.05" 1 8 | sed "s|^|[$cfg] |" || exit 1
+  fi
 done
