@@ -37,7 +37,10 @@ using rtm::dvec2;
 using rtm::dvec3;
 using rtm::mk3;
 
-#define WG 256
+#ifndef RTX_WG
+#define RTX_WG 256  // threads per workgroup (A/B: -DRTX_WG=64 / 128)
+#endif
+#define WG RTX_WG
 #define WAVES_PER_WG (WG / 64)
 // -r limit: the pending-ray stack holds depth + 2 entries per slot in HBM
 // and the slot pool shrinks to fit device memory, so this only bounds the
