@@ -387,8 +387,11 @@ __device__ __forceinline__ void cam_start(LaneRef& LR, const FrameParams& F, Rtx
 // its first camera ray straight away — what advance_fused (claim, ST_CAM,
 // ST_POP) would have done, without the pending-stack entry and the query
 // record round trip.  False: the slot has no sample (left idle).
-// (out of line: inlined into the persistent closest-hit kernel its registers
-// add to the traversal's peak)
+// (out of line, and only in the first iteration's instantiation of the
+// closest-hit kernel, trace_kernel<..., CAM = true>: inlined there its
+// registers add to the traversal's peak, and the backend fails on the
+// inlined STATS instantiation, "Subtarget requires even aligned vector
+// registers")
 template <bool STATS>
 __device__ __noinline__ bool cam_first_claim(LaneRef& LR, const FrameParams& F, Counters& C,
                                              RtxHitRecord* __restrict__ hits, int slot, QRay& qr) {

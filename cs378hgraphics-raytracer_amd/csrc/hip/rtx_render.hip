@@ -1806,7 +1806,10 @@ struct ShadowBlocker {
 #ifndef RTX_WALK_WAVES
 #define RTX_WALK_WAVES RTX_TRACE_WAVES
 #endif
-template <bool STATS, int MODE, bool FUSED = false, bool FORK = false>
+// CAM: the first iteration's instantiation (claims + first camera rays,
+// SA.cam_n > 0); the others carry none of that code, so the later
+// iterations' closest-hit launches keep their own register budget.
+template <bool STATS, int MODE, bool FUSED = false, bool FORK = false, bool CAM = false>
 __global__ void __launch_bounds__(WG, !FUSED ? RTX_TRACE_WAVES : (MODE == Q_CLOSEST ? RTX_SHADE_WAVES : RTX_WALK_WAVES))
     trace_kernel(DevScene S, const DevScene* __restrict__ Sg, QList Q, unsigned int* __restrict__ counters,
                  LaneMem lm, int stack_cap, unsigned long long* __restrict__ stats, double* __restrict__ wterm,
@@ -1839,7 +1842,7 @@ __global__ void __launch_bounds__(WG, !FUSED ? RTX_TRACE_WAVES : (MODE == Q_CLOS
     S.mhot = lds_nodes + ns;
   }
 #endif
-  const bool cam = FUSED && MODE == Q_CLOSEST && SA.cam_n > 0;  // first iteration: claims + camera rays here
+  const bool cam = CAM && FUSED && MODE == Q_CLOSEST && SA.cam_n > 0;  // first iteration: claims + camera rays here
   const unsigned int nq = cam ? static_cast<unsigned int>(SA.cam_n) : counters[CNT_Q + (MODE - 1) * CNT_LINE];
   unsigned int* claim = counters + CNT_CLAIM + (MODE - 1) * CNT_LINE;
 #ifdef RTX_EARLYOUT
@@ -3081,8 +3084,12 @@ rtx_status rtx_render(void* scene, const RtxRenderParams* params, uint8_t* rgb8,
               (void)(hipEventCreate(&d1));
               (void)(hipEventRecord(d0, sg));
             }
-            hipLaunchKernelGGL((trace_kernel<ST_, Q_CLOSEST, true, FK_>), dim3(tg), dim3(WG), lds, sg, S, st->d_scene,
-                               q0, cnt, A, st->stack_cap, st->d_stats, st->d_wterm, sa, -1);
+            if (cam_it)
+              hipLaunchKernelGGL((trace_kernel<ST_, Q_CLOSEST, true, FK_, true>), dim3(tg), dim3(WG), lds, sg, S,
+                                 st->d_scene, q0, cnt, A, st->stack_cap, st->d_stats, st->d_wterm, sa, -1);
+            else
+              hipLaunchKernelGGL((trace_kernel<ST_, Q_CLOSEST, true, FK_>), dim3(tg), dim3(WG), lds, sg, S,
+                                 st->d_scene, q0, cnt, A, st->stack_cap, st->d_stats, st->d_wterm, sa, -1);
             if (dbg_level >= 2) {
               unsigned int hc[CNT_PER_GROUP];
               unsigned long long hs[4] = {0, 0, 0, 0};
