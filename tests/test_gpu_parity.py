@@ -163,6 +163,38 @@ def test_buckets_independent_of_fork_slots(pkg, slots):
             os.environ["RTX_SLOTS"] = saved
 
 
+SCHED_SWITCHES = [{"RTX_CAM_FIRST": "0"}, {"RTX_TAIL_ITER": "2"}, {"RTX_TAIL_ITER": "0"}, {"RTX_LEAF_K": "65"},
+                  {"RTX_LEAF_K": "1"}, {"RTX_GROUPS": "1"}, {"RTX_GROUPS": "2"}]
+
+
+@pytest.mark.parametrize("flags", ["-w 48 -r 5 -O r -A 4", "-w 40 -r 5 -O d -A 2.5 -B 4 -C 0.05"],
+                         ids=["aa4", "dof"])
+def test_scheduling_switches_bit_identical(pkg, flags):
+    """The scheduling switches of the wavefront path — first iteration with or
+    without the advance launch, the tail switch, postponed traversal units,
+    the number of slot groups — change which kernel runs what, never the
+    arithmetic: the f64 images and the per-sample hit records are
+    bit-identical to the default's."""
+    path = scene_path("trimesh2_square.ray")
+    opts = pkg.RenderOptions.from_cli(flags.split())
+    dev = pkg.DeviceScene(pkg.HostScene(path), 0)
+    base = dev.render(opts, want_f64=True, want_hits=True)
+    for sw in SCHED_SWITCHES:
+        saved = {k: os.environ.get(k) for k in sw}
+        os.environ.update(sw)
+        try:
+            r = dev.render(opts, want_f64=True, want_hits=True)
+        finally:
+            for k, v in saved.items():
+                if v is None:
+                    os.environ.pop(k, None)
+                else:
+                    os.environ[k] = v
+        assert np.array_equal(r["rgb"], base["rgb"]), f"{sw}: image differs"
+        for f in ("object", "face", "scene_leaf", "mesh_leaf", "nrays"):
+            assert np.array_equal(r["hits"][f], base["hits"][f]), f"{sw}: hit field {f} differs"
+
+
 @pytest.fixture(scope="session")
 def dragon_path(tmp_path_factory):
     """The generated 1M-triangle dragon stand-in (tools/gen_scenes.py, seed
