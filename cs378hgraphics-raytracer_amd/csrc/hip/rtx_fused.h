@@ -73,6 +73,16 @@ __device__ __forceinline__ bool walk_hit(const DevScene& S, const RtxLight& L, c
   return false;
 }
 
+#ifdef RTX_WALK_OOL
+// Opt-in: walk_hit out of line in the walk kernel (its resolve_hit and
+// material lookups off the kernel's register peak).  Measured 47.1-47.3 vs
+// 45.7 ms on the headline frame (the call's frame and saves cost more).
+__device__ __noinline__ bool walk_hit_ool(const DevScene* Sg, int li, const dvec3 pb, const dvec3 sdir, bool have,
+                                          double bt, int bobj, int bsub, WalkState* w, dvec3* res) {
+  return walk_hit(*Sg, Sg->lights[li], pb, sdir, have, bt, bobj, bsub, *w, *res);
+}
+#endif
+
 // the group's next-hit list and its append counter
 struct WalkEmit {
   QList q;

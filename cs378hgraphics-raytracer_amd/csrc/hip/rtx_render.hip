@@ -1893,7 +1893,11 @@ __global__ void __launch_bounds__(WG, !FUSED ? RTX_TRACE_WAVES : (MODE == Q_CLOS
       const double bt = w_bt;
       const int bo = w_bo, bs = w_bs;
       dvec3 res;
+#ifdef RTX_WALK_OOL
+      if (walk_hit_ool(Sg, li, pb, sdir, w_have, bt, bo, bs, &w, &res)) {
+#else
       if (walk_hit(*Sg, L, pb, sdir, w_have, bt, bo, bs, w, res)) {
+#endif
         const size_t slot = static_cast<size_t>(Q.slot[k]);
         const dvec3 dsc = mk3(Q.d[QF_SCX * cap + k], Q.d[QF_SCY * cap + k], Q.d[QF_SCZ * cap + k]);
         const dvec3 term = Q.d[QF_DATTN * cap + k] * res * ld3(L.color) * dsc;
