@@ -137,7 +137,49 @@ def cpu_baseline(pkg, path, opts, height, budget_s=10.0, repeats=3):
     return {"value": med, "unit": "Mrays/s", "cores": threads, "kind": "port",
             "cpu_model": model, "host_cpus": ncpu, "affinity_cpus": aff, "cgroup_cpu_quota": quota,
             "runs_mrays_s": [round(x, 3) for x in rates], "full_frame": band >= height,
-            "sample": f"CPU restatement (oracle/, g++ -O2, OpenMP {threads} threads) on {what}, median of {repeats} runs"}
+            "sample": f"CPU restatement (oracle/, g++ -O2, OpenMP {threads} threads) on {what}, median of {repeats} runs",
+            "_band": band, "_threads": threads}
+
+
+def parity_block(pkg, dev, path, opts, height, band, threads):
+    """Parity of the timed frame (untimed, after the CPU leg): the GPU frame
+    with its per-sample hit records against the CPU restatement's, under the
+    north-star bar of tests/parity.py — over the whole frame when the CPU leg
+    rendered it whole, else over the CPU leg's row bands."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import numpy as np
+    import oracle  # test infrastructure: the checker
+    from parity import RGB_TOL, measure
+
+    gpu = dev.render(opts, want_f64=True, want_hits=True)
+    if band >= height:
+        rows = [(0, height)]
+    else:
+        nb = 4
+        rows = []
+        for k in range(nb):
+            yc = int(height * (k + 0.5) / nb)
+            y0 = max(0, min(height - band, yc - band // 2))
+            rows.append((y0, y0 + band))
+    sel = np.concatenate([np.arange(a, b) for a, b in rows])
+    ref_rgb = np.zeros_like(gpu["rgb"])
+    ref_rgb8 = np.zeros_like(gpu["rgb8"])
+    ref_hits = None
+    for a, b in rows:
+        r = oracle.render(pkg, path, opts, rect=(0, a, opts.width, b) if (a, b) != (0, height) else None,
+                          threads=threads, want_hits=True)
+        ref_rgb[a:b], ref_rgb8[a:b] = r["rgb"][a:b], r["rgb8"][a:b]
+        if ref_hits is None:
+            ref_hits = np.zeros_like(gpu["hits"])
+        ref_hits[a:b] = r["hits"][a:b]
+        del r
+    m = measure(gpu["rgb"][sel], gpu["rgb8"][sel], ref_rgb[sel], ref_rgb8[sel], gpu["hits"][sel], ref_hits[sel])
+    m["rows"] = "whole frame" if band >= height else [list(x) for x in rows]
+    m["tolerance_rgb"] = RGB_TOL
+    m["pass"] = bool(m["max_abs_rgb"] <= RGB_TOL and m["rgb8_mismatch"] == 0 and m["hit_mismatch"] == 0 and
+                     m["t_mismatch"] == 0 and m["nan_mismatch"] == 0)
+    return m
 
 
 def main():
@@ -150,6 +192,7 @@ def main():
     ap.add_argument("--tile", type=int, default=32)
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     ap.add_argument("--cpu-budget", type=float, default=10.0, help="seconds of CPU work per baseline run")
+    ap.add_argument("--no-parity", action="store_true", help="skip the parity block of the timed frame")
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic_latest.json"),
                     help="PMC-measured HBM bytes per launch (tools/profile_traffic.sh output)")
     args = ap.parse_args()
@@ -266,9 +309,12 @@ def main():
                                    "build_id": tr.get("build_id")}
             except (OSError, ValueError):
                 traffic = None
-        cpu = None
+        cpu, parity = None, None
         if not args.no_cpu and world == 1:
             cpu = cpu_baseline(pkg, args.scene, opts, height, args.cpu_budget)
+            band, threads = cpu.pop("_band"), cpu.pop("_threads")
+            if not args.no_parity:
+                parity = parity_block(pkg, dev, args.scene, opts, height, band, threads)
         line = {
             "metric": METRIC, "value": round(value, 3), "unit": "Mrays/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3),
@@ -288,6 +334,8 @@ def main():
                          "avg_kernel_ms": round(avg_kernel_ms, 3), "launches_per_frame": launches_per_frame,
                          "algorithmic_bytes_per_launch": algo_bytes},
             "cpu_baseline": cpu,
+            # the timed frame against the CPU restatement (tests/parity.py bar)
+            "parity": parity,
             # traversal work of one frame (the counting pass of the same kernels)
             "work": {k: st[k] for k in ("rays", "camera_rays", "secondary_rays", "shadow_rays", "shadow_traced",
                                         "node_visits", "object_tests", "tri_tests", "shades")},

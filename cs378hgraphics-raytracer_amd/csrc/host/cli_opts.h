@@ -12,6 +12,7 @@
 #include <getopt.h>
 
 #include <cctype>
+#include <cerrno>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -135,6 +136,21 @@ inline void cli_load_json(CliOptions& o, const std::string& path) {  // TraceUI.
   o.aa_thresh = aat / 100.0;
 }
 
+// A whole decimal number in [lo, hi] for one of the long options the
+// reference lacks (atoi would turn "abc" into 0 and "-3" into a silent
+// fallback); false with a message otherwise.
+inline bool cli_int_arg(const char* name, const char* s, int lo, int hi, int& out) {
+  char* end = nullptr;
+  errno = 0;
+  const long v = std::strtol(s, &end, 10);
+  if (s[0] == '\0' || *end != '\0' || errno == ERANGE || v < lo || v > hi) {
+    std::cerr << "--" << name << " needs an integer in [" << lo << ", " << hi << "], got '" << s << "'" << std::endl;
+    return false;
+  }
+  out = static_cast<int>(v);
+  return true;
+}
+
 // Returns 0 on success, otherwise the exit code the reference would use.
 inline int cli_parse(int argc, char** argv, CliOptions& o) {
   static struct option longopts[] = {{"device", required_argument, nullptr, 1000},
@@ -201,12 +217,18 @@ inline int cli_parse(int argc, char** argv, CliOptions& o) {
             return 1;
         }
         break;
-      case 1000: o.device = std::atoi(optarg); break;
+      case 1000:
+        if (!cli_int_arg("device", optarg, 0, 1023, o.device)) return 1;
+        break;
       case 1001: o.stats = true; break;
       case 1002: o.dump_f64 = optarg; break;
       case 1003: o.dump_hits = optarg; break;
-      case 1004: o.gpus = std::atoi(optarg); break;
-      case 1005: o.tile = std::atoi(optarg); break;
+      case 1004:
+        if (!cli_int_arg("gpus", optarg, 1, 64, o.gpus)) return 1;
+        break;
+      case 1005:
+        if (!cli_int_arg("tile", optarg, 1, 4096, o.tile)) return 1;
+        break;
       case 'h':
         cli_usage(argv[0], o);
         return 1;

@@ -4,7 +4,8 @@
 // devices instead of threads).
 //
 //   parent  : parses the scene once (host only, no HIP call), forks N ranks,
-//             waits for them and returns the first failing exit status.
+//             reaps them as they end; on the first failing rank it ends the
+//             others (SIGTERM, then SIGKILL) and returns that rank's status.
 //   rank r  : device r; rtx_scene_create; ncclCommInitRank over a unique id
 //             that rank 0 publishes in a shared page; renders the 32x32 tiles
 //             the deal gives shard r (rtx_render, packed tile order, output
@@ -18,7 +19,9 @@
 #include <unistd.h>
 
 #include <atomic>
+#include <cerrno>
 #include <chrono>
+#include <csignal>
 #include <cstdio>
 #include <cstring>
 #include <iostream>
@@ -38,10 +41,32 @@ namespace {
 // the page the ranks share (created before the fork)
 struct Rendezvous {
   std::atomic<int> id_ready;  // 1: uid holds rank 0's ncclUniqueId; -1: rank 0 failed
+  std::atomic<int> joined;    // ranks whose scene and buffers are up (ready for the communicator)
+  std::atomic<int> failed;    // 1: some rank failed before the collectives
   ncclUniqueId uid;
   double rank_ms[64];         // render + gather wall time per rank
   long long rank_rays[64];
 };
+
+// No rank enters ncclCommInitRank (which blocks until all ranks have) until
+// every rank got its device, scene and buffers: a rank that fails before
+// that publishes it here, and the others return instead of waiting for it
+// forever.  (Failures after the collectives started are ended by the
+// parent, which terminates the remaining ranks on the first non-zero exit.)
+bool rendezvous_join(Rendezvous* rv, int rank, int nranks) {
+  rv->joined.fetch_add(1);
+  const auto t0 = std::chrono::steady_clock::now();
+  for (;;) {
+    if (rv->failed.load()) return false;
+    if (rv->joined.load() >= nranks) return true;
+    if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(120)) {
+      std::cerr << "rank " << rank << ": the other ranks did not come up" << std::endl;
+      rv->failed.store(1);
+      return false;
+    }
+    std::this_thread::sleep_for(std::chrono::milliseconds(1));
+  }
+}
 
 #define NCCL_CHECK(expr, what)                                                      \
   do {                                                                              \
@@ -85,7 +110,17 @@ int run_rank(const rtxh::CliOptions& o, void* hs, int rank, int nranks, Rendezvo
     }
     if (rv->id_ready.load() < 0) return 3;
   }
+  // everything up to the communicator: a failure is published (rendezvous)
+  auto early = [&](int code) {
+    rv->failed.store(1);
+    return code;
+  };
   const int device = o.device + rank;
+  int ndev = 0;
+  if (rtx_device_count(&ndev) != RTX_OK || device >= ndev) {
+    std::cerr << "rank " << rank << ": no GPU " << device << " (" << ndev << " visible)" << std::endl;
+    return early(2);
+  }
   RtxSceneDesc desc;
   rtx_host_desc(hs, &desc);
   RtxHostInfo info;
@@ -93,13 +128,17 @@ int run_rank(const rtxh::CliOptions& o, void* hs, int rank, int nranks, Rendezvo
   void* scene = nullptr;
   if (rtx_scene_create(device, &desc, &scene) != RTX_OK) {
     std::cerr << "rank " << rank << ": rtx: " << rtx_last_error() << std::endl;
-    return 2;
+    return early(2);
   }
-  HIP_CHECK(hipSetDevice(device), "hipSetDevice");
-  ncclComm_t comm;
-  NCCL_CHECK(ncclCommInitRank(&comm, nranks, rv->uid, rank), "ncclCommInitRank");
+  if (hipSetDevice(device) != hipSuccess) {
+    std::cerr << "rank " << rank << ": hipSetDevice failed" << std::endl;
+    return early(3);
+  }
   hipStream_t stream;
-  HIP_CHECK(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking), "hipStreamCreate");
+  if (hipStreamCreateWithFlags(&stream, hipStreamNonBlocking) != hipSuccess) {
+    std::cerr << "rank " << rank << ": hipStreamCreate failed" << std::endl;
+    return early(3);
+  }
 
   const int width = o.size;
   const int height = rtx_image_height(width, info.aspect);
@@ -120,9 +159,15 @@ int run_rank(const rtxh::CliOptions& o, void* hs, int rank, int nranks, Rendezvo
   const size_t shard_bytes = size_t(maxpix) * 3;
   uint8_t* d_send = nullptr;
   uint8_t* d_recv = nullptr;
-  HIP_CHECK(hipMalloc(&d_send, shard_bytes > 0 ? shard_bytes : 1), "hipMalloc");
-  HIP_CHECK(hipMemsetAsync(d_send, 0, shard_bytes, stream), "hipMemset");
-  if (rank == 0) HIP_CHECK(hipMalloc(&d_recv, shard_bytes * nranks > 0 ? shard_bytes * nranks : 1), "hipMalloc");
+  if (hipMalloc(&d_send, shard_bytes > 0 ? shard_bytes : 1) != hipSuccess ||
+      hipMemsetAsync(d_send, 0, shard_bytes, stream) != hipSuccess ||
+      (rank == 0 && hipMalloc(&d_recv, shard_bytes * nranks > 0 ? shard_bytes * nranks : 1) != hipSuccess)) {
+    std::cerr << "rank " << rank << ": device buffers: out of memory" << std::endl;
+    return early(3);
+  }
+  if (!rendezvous_join(rv, rank, nranks)) return 3;
+  ncclComm_t comm;
+  NCCL_CHECK(ncclCommInitRank(&comm, nranks, rv->uid, rank), "ncclCommInitRank");
   RtxStats st;
   HIP_CHECK(hipStreamSynchronize(stream), "hipStreamSynchronize");
   const auto t0 = std::chrono::steady_clock::now();
@@ -172,6 +217,8 @@ int rtx_cli_multi_gpu(const rtxh::CliOptions& o, void* hs) {
   }
   Rendezvous* rv = new (page) Rendezvous();
   rv->id_ready.store(0);
+  rv->joined.store(0);
+  rv->failed.store(0);
   std::vector<pid_t> kids;
   const auto t0 = std::chrono::steady_clock::now();
   for (int r = 0; r < n; ++r) {
@@ -191,15 +238,52 @@ int rtx_cli_multi_gpu(const rtxh::CliOptions& o, void* hs) {
     }
     kids.push_back(pid);
   }
+  // Reap the ranks in the order they end.  The first rank to fail ends the
+  // job: the others may be blocked in a collective waiting for it, so they
+  // get SIGTERM, then SIGKILL after a grace period; the job returns the
+  // failing rank's status.
   int rc = 0;
-  for (pid_t k : kids) {
+  std::vector<bool> alive(kids.size(), true);
+  size_t left = kids.size();
+  bool terminating = false;
+  auto kill_rest = [&](int sig) {
+    for (size_t r = 0; r < kids.size(); ++r)
+      if (alive[r]) kill(kids[r], sig);
+  };
+  auto t_term = std::chrono::steady_clock::now();
+  while (left > 0) {
     int status = 0;
-    if (waitpid(k, &status, 0) < 0) {
+    const pid_t pid = waitpid(-1, &status, terminating ? WNOHANG : 0);
+    if (pid < 0) {
+      if (errno == EINTR) continue;
       rc = rc ? rc : 1;
+      break;
+    }
+    if (pid == 0) {  // terminating: ranks still running
+      if (std::chrono::steady_clock::now() - t_term > std::chrono::seconds(10)) {
+        kill_rest(SIGKILL);
+        terminating = false;  // block until they are reaped
+      } else {
+        std::this_thread::sleep_for(std::chrono::milliseconds(20));
+      }
       continue;
     }
+    size_t r = 0;
+    while (r < kids.size() && kids[r] != pid) ++r;
+    if (r == kids.size()) continue;
+    alive[r] = false;
+    --left;
     const int code = WIFEXITED(status) ? WEXITSTATUS(status) : 128 + (WIFSIGNALED(status) ? WTERMSIG(status) : 0);
-    if (code != 0 && rc == 0) rc = code;
+    if (code != 0 && rc == 0) {
+      rc = code;
+      if (left > 0) {
+        std::cerr << "rank " << r << " failed (status " << code << "): ending the other ranks" << std::endl;
+        rv->failed.store(1);
+        kill_rest(SIGTERM);
+        terminating = true;
+        t_term = std::chrono::steady_clock::now();
+      }
+    }
   }
   const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   if (o.stats && rc == 0) {

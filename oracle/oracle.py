@@ -93,12 +93,17 @@ def render(pkg, path: str, opts, rect=None, threads: int = 0, want_hits: bool = 
     w = opts.width
     rgb8 = np.zeros((h, w, 3), np.uint8)
     rgb = np.zeros((h, w, 3), np.float64)
+    # np.zeros maps lazily: with a rect only the rect's rows are touched (a
+    # band of the 3840x2160x64 C5 frame must not commit 17 GB of records)
     hits = np.zeros((h, w, opts.spp), pkg.HIT_DTYPE) if want_hits else None
-    if hits is not None:
-        hits["object"] = -1
     r = OracleRect(0, 0, 0, 0, threads)
     if rect is not None:
         r.x0, r.y0, r.x1, r.y1 = rect
+    if hits is not None:
+        if rect is not None:
+            hits[rect[1]:rect[3], rect[0]:rect[2]]["object"] = -1
+        else:
+            hits["object"] = -1
     st = pkg.RtxStats()
     rc = L.oracle_render(path.encode(), opts.cubemap.encode(), C.byref(p), C.byref(r), rgb8.ctypes.data, rgb.ctypes.data,
                          hits.ctypes.data if hits is not None else None, C.byref(st))

@@ -57,3 +57,29 @@ def test_multi_gpu_cli_equals_single(pkg, tmp_path, scene, flags):
         got = pkg.read_image(str(out))
         assert np.array_equal(got, want), f"--gpus {n} differs from the single-GPU render"
         assert '"gpus": %d' % n in r.stdout
+
+
+def test_bad_numeric_options_refused():
+    """--gpus / --tile / --device take whole numbers in range:
+    no silent fallback to one GPU or to 32x32 tiles."""
+    for args in (["--gpus", "abc"], ["--gpus", "0"], ["--tile", "0"], ["--tile", "-4"], ["--device", "x1"]):
+        r = _run(args + [scene_path("hitchcock.ray"), "/tmp/never.png"])
+        assert r.returncode == 1, (args, r.returncode, r.stderr)
+        assert "--" + args[0].lstrip("-") in r.stderr
+
+
+@pytest.mark.gpu
+def test_multi_gpu_more_ranks_than_devices_fails_fast(pkg, tmp_path):
+    """A rank that cannot come up (here: more ranks than visible GPUs) makes
+    the job exit non-zero within a bound instead of leaving the other ranks
+    blocked in ncclCommInitRank / ncclGather (multi_gpu.cpp: the rendezvous
+    page's failure flag and the parent's termination of the remaining
+    ranks)."""
+    import time
+
+    n = _device_count(pkg) + 1
+    t0 = time.monotonic()
+    r = _run(["--gpus", str(n), "-w", "32", scene_path("hitchcock.ray"), str(tmp_path / "x.png")], timeout=90)
+    assert r.returncode != 0, r.stdout
+    assert time.monotonic() - t0 < 60
+    assert "no GPU" in r.stderr, r.stderr
