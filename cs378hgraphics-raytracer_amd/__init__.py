@@ -129,6 +129,7 @@ def host_lib():
                                        C.POINTER(C.c_int32), C.c_void_p, C.c_int64]
         lib.rtx_shard_tiles.argtypes = [C.c_int32, C.c_int32, C.c_int32, C.c_int32, C.c_int32, C.c_void_p,
                                         C.c_int32, C.POINTER(C.c_int32)]
+        lib.rtx_host_tokens.argtypes = [C.c_char_p, C.c_char_p, C.c_int64, C.POINTER(C.c_int64)]
         lib.rtx_unpack_tiles.argtypes = [C.c_void_p, C.c_int32, C.c_int32, C.c_int32, C.c_int32, C.c_int32,
                                          C.c_int32, C.c_void_p]
         _host = lib
@@ -162,7 +163,7 @@ HIP_SYMBOLS = ["rtx_last_error", "rtx_device_count", "rtx_scene_create", "rtx_sc
                "rtx_shard_pixels", "rtx_kernel_time"]
 HOST_SYMBOLS = ["rtx_host_last_error", "rtx_host_load", "rtx_host_desc", "rtx_host_info", "rtx_host_free",
                 "rtx_host_cubemap", "rtx_write_image", "rtx_image_height", "rtx_read_image", "rtx_shard_tiles",
-                "rtx_unpack_tiles"]
+                "rtx_unpack_tiles", "rtx_host_tokens"]
 
 
 def _check_host(rc, what):

@@ -16,8 +16,10 @@
 // (kdTree.h:100-117).
 #include <algorithm>
 #include <cstring>
+#include <fstream>
 #include <memory>
 #include <numeric>
+#include <sstream>
 #include <string>
 
 #include "../../../include/rtx_host.h"
@@ -438,6 +440,30 @@ rtx_status rtx_write_image(const char* path, int32_t w, int32_t h, const uint8_t
   return RTX_OK;
 }
 
+rtx_status rtx_host_tokens(const char* ray_path, char* out, int64_t cap, int64_t* need) {
+  if (!ray_path || !need) {
+    g_host_err = "rtx_host_tokens: null argument";
+    return RTX_ERR_INVALID;
+  }
+  std::ifstream ifs(ray_path, std::ios::binary);
+  if (!ifs) {
+    g_host_err = std::string("Error: couldn't read scene file ") + ray_path;
+    return RTX_ERR_INVALID;
+  }
+  std::stringstream ss;
+  ss << ifs.rdbuf();
+  const std::string t = rtxh::dump_ray_tokens(ss.str());
+  *need = static_cast<int64_t>(t.size()) + 1;
+  if (out) {
+    if (cap < *need) {
+      g_host_err = "rtx_host_tokens: output buffer too small";
+      return RTX_ERR_INVALID;
+    }
+    std::memcpy(out, t.c_str(), t.size() + 1);
+  }
+  return RTX_OK;
+}
+
 int32_t rtx_image_height(int32_t width, double aspect) {
   return static_cast<int32_t>(width / aspect + 0.5);
 }
@@ -448,7 +474,13 @@ rtx_status rtx_read_image(const char* path, int32_t* w, int32_t* h, int32_t* cha
     return RTX_ERR_INVALID;
   }
   int iw = 0, ih = 0;
-  std::vector<uint8_t> d = rtxh::read_image(path, iw, ih);
+  std::vector<uint8_t> d;
+  try {
+    d = rtxh::read_image(path, iw, ih);
+  } catch (const std::exception& e) {  // (bad_alloc on a huge image: an error, not terminate)
+    g_host_err = std::string("rtx_read_image: ") + e.what();
+    return RTX_ERR_INVALID;
+  }
   if (d.empty()) {
     g_host_err = std::string("Unable to load texture map '") + path + "'.";
     return RTX_ERR_INVALID;

@@ -85,7 +85,9 @@ bool write_bmp(const std::string& fn, int width, int height, const uint8_t* data
   uint8_t hdr[54] = {0};
   auto w32 = [&](int o, uint32_t v) { for (int k = 0; k < 4; ++k) hdr[o + k] = uint8_t(v >> (8 * k)); };
   hdr[0] = 'B'; hdr[1] = 'M';
-  w32(2, 54 + bytes * height);
+  // bfSize counts sizeof(BMP_BITMAPFILEHEADER), which is 16 with the
+  // struct's padding, not the 14 bytes written (bitmap.cpp:105)
+  w32(2, 56 + bytes * height);
   w32(10, 54);
   w32(14, 40);
   w32(18, width);
@@ -96,8 +98,15 @@ bool write_bmp(const std::string& fn, int width, int height, const uint8_t* data
   w32(42, 2834);
   std::fwrite(hdr, 1, 54, f);
   std::vector<uint8_t> line(bytes, 0);
+  // The reference copies the PADDED row length from the packed buffer
+  // (bitmap.cpp:137), so a row's padding holds the first bytes of the next
+  // row; for the last row it reads past the buffer (undefined: decision
+  // U25, zeros here).
+  const size_t total = size_t(width) * 3 * height;
   for (int j = 0; j < height; ++j) {
-    std::memcpy(line.data(), data + size_t(j) * 3 * width, size_t(width) * 3);
+    const size_t at = size_t(j) * 3 * width;
+    std::fill(line.begin(), line.end(), 0);
+    std::memcpy(line.data(), data + at, std::min(size_t(bytes), total - at));
     for (int i = 0; i < width; ++i) std::swap(line[i * 3], line[i * 3 + 2]);
     std::fwrite(line.data(), 1, bytes, f);
   }
@@ -265,7 +274,11 @@ std::vector<uint8_t> read_png(const std::string& fn, int& width, int& height) {
     }
     pos += 12 + size_t(len);
   }
-  if (w == 0 || h == 0 || w > (1u << 24) || h > (1u << 24) || interlace > 1) return {};
+  // at most 2^28 pixels (a 16k x 16k texture), so a few-byte header cannot
+  // ask for a multi-terabyte allocation
+  if (w == 0 || h == 0 || w > (1u << 24) || h > (1u << 24) || uint64_t(w) * h > (uint64_t(1) << 28) ||
+      interlace > 1)
+    return {};
   int spp_in;  // samples per pixel in the file
   switch (ctype) {
     case 0: spp_in = 1; break;
@@ -290,6 +303,9 @@ std::vector<uint8_t> read_png(const std::string& fn, int& width, int& height) {
     const uint32_t ph = interlace ? (h + A7[p][3] - 1 - A7[p][1]) / A7[p][3] : h;
     if (pw && ph) raw_len += size_t(ph) * ((size_t(pw) * bits_px + 7) / 8 + 1);
   }
+  // deflate expands at most ~1032:1: a stream too short for the header's
+  // size is a truncated or forged file, rejected before allocating
+  if (raw_len > idat.size() * 1032 + 4096) return {};
   std::vector<uint8_t> raw(raw_len);
   {
     z_stream zs;

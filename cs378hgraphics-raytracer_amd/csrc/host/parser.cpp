@@ -13,6 +13,7 @@
 // (RayTracer.cpp:216-234).
 #include <dirent.h>
 #include <cmath>
+#include <cstdio>
 #include <cstdlib>
 #include <fstream>
 #include <list>
@@ -1013,6 +1014,58 @@ SceneModel parse_ray_text(const std::string& text, const std::string& base_path)
   Tokenizer tk(text);
   Parser p(tk, base_path);
   return p.parseScene();
+}
+
+namespace {
+// A token's name as the reference prints it (Token::toString: getNameForToken,
+// Token.cpp:27-107, which has no entry for fov / gennormals — those print the
+// reserved word itself here).
+const char* token_text(Sym s) {
+  switch (s) {
+    case IDENT: return "Identifier";
+    case SCALAR: return "Scalar";
+    case SYMTRUE: return "true";
+    case SYMFALSE: return "false";
+    case EOFSYM: case SBT_RAYTRACER: case LPAREN: case RPAREN: case LBRACE: case RBRACE: case COMMA: case EQUALS:
+    case SEMICOLON: case MATERIAL:
+      return sym_name(s);
+    default: break;
+  }
+  static const std::map<Sym, std::string> canon = [] {
+    std::map<Sym, std::string> m;
+    for (const auto& kv : reserved())  // the reference's name: the canonical spelling of aliases
+      if (!m.count(kv.second) || kv.first == "trimesh" || kv.first == "color") m[kv.second] = kv.first;
+    return m;
+  }();
+  auto it = canon.find(s);
+  return it == canon.end() ? "Unknown token type" : it->second.c_str();
+}
+}  // namespace
+
+// The token stream of a .ray text, one token per line: its name, then a
+// tab and the identifier or the scalar (%.17g) — Tokenizer(fp, printTokens)
+// (Tokenizer.cpp:39-46, 119-123) made comparable; "ERROR" after the tokens
+// read before a syntax error.
+std::string dump_ray_tokens(const std::string& text) {
+  std::ostringstream o;
+  try {
+    Tokenizer tk(text);
+    for (;;) {
+      const Token t = tk.get();
+      o << token_text(t.kind);
+      if (t.kind == IDENT) o << '\t' << t.ident;
+      if (t.kind == SCALAR) {
+        char b[40];
+        std::snprintf(b, sizeof(b), "%.17g", t.value);
+        o << '\t' << b;
+      }
+      o << '\n';
+      if (t.kind == EOFSYM) break;
+    }
+  } catch (const ParseError&) {
+    o << "ERROR\n";
+  }
+  return o.str();
 }
 
 SceneModel parse_ray_file_raw(const std::string& path) {  // RayTracer::loadScene's parse (RayTracer.cpp:196-240)

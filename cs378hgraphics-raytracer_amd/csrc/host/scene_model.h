@@ -166,6 +166,8 @@ struct ParseError : public std::runtime_error {
 // Throws ParseError with the reference's messages on malformed input.
 SceneModel parse_ray_file_raw(const std::string& path);
 SceneModel parse_ray_text(const std::string& text, const std::string& base_path);
+// the tokenizer's output, one token per line (rtx_host_tokens)
+std::string dump_ray_tokens(const std::string& text);
 // Product scene build (scene_build.cpp): the derived fields from the raw
 // records (TransformNode ctor, Geometry::ComputeBoundingBox, Camera,
 // Trimesh::addFace / generateNormals / ComputeLocalBoundingBox, light ctors).

@@ -65,6 +65,13 @@ rtx_status rtx_shard_tiles(int32_t width, int32_t height, int32_t tile, int32_t 
  * (row 0 = bottom) — the reassembly after the gather. */
 rtx_status rtx_unpack_tiles(const void* packed, int32_t width, int32_t height, int32_t tile, int32_t shard,
                             int32_t nshards, int32_t elem, void* frame);
+/* The tokenizer's view of a .ray file (Tokenizer(fp, printTokens = true),
+ * parser/Tokenizer.cpp:39-46,119-123; token names of Token::toString,
+ * Token.cpp:27-107): one token per line — its name, then a tab and the
+ * identifier or the scalar as %.17g — ending with "EOF", or with "ERROR"
+ * after the tokens read before a syntax error.  `out` (capacity `cap`
+ * bytes, NUL-terminated) may be NULL to query `*need`. */
+rtx_status rtx_host_tokens(const char* ray_path, char* out, int64_t cap, int64_t* need);
 /* height the CLI derives from -w (CommandLineUI.cpp:156) */
 int32_t rtx_image_height(int32_t width, double aspect);
 
