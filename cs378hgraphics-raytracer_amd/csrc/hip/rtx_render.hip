@@ -26,6 +26,7 @@
 #include <cmath>
 #include <cstdio>
 #include <cstring>
+#include <memory>
 #include <string>
 #include <type_traits>
 #include <vector>
@@ -60,6 +61,15 @@ using rtm::mk3;
 
 
 // ============================================================ frame parameters
+// A region of adaptaa's recursion below the pixel (RayTracer.cpp:316-365):
+// its rectangle in image coordinates, the region of the level above that
+// subdivided (`parent`: a pixel's output slot at level 1) and which quarter
+// it is (child = 2a + b of adaptaa's loops).
+struct ARegion {
+  double x1, x2, y1, y2;
+  int parent, child;
+};
+
 struct FrameParams {
   RtxRenderParams P;
   RtxCamera cam;
@@ -100,6 +110,11 @@ struct FrameParams {
   // wterm[(light * nslot + slot) * 3 + c]
   int fuse;
   double* wterm;
+  // adaptive AA on the wavefront path: a work unit is (region, Hammersley
+  // index k) — level 0's regions are the pixels (item_pixel), a deeper
+  // level's are aregs[0 .. n_samples / spp) (adapt_stats_kernel)
+  int adapt;
+  const ARegion* aregs;
 };
 
 // Tile deal: deal index d = shard + k * nshards is tile row d / tiles_x,
@@ -1513,24 +1528,45 @@ __device__ __forceinline__ void claim_sample(LaneRef& L, const FrameParams& F, R
     const int64_t item = sid / (F.ppw * F.spp);
     const int sl = static_cast<int>(sid % (F.ppw * F.spp));
     const int pix = sl / F.spp, smp = sl % F.spp;
-    int i, j;
     int64_t oidx;
-    if (!item_pixel(F, item, pix, i, j, oidx)) continue;
-    int pi = i, pj = j;
-    double ssx = 1.0, ssy = 1.0;
-    if (P.aa_mode != RTX_AA_NONE) {  // tracePixel(i*s + si, j*s + sj)
-      pi = i * F.s + smp / F.s;
-      pj = j * F.s + smp % F.s;
-      ssx = F.s;
-      ssy = F.s;
+    bool rec = hits != nullptr;
+    if (F.adapt) {
+      // adaptaa's sample k of a region: trace(hammersley(k, s*s) * (w, h) +
+      // (x1, y1)) (RayTracer.cpp:333-337; hammersley's y is 0, U7)
+      double x1, x2, y1, y2;
+      if (F.aregs) {
+        const ARegion R = F.aregs[item];
+        x1 = R.x1, x2 = R.x2, y1 = R.y1, y2 = R.y2;
+        oidx = item;
+        rec = false;  // hit records: the pixel's own samples only
+      } else {
+        int i, j;
+        if (!item_pixel(F, item, 0, i, j, oidx)) continue;
+        x1 = double(i) / double(P.width), x2 = double(i + 1) / double(P.width);
+        y1 = double(j) / double(P.height), y2 = double(j + 1) / double(P.height);
+        if (x1 + 0.0001 >= x2 || y1 + 0.0001 >= y2) continue;  // the whole pixel under eps: black (U8)
+      }
+      L.sx() = radinv2(smp) * (x2 - x1) + x1;
+      L.sy() = (0.0 / F.spp) * (y2 - y1) + y1;
+    } else {
+      int i, j;
+      if (!item_pixel(F, item, pix, i, j, oidx)) continue;
+      int pi = i, pj = j;
+      double ssx = 1.0, ssy = 1.0;
+      if (P.aa_mode != RTX_AA_NONE) {  // tracePixel(i*s + si, j*s + sj)
+        pi = i * F.s + smp / F.s;
+        pj = j * F.s + smp % F.s;
+        ssx = F.s;
+        ssy = F.s;
+      }
+      L.sx() = double(pi) / (double(P.width) * ssx);  // tracePixel (RayTracer.cpp:87-88)
+      L.sy() = double(pj) / (double(P.height) * ssy);
     }
-    L.sx() = double(pi) / (double(P.width) * ssx);  // tracePixel (RayTracer.cpp:87-88)
-    L.sy() = double(pj) / (double(P.height) * ssy);
     L.sample_slot() = static_cast<int>(oidx * F.spp + smp);
     // the buckets' owner: the sample, or with the DoF split its camera ray
     L.bunit() = F.cam_split ? L.sample_slot() * F.ncam + cam0 : L.sample_slot();
     if (F.fork_on) F.fmask[L.bunit()] = 0u;  // no bucket written yet (forks come later)
-    L.rec_on() = hits != nullptr;
+    L.rec_on() = rec;
     L.pass() = 0;
     L.camk() = cam0;
     L.cam_end() = F.cam_split ? cam0 + 1 : F.ncam;
@@ -2066,6 +2102,57 @@ __global__ void __launch_bounds__(WG) lane_init_kernel(LaneMem lm, int first, in
   lane_init(L);
 }
 
+// trace()'s value of sample sid (RayTracer.cpp:35-79) from the sample buffer:
+//   DoF split — the sample's camera rays' sums added in order, scaled and
+//     clamped (RayTracer.cpp:73-77); a camera ray's sum is its root's plus,
+//     with buckets, its buckets in heap order;
+//   buckets — the root's sum plus the forked sub-trees' sums in heap order,
+//     then the clamp (RayTracer.cpp:77);
+//   otherwise the buffer holds the clamped value already.
+__device__ __forceinline__ dvec3 sample_value(const FrameParams& F, const double* __restrict__ sbuf, int64_t sid) {
+  auto unit_sum = [&](int64_t uid) {
+    const double* r = sbuf + uid * 3;
+    dvec3 u = mk3(r[0], r[1], r[2]);
+    if (F.fork_on) {
+      unsigned int m = F.fmask[uid];
+      while (m) {
+        const int b = __builtin_ctz(m);
+        m &= m - 1;
+        const double* f = F.fbuf + (uid * F.fork_npos + b) * 3;
+        u += mk3(f[0], f[1], f[2]);
+      }
+    }
+    return u;
+  };
+  if (F.cam_split) {
+    dvec3 ret = unit_sum(sid * F.ncam);
+    for (int k = 1; k < F.ncam; ++k) ret += unit_sum(sid * F.ncam + k);
+    ret *= (1.0 / (F.P.dof_div + 1.0));
+    return rtm::gclamp3(ret, 0.0, 1.0);
+  }
+  if (F.fork_on) return rtm::gclamp3(unit_sum(sid), 0.0, 1.0);
+  return ld3(sbuf + sid * 3);
+}
+
+// The pixel (i, j) of output slot o, false for a slot this frame does not
+// write: outside the image (packed tiles at the border) or, on a sharded
+// full frame, another shard's tile.
+__device__ __forceinline__ bool slot_pixel(const FrameParams& F, int64_t o, int& i, int& j) {
+  if (F.P.packed && F.P.tile > 0) {
+    const int64_t k = o / (int64_t(F.tw) * F.th);
+    const int r = static_cast<int>(o % (int64_t(F.tw) * F.th));
+    int tx, ty;
+    deal_tile(F.P.shard + static_cast<int>(k) * F.P.nshards, F.tiles_x, tx, ty);
+    i = tx * F.tw + r % F.tw;
+    j = ty * F.th + r / F.tw;
+    return i < F.P.width && j < F.P.height;
+  }
+  i = static_cast<int>(o % F.P.width);
+  j = static_cast<int>(o / F.P.width);
+  if (F.P.tile > 0) return tile_deal(i / F.tw, j / F.th, F.tiles_x) % F.P.nshards == F.P.shard;
+  return true;
+}
+
 // Per-pixel ordered reduction of the sample buffer (RayTracer.cpp:288-298:
 // col += tracePixel(...) in si-major order, col /= s*s; setPixel truncates).
 __global__ void __launch_bounds__(WG) reduce_kernel(const FrameParams* __restrict__ Fp, const double* __restrict__ sbuf,
@@ -2074,66 +2161,10 @@ __global__ void __launch_bounds__(WG) reduce_kernel(const FrameParams* __restric
   const FrameParams& F = *Fp;
   const int64_t o = static_cast<int64_t>(blockIdx.x) * WG + threadIdx.x;
   if (o >= npix_slots) return;
-  // skip slots that map outside the image (packed tiles at the border)
-  if (F.P.packed && F.P.tile > 0) {
-    const int64_t k = o / (int64_t(F.tw) * F.th);
-    const int r = static_cast<int>(o % (int64_t(F.tw) * F.th));
-    int tx, ty;
-    deal_tile(F.P.shard + static_cast<int>(k) * F.P.nshards, F.tiles_x, tx, ty);
-    const int i = tx * F.tw + r % F.tw;
-    const int j = ty * F.th + r / F.tw;
-    if (i >= F.P.width || j >= F.P.height) return;
-  } else if (F.P.tile > 0) {  // full frame, sharded: only this shard's tiles
-    const int i = static_cast<int>(o % F.P.width), j = static_cast<int>(o / F.P.width);
-    if (tile_deal(i / F.tw, j / F.th, F.tiles_x) % F.P.nshards != F.P.shard) return;
-  }
+  int i, j;
+  if (!slot_pixel(F, o, i, j)) return;
   dvec3 acc = mk3(0.0, 0.0, 0.0);
-  if (F.cam_split) {
-    // DoF split: a sample = its camera rays' sums added in order, then
-    // trace()'s scale and clamp (RayTracer.cpp:73-77)
-    const double* s = sbuf + o * F.spp * F.ncam * 3;
-    // a camera ray's sum: its root's plus (forking) its buckets in heap order
-    auto unit_sum = [&](int q, int k) {
-      const double* r = s + (q * F.ncam + k) * 3;
-      dvec3 u = mk3(r[0], r[1], r[2]);
-      if (F.fork_on) {
-        const int64_t uid = (o * F.spp + q) * F.ncam + k;
-        unsigned int m = F.fmask[uid];
-        while (m) {
-          const int b = __builtin_ctz(m);
-          m &= m - 1;
-          const double* f = F.fbuf + (uid * F.fork_npos + b) * 3;
-          u += mk3(f[0], f[1], f[2]);
-        }
-      }
-      return u;
-    };
-    for (int q = 0; q < F.spp; ++q) {
-      dvec3 ret = unit_sum(q, 0);
-      for (int k = 1; k < F.ncam; ++k) ret += unit_sum(q, k);
-      ret *= (1.0 / (F.P.dof_div + 1.0));
-      acc += rtm::gclamp3(ret, 0.0, 1.0);
-    }
-  } else if (F.fork_on) {
-    // forked ray trees: the root's sum plus the forked sub-trees' sums in
-    // heap order, then trace()'s clamp (RayTracer.cpp:77)
-    const double* s = sbuf + o * F.spp * 3;
-    for (int q = 0; q < F.spp; ++q) {
-      dvec3 ret = mk3(s[q * 3 + 0], s[q * 3 + 1], s[q * 3 + 2]);
-      const int64_t sid = o * F.spp + q;
-      unsigned int m = F.fmask[sid];
-      while (m) {
-        const int b = __builtin_ctz(m);
-        m &= m - 1;
-        const double* f = F.fbuf + (sid * F.fork_npos + b) * 3;
-        ret += mk3(f[0], f[1], f[2]);
-      }
-      acc += rtm::gclamp3(ret, 0.0, 1.0);
-    }
-  } else {
-    const double* s = sbuf + o * F.spp * 3;
-    for (int q = 0; q < F.spp; ++q) acc += mk3(s[q * 3 + 0], s[q * 3 + 1], s[q * 3 + 2]);
-  }
+  for (int q = 0; q < F.spp; ++q) acc += sample_value(F, sbuf, o * F.spp + q);
   if (F.P.aa_mode != RTX_AA_NONE) acc = acc / double(F.s * F.s);
   if (rgb8) {
     rgb8[o * 3 + 0] = rtm::to_byte(acc.x);
@@ -2144,6 +2175,150 @@ __global__ void __launch_bounds__(WG) reduce_kernel(const FrameParams* __restric
     rgbf[o * 3 + 0] = acc.x;
     rgbf[o * 3 + 1] = acc.y;
     rgbf[o * 3 + 2] = acc.z;
+  }
+}
+
+// ============================================================ adaptive AA, wavefront path
+// adaptaa (RayTracer.cpp:316-365) level by level.  A level's regions run
+// their s*s samples as ordinary work units of the wavefront machine
+// (claim_sample); then
+//   adapt_stats_kernel   — each region's mean and deviation in the
+//                          reference's order; keeps mu, or marks the region
+//                          for subdivision and counts its quarters above eps;
+//   adapt_emit_kernel    — appends the marked regions' quarters to the next
+//                          level (their order there does not matter: each
+//                          keeps its parent and quarter);
+//   adapt_combine_kernel — deepest level first: a subdivided region's value
+//                          is (sum of its quarters' values, in adaptaa's loop
+//                          order, 0 for a quarter under eps) * 1/4; level 0
+//                          writes the pixel (setPixel).
+// With the default threshold no region subdivides and a frame is one level:
+// the samples, one stats launch, one combine launch.
+struct ALevel {
+  dvec3* val;          // [n] region value
+  int* first;          // [n] -1 kept; -2 subdivided, quarters not yet emitted; >= 0 first quarter's index below
+  int* mask;           // [n] quarters present below (bit 2a + b)
+  const ARegion* reg;  // [n] the regions (level >= 1; level 0's are the output slots' pixels)
+  int64_t n;
+};
+
+// The regions [r0, r0 + nr) of a level whose samples are sample ids
+// (r - r0) * spp + k of the sample buffer.
+__global__ void __launch_bounds__(WG) adapt_stats_kernel(const FrameParams* __restrict__ Fp,
+                                                          const double* __restrict__ sbuf, ALevel lv, int64_t r0,
+                                                          int64_t nr, unsigned int* __restrict__ nsub) {
+  const FrameParams& F = *Fp;
+  const int64_t t = static_cast<int64_t>(blockIdx.x) * WG + threadIdx.x;
+  if (t >= nr) return;
+  const int64_t r = r0 + t;
+  double x1, x2, y1, y2;
+  if (lv.reg) {
+    const ARegion R = lv.reg[r];
+    x1 = R.x1, x2 = R.x2, y1 = R.y1, y2 = R.y2;
+  } else {
+    int i, j;
+    if (!slot_pixel(F, r, i, j)) {
+      lv.first[r] = -1;
+      return;
+    }
+    x1 = double(i) / double(F.P.width), x2 = double(i + 1) / double(F.P.width);
+    y1 = double(j) / double(F.P.height), y2 = double(j + 1) / double(F.P.height);
+    if (x1 + 0.0001 >= x2 || y1 + 0.0001 >= y2) {  // no samples: black (U8)
+      lv.val[r] = mk3(0.0, 0.0, 0.0);
+      lv.first[r] = -1;
+      return;
+    }
+  }
+  const int an = F.spp;
+  dvec3 mu = mk3(0.0, 0.0, 0.0), sd = mk3(0.0, 0.0, 0.0);
+  for (int k = 0; k < an; ++k) mu += sample_value(F, sbuf, t * an + k);
+  mu *= (1.0 / (an));
+  for (int k = 0; k < an; ++k) {
+    const dvec3 s_c = sample_value(F, sbuf, t * an + k);
+    sd += mk3(pow(fabs(s_c.x - mu.x), 2.0), pow(fabs(s_c.y - mu.y), 2.0), pow(fabs(s_c.z - mu.z), 2.0));
+  }
+  sd *= (1.0 / (an - 1));
+  lv.val[r] = mu;
+  lv.first[r] = -1;
+  if (!(rtm::length(sd) > F.P.aa_thresh)) return;
+  const double xs[3] = {x1, (x1 + x2) / 2.0, x2};
+  const double ys[3] = {y1, (y1 + y2) / 2.0, y2};
+  int m = 0;
+  for (int c = 0; c < 4; ++c) {
+    const int a = c >> 1, b = c & 1;
+    if (!(xs[a] + 0.0001 >= xs[a + 1] || ys[b] + 0.0001 >= ys[b + 1])) m |= 1 << c;
+  }
+  lv.first[r] = -2;
+  lv.mask[r] = m;
+  if (m) atomicAdd(nsub, static_cast<unsigned int>(__popc(m)));
+}
+
+__global__ void __launch_bounds__(WG) adapt_emit_kernel(const FrameParams* __restrict__ Fp, ALevel lv, ARegion* next,
+                                                         unsigned int* __restrict__ cursor) {
+  const FrameParams& F = *Fp;
+  const int64_t r = static_cast<int64_t>(blockIdx.x) * WG + threadIdx.x;
+  if (r >= lv.n || lv.first[r] != -2) return;
+  double x1, x2, y1, y2;
+  if (lv.reg) {
+    const ARegion R = lv.reg[r];
+    x1 = R.x1, x2 = R.x2, y1 = R.y1, y2 = R.y2;
+  } else {
+    int i, j;
+    slot_pixel(F, r, i, j);
+    x1 = double(i) / double(F.P.width), x2 = double(i + 1) / double(F.P.width);
+    y1 = double(j) / double(F.P.height), y2 = double(j + 1) / double(F.P.height);
+  }
+  const double xs[3] = {x1, (x1 + x2) / 2.0, x2};
+  const double ys[3] = {y1, (y1 + y2) / 2.0, y2};
+  const int m = lv.mask[r];
+  const unsigned int base = m ? atomicAdd(cursor, static_cast<unsigned int>(__popc(m))) : 0u;
+  unsigned int k = base;
+  for (int c = 0; c < 4; ++c) {
+    if (!((m >> c) & 1)) continue;
+    const int a = c >> 1, b = c & 1;
+    ARegion q;
+    q.x1 = xs[a];
+    q.x2 = xs[a + 1];
+    q.y1 = ys[b];
+    q.y2 = ys[b + 1];
+    q.parent = static_cast<int>(r);
+    q.child = c;
+    next[k++] = q;
+  }
+  lv.first[r] = static_cast<int>(base);
+}
+
+// fold level `below` into `lv` (below.n == 0: nothing subdivided), and at
+// level 0 write the pixels
+__global__ void __launch_bounds__(WG) adapt_combine_kernel(const FrameParams* __restrict__ Fp, ALevel lv, ALevel below,
+                                                            uint8_t* __restrict__ rgb8, double* __restrict__ rgbf) {
+  const FrameParams& F = *Fp;
+  const int64_t r = static_cast<int64_t>(blockIdx.x) * WG + threadIdx.x;
+  if (r >= lv.n) return;
+  if (!lv.reg) {
+    int i, j;
+    if (!slot_pixel(F, r, i, j)) return;
+  }
+  dvec3 v = lv.val[r];
+  if (lv.first[r] != -1) {  // mu = 0; mu += subval (2 x 2, RayTracer.cpp:352-360); mu *= 1/4
+    const int m = lv.mask[r];
+    int k = lv.first[r];
+    dvec3 mu = mk3(0.0, 0.0, 0.0);
+    for (int c = 0; c < 4; ++c) mu += ((m >> c) & 1) ? below.val[k++] : mk3(0.0, 0.0, 0.0);
+    mu *= (1.0 / 4.0);
+    v = mu;
+    lv.val[r] = v;
+  }
+  if (lv.reg) return;
+  if (rgb8) {
+    rgb8[r * 3 + 0] = rtm::to_byte(v.x);
+    rgb8[r * 3 + 1] = rtm::to_byte(v.y);
+    rgb8[r * 3 + 2] = rtm::to_byte(v.z);
+  }
+  if (rgbf) {
+    rgbf[r * 3 + 0] = v.x;
+    rgbf[r * 3 + 1] = v.y;
+    rgbf[r * 3 + 2] = v.z;
   }
 }
 
@@ -2199,6 +2374,7 @@ struct SceneState {
   unsigned int* d_counters = nullptr;
   unsigned int* h_counters = nullptr;  // pinned
   DevScene* d_scene = nullptr;         // device copy of S_launch (shadow early-out)
+  unsigned int* d_acnt = nullptr;      // adaptive AA: regions to subdivide, emit cursor
   std::vector<hipEvent_t> ev_pool;
   size_t ev_used = 0;
   std::vector<hipEvent_t> ev_start, ev_stop;
@@ -2422,6 +2598,7 @@ rtx_status rtx_scene_destroy(void* scene) {
   if (st->d_frame) (void)hipFree(st->d_frame);
   if (st->d_work) (void)hipFree(st->d_work);
   if (st->d_stats) (void)hipFree(st->d_stats);
+  if (st->d_acnt) (void)hipFree(st->d_acnt);
   if (st->d_picks) (void)hipFree(st->d_picks);
   if (st->d_offv) (void)hipFree(st->d_offv);
   if (st->d_sbuf) (void)hipFree(st->d_sbuf);
@@ -2449,6 +2626,9 @@ static rtx_status build_frame(const SceneState* st, const RtxRenderParams* p, Fr
                               std::vector<double>& offv) {
   std::memset(&F, 0, sizeof(F));
   F.P = *p;
+  // adaptaa calls trace(), not tracePixel (RayTracer.cpp:305, :337): no
+  // anaglyph eye on adaptive frames
+  if (p->aa_mode == RTX_AA_ADAPTIVE) F.P.anaglyph = 0;
   F.cam = st->cam;
   if (p->width <= 0 || p->height <= 0) {
     g_err = "rtx_render: width/height must be positive";
@@ -2619,19 +2799,20 @@ rtx_status rtx_render(void* scene, const RtxRenderParams* params, uint8_t* rgb8,
   }
   const bool adaptive = params->aa_mode == RTX_AA_ADAPTIVE;
   const bool media = params->overlapping != 0;  // -O o: the kernels with the discoverMat states
-  // wavefront path by default; adaptive AA (per-pixel sample frames) and
-  // RTX_MEGAKERNEL=1 use the persistent megakernel (kernels)
+  // wavefront path by default (adaptive AA too: its levels run as work
+  // units, adapt_*_kernel); RTX_MEGAKERNEL=1 uses the persistent megakernel
+  // (kernels)
   const char* mk_env = getenv("RTX_MEGAKERNEL");
-  const bool megakernel = adaptive || (mk_env && atoi(mk_env) != 0);
+  const bool megakernel = mk_env && atoi(mk_env) != 0;
   // DoF on the wavefront path: each of a sample's divs + 1 camera rays is a
   // work unit of its own (17x the parallel units, paths 17x shorter)
   const char* split_env = getenv("RTX_DOF_SPLIT");
-  if (!megakernel && params->dof && !params->anaglyph && !(split_env && atoi(split_env) == 0)) {
+  if (!megakernel && params->dof && !F.P.anaglyph && !(split_env && atoi(split_env) == 0)) {
     F.cam_split = 1;
     F.n_samples *= F.ncam;
   }
   if (F.cam_split && hits) HIP_TRY(hipMemsetAsync(d_hits, 0xff, npix * F.spp * sizeof(RtxHitRecord), stream));
-  if (!adaptive) {
+  if (!(adaptive && megakernel)) {
     const size_t need = size_t(npix) * F.spp * (F.cam_split ? F.ncam : 1) * 3 * sizeof(double);
     if (need > st->sbuf_bytes) {
       if (st->d_sbuf) (void)hipFree(st->d_sbuf);
@@ -2667,7 +2848,7 @@ rtx_status rtx_render(void* scene, const RtxRenderParams* params, uint8_t* rgb8,
     }
     return RTX_OK;
   };
-  double* sb = adaptive ? nullptr : st->d_sbuf;
+  double* sb = adaptive && megakernel ? nullptr : st->d_sbuf;
   std::vector<std::pair<hipEvent_t, hipEvent_t>> frame_events;
 
   if (megakernel) {
@@ -2727,7 +2908,12 @@ rtx_status rtx_render(void* scene, const RtxRenderParams* params, uint8_t* rgb8,
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipEventRecord(e1, stream));
     frame_events.push_back({e0, e1});
-  } else {
+  }
+  // One run of the wavefront machine over F's work units (F.n_samples), whose
+  // samples land in sample ids [0, nout * spp) of the sample buffer: the
+  // whole frame, or one chunk of a deeper adaptive level (level0 false: the
+  // hit records are not reset, the buckets are sized for the chunk).
+  auto run_wavefront = [&](FrameParams& F, int64_t nout, bool level0) -> rtx_status {
     // ---------------- wavefront path
     // NSLOT path slots split into G groups, each iterating advance -> trace
     // (closest) -> trace (next) on its own stream, so one group's launch
@@ -2750,8 +2936,8 @@ rtx_status rtx_render(void* scene, const RtxRenderParams* params, uint8_t* rgb8,
     const char* fd_env = getenv("RTX_FORK_DEPTH");
     if (fd_env && atoi(fd_env) > 0) fork_depth = std::min(4, atoi(fd_env));
     // (DoF: with the camera-ray split each camera ray owns its buckets)
-    bool fork_ok = !(fork_env && atoi(fork_env) == 0) && !params->anaglyph && (!params->dof || F.cam_split);
-    const size_t nunit_out = size_t(npix) * F.spp * (F.cam_split ? F.ncam : 1);  // bucket owners
+    bool fork_ok = !(fork_env && atoi(fork_env) == 0) && !F.P.anaglyph && (!params->dof || F.cam_split);
+    const size_t nunit_out = size_t(nout) * F.spp * (F.cam_split ? F.ncam : 1);  // bucket owners
     // fused shadow walks (rtx_fused.h): every light a point or directional
     // light, no overlapping media, no adaptive termination (RTX_FUSE=0: the
     // sequential machine)
@@ -2808,7 +2994,7 @@ rtx_status rtx_render(void* scene, const RtxRenderParams* params, uint8_t* rgb8,
     F.fbuf = nullptr;
     F.fmask = nullptr;
     if (fork_ok) {
-      const size_t nsamp_out = size_t(npix) * F.spp;
+      const size_t nsamp_out = size_t(nout) * F.spp;
       if ((rc = ensure(reinterpret_cast<void**>(&st->d_fbuf), &st->fbuf_bytes,
                        nunit_out * F.fork_npos * 3 * sizeof(double))) != RTX_OK)
         return rc;
@@ -2818,7 +3004,7 @@ rtx_status rtx_render(void* scene, const RtxRenderParams* params, uint8_t* rgb8,
       F.fbuf = st->d_fbuf;
       F.fmask = st->d_fmask;
       // fmask[sample] is cleared when the sample is claimed (claim_sample)
-      if (hits) HIP_TRY(hipMemsetAsync(d_hits, 0xff, nsamp_out * sizeof(RtxHitRecord), stream));
+      if (hits && level0) HIP_TRY(hipMemsetAsync(d_hits, 0xff, nsamp_out * sizeof(RtxHitRecord), stream));
     }
     const size_t ns = static_cast<size_t>(nslot64);
     const size_t gs = static_cast<size_t>(gslots);
@@ -3185,11 +3371,90 @@ rtx_status rtx_render(void* scene, const RtxRenderParams* params, uint8_t* rgb8,
     for (int g = 1; g < G; ++g) HIP_TRY(hipStreamWaitEvent(stream, st->wf_join[size_t(g)], 0));
     HIP_TRY(hipEventRecord(e1, stream));
     frame_events.push_back({e0, e1});
-  }
-  if (!adaptive) {
+    return RTX_OK;
+  };
+  if (!megakernel && !adaptive) {
+    if ((rc = run_wavefront(F, npix, true)) != RTX_OK) return rc;
     const int64_t rblocks = (npix + WG - 1) / WG;
     hipLaunchKernelGGL(reduce_kernel, dim3(rblocks), dim3(WG), 0, stream, st->d_frame, sb, d_rgb8, d_rgbf, npix);
     HIP_TRY(hipGetLastError());
+  } else if (!megakernel) {
+    // adaptive AA, level by level (adapt_*_kernel): level 0's regions are the
+    // output slots' pixels; a deeper level runs in chunks of at most npix
+    // regions (the sample buffer and buckets are sized for npix * spp)
+    F.adapt = 1;
+    F.aregs = nullptr;
+    if ((rc = run_wavefront(F, npix, true)) != RTX_OK) return rc;
+    struct LevelBufs {
+      void* p = nullptr;
+      ~LevelBufs() {
+        if (p) (void)hipFree(p);
+      }
+    };
+    std::vector<std::unique_ptr<LevelBufs>> held_levels;
+    auto level_alloc = [&](int64_t n, bool regs, ALevel& lv) -> rtx_status {
+      auto al = [](size_t x) { return (x + 255) & ~size_t(255); };
+      const size_t bv = al(size_t(n) * sizeof(dvec3)), bi = al(size_t(n) * sizeof(int));
+      const size_t br = regs ? al(size_t(n) * sizeof(ARegion)) : 0;
+      held_levels.emplace_back(new LevelBufs());
+      HIP_TRY(hipMalloc(&held_levels.back()->p, bv + 2 * bi + br + 256));
+      char* b = static_cast<char*>(held_levels.back()->p);
+      lv.val = reinterpret_cast<dvec3*>(b);
+      lv.first = reinterpret_cast<int*>(b + bv);
+      lv.mask = reinterpret_cast<int*>(b + bv + bi);
+      lv.reg = regs ? reinterpret_cast<const ARegion*>(b + bv + 2 * bi) : nullptr;
+      lv.n = n;
+      return RTX_OK;
+    };
+    std::vector<ALevel> levels(1);
+    if ((rc = level_alloc(npix, false, levels[0])) != RTX_OK) return rc;
+    if (!st->d_acnt) HIP_TRY(hipMalloc(&st->d_acnt, 2 * sizeof(unsigned int)));
+    unsigned int hcnt[2] = {0u, 0u};
+    HIP_TRY(hipMemsetAsync(st->d_acnt, 0, 2 * sizeof(unsigned int), stream));
+    hipLaunchKernelGGL(adapt_stats_kernel, dim3((npix + WG - 1) / WG), dim3(WG), 0, stream, st->d_frame, sb,
+                       levels[0], int64_t(0), int64_t(npix), st->d_acnt);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipMemcpyAsync(hcnt, st->d_acnt, sizeof(hcnt), hipMemcpyDeviceToHost, stream));
+    HIP_TRY(hipStreamSynchronize(stream));
+    // (the recursion ends once a region is under eps: ~14 levels at most)
+    while (hcnt[0] > 0 && levels.size() < 64) {
+      const int64_t n = hcnt[0];
+      ALevel nx;
+      if ((rc = level_alloc(n, true, nx)) != RTX_OK) return rc;
+      HIP_TRY(hipMemsetAsync(st->d_acnt, 0, 2 * sizeof(unsigned int), stream));
+      const ALevel& up = levels.back();
+      hipLaunchKernelGGL(adapt_emit_kernel, dim3((up.n + WG - 1) / WG), dim3(WG), 0, stream, st->d_frame, up,
+                         const_cast<ARegion*>(nx.reg), st->d_acnt + 1);
+      HIP_TRY(hipGetLastError());
+      levels.push_back(nx);
+      for (int64_t c0 = 0; c0 < n; c0 += npix) {
+        const int64_t nc = std::min<int64_t>(npix, n - c0);
+        FrameParams FL = F;
+        FL.aregs = nx.reg + c0;
+        FL.n_items = nc;
+        FL.n_samples = nc * FL.spp * (FL.cam_split ? FL.ncam : 1);
+        if ((rc = run_wavefront(FL, nc, false)) != RTX_OK) return rc;
+        hipLaunchKernelGGL(adapt_stats_kernel, dim3((nc + WG - 1) / WG), dim3(WG), 0, stream, st->d_frame, sb, nx, c0,
+                           nc, st->d_acnt);
+        HIP_TRY(hipGetLastError());
+        // (run_wavefront copies FL to the device before its first launch;
+        // FL must outlive that copy)
+        HIP_TRY(hipStreamSynchronize(stream));
+      }
+      HIP_TRY(hipMemcpyAsync(hcnt, st->d_acnt, sizeof(hcnt), hipMemcpyDeviceToHost, stream));
+      HIP_TRY(hipStreamSynchronize(stream));
+    }
+    if (hcnt[0] > 0) {
+      g_err = "rtx_render: adaptive AA recursion deeper than 64 levels";
+      return RTX_ERR_CAPACITY;
+    }
+    for (size_t L = levels.size(); L-- > 0;) {
+      ALevel below = L + 1 < levels.size() ? levels[L + 1] : ALevel{nullptr, nullptr, nullptr, nullptr, 0};
+      hipLaunchKernelGGL(adapt_combine_kernel, dim3((levels[L].n + WG - 1) / WG), dim3(WG), 0, stream, st->d_frame,
+                         levels[L], below, d_rgb8, d_rgbf);
+      HIP_TRY(hipGetLastError());
+    }
+    HIP_TRY(hipStreamSynchronize(stream));  // the level buffers are freed on return
   }
   for (auto& pr : frame_events) {
     st->ev_start.push_back(pr.first);

@@ -50,4 +50,10 @@ CASES = [
     # unbounded): 2.3 M secondary rays in a 16 x 16 frame
     ("spheres_deep_r20", "spheres_overlap.ray", "-w 16 -r 20"),
     ("circ_deep_r40", "circ_light.ray", "-w 16 -r 40"),
+    # adaptive AA on the wavefront path (adapt_*_kernel): subdivision levels
+    # on a trimesh frame with fused walks and ray-tree buckets, with the DoF
+    # camera-ray split, and with -O g (adaptaa calls trace(): no anaglyph eye)
+    ("trimesh2_adaptive", "trimesh2.ray", "-w 32 -r 5 -O a -A 4 -B 0.03"),
+    ("adaptive_dof", "trimesh2.ray", "-w 24 -r 3 -O a -A 2 -B 0.05 -O d -A 2.5 -B 4 -C 0.05"),
+    ("adaptive_anaglyph", "spheres_overlap.ray", "-w 24 -r 3 -O g -O a -A 2 -B 0.05"),
 ]

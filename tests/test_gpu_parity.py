@@ -101,6 +101,11 @@ SHARD_CASES = [
     # and forks on every shard
     ("headline_aa4_x8", "trimesh2.ray", "-w 64 -r 5 -O r -A 4", 16, 8),
     ("hitchcock_aa2_x3", "hitchcock.ray", "-w 100 -r 2 -O r -A 2", 32, 3),
+    # adaptive AA (C5 is an 8-GPU adaptive config): the default threshold
+    # (one level) on a trimesh frame across 8 ranks, and subdivision levels
+    # across 4
+    ("trimesh2_adaptive_x8", "trimesh2.ray", "-w 64 -r 5 -O a -A 4", 16, 8),
+    ("hitchcock_adaptive_x4", "hitchcock.ray", "-w 48 -r 2 -O a -A 3 -B 0.02", 16, 4),
 ]
 
 

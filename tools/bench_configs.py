@@ -58,7 +58,8 @@ def main():
                 "mrays_per_s": round(st["rays"] / wall / 1e6, 2),
                 "work": {k: st[k] for k in ("camera_rays", "secondary_rays", "shadow_rays", "node_visits",
                                             "object_tests", "tri_tests")},
-                "path": "megakernel (adaptive AA)" if opts.aa_mode == pkg.RTX_AA_ADAPTIVE else "wavefront"}
+                "path": ("megakernel" if os.environ.get("RTX_MEGAKERNEL", "0") not in ("", "0") else
+                         "wavefront (adaptive levels)" if opts.aa_mode == pkg.RTX_AA_ADAPTIVE else "wavefront")}
         print(json.dumps(line), flush=True)
         dev.close()
         host.close()
