@@ -32,6 +32,18 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 # record, triangle record, material record per shade
 # (a BVH box test reads one 32-B entry of a 128-B 4-wide float record)
 B_RAY, B_NODE, B_OBJ, B_TRI, B_SHADE = 48 + 72, 32, 224, 96, 176
+# VALU issue ceiling (MI355X_MICROARCH.md: 256 CUs x 4 SIMDs at 2.4 GHz; a
+# wave64 VALU instruction issues over 2 cycles on a SIMD-32, an FP64 one at
+# half the FP32 rate, i.e. 4 cycles): wave-instructions per second
+N_CU, SIMD_PER_CU, CLOCK_HZ = 256, 4, 2.4e9
+VALU_PEAK_F64 = N_CU * SIMD_PER_CU * CLOCK_HZ / 4   # every instruction priced as FP64
+VALU_PEAK_ISSUE = N_CU * SIMD_PER_CU * CLOCK_HZ / 2  # every instruction at the 2-cycle issue rate
+
+
+def kernel_bytes(w):
+    """algorithmic bytes of one kernel class's work (rtx_last_work)"""
+    return (B_RAY * w["queries"] + B_NODE * w["node_visits"] + B_OBJ * w["object_tests"] +
+            B_TRI * w["tri_tests"] + B_SHADE * w["shades"])
 LIB = os.path.join(ROOT, "cs378hgraphics-raytracer_amd", "lib", "librtx_hip.so")
 
 
@@ -296,7 +308,7 @@ def main():
         achieved = algo_bytes / (avg_kernel_ms * 1e-3) / 1e9
         # PMC-measured HBM bytes of one frame (tools/profile_traffic.sh): only
         # from a pass over this very library build, flags and GPU count
-        traffic, traffic_src = None, None
+        traffic, traffic_src, totals = None, None, {}
         lib_hash = file_sha256(LIB)
         if os.path.exists(args.traffic):
             try:
@@ -305,10 +317,25 @@ def main():
                 if (tr.get("flags") == args.flags and tr.get("n_gpus", 1) == world and
                         tr.get("lib_sha256") == lib_hash):
                     traffic = tr.get("hbm_bytes_per_launch")
+                    totals = tr.get("totals", {})
                     traffic_src = {"file": os.path.relpath(args.traffic, ROOT), "tag": tr.get("tag"),
                                    "build_id": tr.get("build_id")}
             except (OSError, ValueError):
                 traffic = None
+        # VALU issue ceiling (SURVEY 8(d)'s FP64-VALU secondary bound), from
+        # the same stamped PMC passes: VALU wave-instructions of one frame /
+        # the frame's GPU time / the issue peak
+        valu = totals.get("SQ_INSTS_VALU")
+        frac_valu = round(valu / (avg_kernel_ms * 1e-3) / VALU_PEAK_F64, 4) if valu else None
+        frac_valu_issue = round(valu / (avg_kernel_ms * 1e-3) / VALU_PEAK_ISSUE, 4) if valu else None
+        f64 = sum(totals.get(k, 0.0) for k in ("SQ_INSTS_VALU_ADD_F64", "SQ_INSTS_VALU_MUL_F64",
+                                                 "SQ_INSTS_VALU_FMA_F64", "SQ_INSTS_VALU_TRANS_F64"))
+        frac_hbm = round(traffic / (avg_kernel_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4) if traffic else None
+        # the ceiling the frame is closer to, by the measured fractions
+        bound = "valu" if frac_valu and (frac_hbm is None or frac_valu > frac_hbm) else "hbm"
+        kernels = st.get("kernels") or {}
+        for w in kernels.values():
+            w["algorithmic_bytes"] = kernel_bytes(w)
         cpu, parity = None, None
         if not args.no_cpu and world == 1:
             cpu = cpu_baseline(pkg, args.scene, opts, height, args.cpu_budget)
@@ -323,11 +350,15 @@ def main():
             "config": {"workload": f"trimesh2 {opts.width}x{height} {args.flags}", "scene": os.path.basename(args.scene),
                        "triangles": host.info.n_faces, "rays_per_frame": frame_rays, "tile": tile or None,
                        "parallelism": f"tile-shard x{world} + RCCL gather" if world > 1 else "single GPU"},
-            "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "roofline": {"bound": bound, "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                          # measured: PMC HBM bytes of a frame / the frame's GPU time / peak
-                         "frac_hbm": (round(traffic / (avg_kernel_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
-                                      if traffic else None),
+                         "frac_hbm": frac_hbm,
+                         # measured: VALU wave-instructions of a frame / GPU time / issue peak,
+                         # priced as FP64 (4 cycles) and at the 2-cycle issue rate
+                         "frac_valu": frac_valu, "frac_valu_issue": frac_valu_issue,
+                         "valu_insts": valu, "valu_f64_insts": f64 or None,
+                         "valu_peak_per_s": {"f64": VALU_PEAK_F64, "issue": VALU_PEAK_ISSUE},
                          "traffic_source": traffic_src,
                          "kernel": ("render_kernel<false,false> (megakernel, 1 launch per frame)" if mega else
                                     "frame span: advance_kernel + trace_kernel<false,1|2> iterations on 3 streams"),
@@ -337,8 +368,13 @@ def main():
             # the timed frame against the CPU restatement (tests/parity.py bar)
             "parity": parity,
             # traversal work of one frame (the counting pass of the same kernels)
-            "work": {k: st[k] for k in ("rays", "camera_rays", "secondary_rays", "shadow_rays", "shadow_traced",
-                                        "node_visits", "object_tests", "tri_tests", "shades")},
+            "work": dict({k: st[k] for k in ("rays", "camera_rays", "secondary_rays", "shadow_rays",
+                                             "shadow_traced", "node_visits", "object_tests", "tri_tests",
+                                             "shades")},
+                         # per kernel class (rtx_last_work): closest-hit, next-hit (walk) and tail
+                         # launches, with their algorithmic bytes (tools/kernel_roofline.py
+                         # divides them by the rocprof kernel times)
+                         kernels=kernels),
             # rays counted as the reference traces them vs rays the GPU traced
             # (dark-light shadow rays are counted, not traced: DESIGN.md §2)
             "rays_traced_per_frame": traced_rays,

@@ -154,13 +154,14 @@ def hip_lib():
                                    C.c_int, C.c_void_p, C.POINTER(RtxStats)]
         lib.rtx_shard_pixels.argtypes = [C.POINTER(RtxRenderParams), C.POINTER(C.c_int64)]
         lib.rtx_kernel_time.argtypes = [C.c_void_p, C.POINTER(C.c_double), C.POINTER(C.c_int)]
+        lib.rtx_last_work.argtypes = [C.c_void_p, C.POINTER(C.c_int64), C.c_int]
         _hip = lib
     return _hip
 
 
 # symbols include/*.h declare (checked by the CPU test suite)
 HIP_SYMBOLS = ["rtx_last_error", "rtx_device_count", "rtx_scene_create", "rtx_scene_destroy", "rtx_render",
-               "rtx_shard_pixels", "rtx_kernel_time"]
+               "rtx_shard_pixels", "rtx_kernel_time", "rtx_last_work"]
 HOST_SYMBOLS = ["rtx_host_last_error", "rtx_host_load", "rtx_host_desc", "rtx_host_info", "rtx_host_free",
                 "rtx_host_cubemap", "rtx_write_image", "rtx_image_height", "rtx_read_image", "rtx_shard_tiles",
                 "rtx_unpack_tiles", "rtx_host_tokens"]
@@ -351,6 +352,8 @@ class DeviceScene:
             out["rgb"] = rgbf.reshape(h, opts.width, 3) if rgbf is not None else None
             out["hits"] = hits.reshape(h, opts.width, opts.spp) if hits is not None else None
         out["stats"] = st.as_dict() if stats else None
+        if stats:
+            out["stats"]["kernels"] = self.last_work()
         return out
 
     def render_device(self, opts: RenderOptions, rgb8_ptr: int, rgbf_ptr: int = 0, stream: int = 0,
@@ -364,6 +367,21 @@ class DeviceScene:
                             C.c_void_p(rgbf_ptr) if rgbf_ptr else None, None, 1,
                             C.c_void_p(stream) if stream else None, None)
         _check(rc, lib, "rtx_render")
+
+    # rtx_last_work's kernel classes (include/rtx.h)
+    WORK_CLASSES = ("closest", "next", "tail")
+    WORK_FIELDS = ("queries", "node_visits", "object_tests", "tri_tests", "shades")
+
+    def last_work(self):
+        """Per-kernel-class work of the last render with stats=True:
+        {class: {queries, node_visits, object_tests, tri_tests}}."""
+        lib = hip_lib()
+        n = len(self.WORK_CLASSES) * len(self.WORK_FIELDS)
+        buf = (C.c_int64 * n)()
+        _check(lib.rtx_last_work(self._s, buf, n), lib, "rtx_last_work")
+        nf = len(self.WORK_FIELDS)
+        return {c: {f: int(buf[i * nf + j]) for j, f in enumerate(self.WORK_FIELDS)}
+                for i, c in enumerate(self.WORK_CLASSES)}
 
     def kernel_time(self):
         lib = hip_lib()

@@ -105,6 +105,7 @@ struct DevScene {
 
 struct Counters {
   int64_t camera, secondary, shadow, nodes, objects, tris, shades, shadow_traced;
+  int64_t queries;  // traversal queries started (trav_init): per-kernel work (rtx_last_work)
 };
 
 __host__ __device__ __forceinline__ dvec3 ld3(const double* p) { return mk3(p[0], p[1], p[2]); }
@@ -240,15 +241,18 @@ RT_HD float f_down(double x) {
 //   2^-24 + 3.1 2^-24 |t|.  err = 2^-22 max_q |o_q / d_q| and the relative
 //   2^-21 |t| applied to the result cover that with room (and the 2^-52
 //   relative error of the double slab the exact test computes).
-// An axis with d == 0 (or 1/d past the float range) is an inside test
-// instead: inv = +inf, the entry side's origin rounded up past o and the
-// exit side's down (olo > o > ohi strictly), so its slab is (-inf, +inf)
-// when lo <= o <= hi and empty otherwise.  That is NOT bbox.cc's rule (it
-// skips the axis) but the conservative one for the device's own trees: their
-// boxes only steer the walk and must contain every hit point, and a hit of
-// such a ray has P.x == o.x exactly (DESIGN.md "Float record tests").
-// Skipping the axis made every such ray — the image column whose direction
-// has x == 0 — visit thousands of records.
+// An axis with d == 0 is an inside test instead: inv = +inf, the entry
+// side's origin rounded up past o and the exit side's down (olo > o > ohi
+// strictly), so its slab is (-inf, +inf) when lo <= o <= hi and empty
+// otherwise.  That is NOT bbox.cc's rule (it skips the axis) but the
+// conservative one for the device's own trees: their boxes only steer the
+// walk and must contain every hit point, and a hit of such a ray has
+// P.x == o.x exactly (DESIGN.md "Float record tests").  Skipping the axis
+// made every such ray — the image column whose direction has x == 0 — visit
+// thousands of records.  A nonzero d whose 1/d is past the float range
+// (|d| < 3.4e-39) is skipped (olo = +inf, ohi = -inf: the slab is
+// (-inf, +inf)): its hit points drift off o.x by t |d|, which an inside test
+// would not cover at large t.
 struct RayF {
   float olo[3], ohi[3], inv[3];
   float err;
@@ -261,10 +265,16 @@ RT_HD RayF ray_f(const dvec3& o, const dvec3& d, const RayInv& ri) {
   for (int a = 0; a < 3; ++a) {
     const double da = rtm::get(d, a), oa = rtm::get(o, a);
     const double inv = rtm::get(ri.inv, a);  // 1 / da (ray_inv), 0 for da == 0
-    if (da == 0.0 || !(fabs(inv) < 3.0e38)) {
+    if (da == 0.0) {
       const double dl = fabs(oa) * 0x1p-23 + 1e-30;
       r.olo[a] = f_up(oa + dl);
       r.ohi[a] = f_down(oa - dl);
+      r.inv[a] = __builtin_inff();
+      continue;
+    }
+    if (!(fabs(inv) < 3.0e38)) {  // tiny nonzero d: no slab on this axis
+      r.olo[a] = __builtin_inff();
+      r.ohi[a] = -__builtin_inff();
       r.inv[a] = __builtin_inff();
       continue;
     }

@@ -709,5 +709,6 @@ __global__ void __launch_bounds__(WG) tail_fused_kernel(DevScene S, const DevSce
   }
   if (STATS) {
     stats_add(C, stats, lane);
+    stats_add_class(C, stats, lane, 30);
   }
 }

@@ -1166,6 +1166,19 @@ __device__ __forceinline__ void stats_add(const Counters& C, unsigned long long*
     if (lane == 0 && x) atomicAdd(&stats[k < 7 ? k : 18], static_cast<unsigned long long>(x));
   }
 }
+// per-kernel work (rtx_last_work): queries, node visits, object and triangle
+// tests, shades of one kernel class at stats[base .. base + 4] (20 batched
+// closest-hit launches, 25 batched next-hit / walk launches, 30 tail launches)
+#define RTX_STATS_N 35
+__device__ __forceinline__ void stats_add_class(const Counters& C, unsigned long long* stats, int lane, int base) {
+  const int64_t v[5] = {C.queries, C.nodes, C.objects, C.tris, C.shades};
+#pragma unroll
+  for (int k = 0; k < 5; ++k) {
+    int64_t x = v[k];
+    for (int off = 32; off > 0; off >>= 1) x += __shfl_down(x, off);
+    if (lane == 0 && x) atomicAdd(&stats[base + k], static_cast<unsigned long long>(x));
+  }
+}
 
 template <bool STATS, bool ADAPTIVE, bool MEDIA>
 __global__ void __launch_bounds__(WG) render_kernel(DevScene S, const DevScene* __restrict__ Sg, const FrameParams* __restrict__ Fp,
@@ -1782,6 +1795,7 @@ __global__ void __launch_bounds__(WG) tail_kernel(DevScene S, const DevScene* __
   }
   if (STATS) {
     stats_add(C, stats, lane);
+    stats_add_class(C, stats, lane, 30);
   }
 }
 
@@ -2069,6 +2083,7 @@ __global__ void __launch_bounds__(WG, !FUSED ? RTX_TRACE_WAVES : (MODE == Q_CLOS
   }
   if (STATS) {
     stats_add(C, stats, lane);  // traversal counts (and the shading's, FUSED Q_CLOSEST)
+    stats_add_class(C, stats, lane, MODE == Q_CLOSEST ? 20 : 25);
     if (lane == 0) {
       atomicAdd(&stats[8 + 2 * (MODE - 1)], static_cast<unsigned long long>(wsteps));
       atomicAdd(&stats[9 + 2 * (MODE - 1)], static_cast<unsigned long long>(lsteps));
@@ -2375,6 +2390,7 @@ struct SceneState {
   unsigned int* h_counters = nullptr;  // pinned
   DevScene* d_scene = nullptr;         // device copy of S_launch (shadow early-out)
   unsigned int* d_acnt = nullptr;      // adaptive AA: regions to subdivide, emit cursor
+  int64_t last_work[RTX_STATS_N] = {};  // raw counters of the last counting render (rtx_last_work)
   std::vector<hipEvent_t> ev_pool;
   size_t ev_used = 0;
   std::vector<hipEvent_t> ev_start, ev_stop;
@@ -2581,7 +2597,7 @@ rtx_status rtx_scene_create(int device, const RtxSceneDesc* d, void** out) {
   st->lights.assign(d->lights, d->lights + d->n_lights);
   if (hipMalloc(&st->d_frame, sizeof(FrameParams)) != hipSuccess ||
       hipMalloc(&st->d_work, sizeof(unsigned long long)) != hipSuccess ||
-      hipMalloc(&st->d_stats, 20 * sizeof(unsigned long long)) != hipSuccess) {
+      hipMalloc(&st->d_stats, RTX_STATS_N * sizeof(unsigned long long)) != hipSuccess) {
     g_err = "rtx_scene_create: hipMalloc failed";
     rtx_scene_destroy(st);
     return RTX_ERR_HIP;
@@ -2827,7 +2843,7 @@ rtx_status rtx_render(void* scene, const RtxRenderParams* params, uint8_t* rgb8,
   // through this pointer (a kernel-argument copy has no address)
   if (!st->d_scene) HIP_TRY(hipMalloc(&st->d_scene, sizeof(DevScene)));
   HIP_TRY(hipMemcpyAsync(st->d_scene, &st->S_launch, sizeof(DevScene), hipMemcpyHostToDevice, stream));
-  if (stats) HIP_TRY(hipMemsetAsync(st->d_stats, 0, 20 * sizeof(unsigned long long), stream));
+  if (stats) HIP_TRY(hipMemsetAsync(st->d_stats, 0, RTX_STATS_N * sizeof(unsigned long long), stream));
   const int pend_cap = (params->depth > 0 ? params->depth : 0) + 2;
   auto get_event = [&](hipEvent_t* e) -> rtx_status {
     if (!st->ev_pool.empty()) {
@@ -3348,8 +3364,9 @@ rtx_status rtx_render(void* scene, const RtxRenderParams* params, uint8_t* rgb8,
                 fork ? std::max<int64_t>(0, (gslots - gsamp) - static_cast<int64_t>(hc[CNT_FORK])) : 0;
             grid_bound[size_t(g)] = std::min<int64_t>(gslots, alive + forks_left);
             if (dbg)
-              fprintf(stderr, "rtx group %d iter %d: alive %u (closest %u next %u)\n", g, pending_check[size_t(g)],
-                      alive, hc[CNT_Q], hc[CNT_Q + CNT_LINE]);
+              // (the query counts of that iteration are already cleared by the
+              // next one's last workgroup: RTX_DEBUG=2 prints them per launch)
+              fprintf(stderr, "rtx group %d iter %d: alive %u\n", g, pending_check[size_t(g)], alive);
             if (alive == 0) {
               done[size_t(g)] = 1;
               ++ndone;
@@ -3467,7 +3484,7 @@ rtx_status rtx_render(void* scene, const RtxRenderParams* params, uint8_t* rgb8,
     HIP_TRY(hipStreamSynchronize(stream));
   }
   if (stats) {
-    unsigned long long c[20];
+    unsigned long long c[RTX_STATS_N];
     HIP_TRY(hipMemcpyAsync(c, st->d_stats, sizeof(c), hipMemcpyDeviceToHost, stream));
     HIP_TRY(hipStreamSynchronize(stream));
     {
@@ -3498,7 +3515,16 @@ rtx_status rtx_render(void* scene, const RtxRenderParams* params, uint8_t* rgb8,
       tot += ms;
     }
     stats->kernel_ms = tot;
+    for (int k = 0; k < RTX_STATS_N; ++k) st->last_work[k] = static_cast<int64_t>(c[k]);
   }
+  return RTX_OK;
+}
+
+rtx_status rtx_last_work(void* scene, int64_t* out, int n) {
+  if (!scene || !out || n < 0) return RTX_ERR_INVALID;
+  const SceneState* st = static_cast<const SceneState*>(scene);
+  const int m = n < RTX_WORK_COUNT ? n : RTX_WORK_COUNT;
+  for (int k = 0; k < m; ++k) out[k] = st->last_work[20 + k];
   return RTX_OK;
 }
 

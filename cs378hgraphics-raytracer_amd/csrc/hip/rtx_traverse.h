@@ -183,7 +183,10 @@ RT_HD bool trav_init(Trav& T, const DevScene& S, const dvec3& P, const dvec3& D,
   T.tlo = QMODE == Q_CLOSEST ? -RTX_INF : tp - S.margin;  // Q_ANY: tp = -inf for a closest query
   T.ri = ray_inv(D);
   T.rf = ray_f(P, D, T.ri);
-  if (STATS) C.nodes++;
+  if (STATS) {
+    C.nodes++;
+    C.queries++;
+  }
   double a, b;
   if (!box_test(S.sroot.lo, S.sroot.hi, P, D, T.ri, a, b) || a > T.bt + S.margin || b < T.tlo) return false;
   T.sp = 0;

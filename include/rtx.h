@@ -251,6 +251,19 @@ rtx_status rtx_render(void* scene, const RtxRenderParams* params,
 /* Number of pixels this shard owns (size of packed outputs). */
 rtx_status rtx_shard_pixels(const RtxRenderParams* params, int64_t* npixels);
 
+/* Per-kernel work of the last render called with `stats` (the counting
+ * variant of the kernels), RTX_WORK_COUNT int64 values, five per kernel
+ * class — queries, BVH node visits, object tests, triangle tests, shades:
+ *   [0..4]   batched closest-hit launches (trace_kernel<Q_CLOSEST>: camera,
+ *            reflection and refraction rays; fused frames shade there too)
+ *   [5..9]   batched next-hit launches (trace_kernel<Q_NEXT>: shadow walks)
+ *   [10..14] tail launches (tail_kernel / tail_fused_kernel: both kinds)
+ * A query is one traversal (a shadow walk is one query per hit it steps
+ * through).  The megakernel path (RTX_MEGAKERNEL=1) leaves them 0.
+ * `n` values are written (at most RTX_WORK_COUNT). */
+#define RTX_WORK_COUNT 15
+rtx_status rtx_last_work(void* scene, int64_t* out, int n);
+
 /* Device time (ms) of render kernels launched since the last call, read
  * from hipEvents recorded on the render stream; synchronizes those events. */
 rtx_status rtx_kernel_time(void* scene, double* total_ms, int* launches);

@@ -99,3 +99,34 @@ def test_float_record_test_is_conservative(pkg):
     culled = sum(1 for k in range(n) if not exact_hit(P[k], D[k], far[k, :3], far[k, 3:]) and ok2[k] == 0)
     missed = sum(1 for k in range(n) if not exact_hit(P[k], D[k], far[k, :3], far[k, 3:]))
     assert missed > 0 and culled >= 0.9 * missed
+
+
+def test_tiny_direction_components(pkg):
+    """A nonzero direction component too small for a float reciprocal
+    (|d| < 3.4e-39): the hit points drift off the origin's coordinate by
+    t |d|, so that axis must not be an inside test.  Boxes that
+    hold a far point of such a ray, but not the origin's coordinate on that
+    axis, must pass."""
+    L = _harness(pkg)
+    L.rec_test_host.argtypes = [C.c_int32] + [C.c_void_p] * 5
+    P, D, B = [], [], []
+    for tiny in (1e-40, -2e-39, 3e-39, 5e-45, -1e-42):
+        for ax in range(3):
+            for t in (1e9, 1e12, 1e15):
+                o = np.zeros(3)
+                d = np.ones(3)
+                d[ax] = tiny
+                d[(ax + 1) % 3] = 0.0  # one zero axis too (an inside test that does hold)
+                x = o + t * d
+                lo, hi = x - abs(x) * 1e-3 - 1e-300, x + abs(x) * 1e-3 + 1e-300
+                P.append(o)
+                D.append(d)
+                B.append(np.concatenate([lo, hi]))
+    P, D, B = np.array(P), np.array(D), np.array(B)
+    n = len(P)
+    ok = np.zeros(n, np.int32)
+    a = np.zeros(n, np.float32)
+    assert L.rec_test_host(n, P.ctypes.data, D.ctypes.data, B.ctypes.data, ok.ctypes.data, a.ctypes.data) == 0
+    for k in range(n):
+        assert exact_hit(P[k], D[k], B[k, :3], B[k, 3:]), k
+        assert ok[k] == 1, f"case {k}: exact hit rejected (d={D[k]!r}, box={B[k]!r})"

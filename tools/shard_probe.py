@@ -3,9 +3,11 @@
 GPU: rank r of N renders tiles t % N == r (what bench.py --gpus N runs on
 each GPU).  The slowest shard's time bounds the N-GPU frame (plus the RCCL
 gather of a few MB).  Prints one JSON line per N.
-usage (GPU box): python tools/shard_probe.py [--flags "-w 1920 ..."] [N ...]"""
+usage (GPU box): python tools/shard_probe.py [--scene NAME.ray] [--flags "-w 1920 ..."] [N ...]
+(dragon.ray, C5's scene, is generated when missing: tools/gen_scenes.py --dragon)"""
 import json
 import os
+import subprocess
 import sys
 import time
 
@@ -20,11 +22,19 @@ def main():
     pkg = bench.load_package()
     args = sys.argv[1:]
     flags = "-w 1920 -r 5 -O r -A 4"
-    if args and args[0] == "--flags":
-        flags, args = args[1], args[2:]
+    scene = "trimesh2.ray"
+    while args and args[0] in ("--flags", "--scene"):
+        if args[0] == "--flags":
+            flags = args[1]
+        else:
+            scene = args[1]
+        args = args[2:]
+    if scene == "dragon.ray" and not os.path.exists(os.path.join(ROOT, "scenes", scene)):
+        subprocess.run([sys.executable, os.path.join(ROOT, "tools", "gen_scenes.py"), "--dragon"], check=True,
+                       stdout=subprocess.DEVNULL)
     ns = [int(a) for a in args] or [1, 2, 4, 8]
     opts = pkg.RenderOptions.from_cli(flags.split())
-    host = pkg.HostScene(os.path.join(ROOT, "scenes", "trimesh2.ray"))
+    host = pkg.HostScene(os.path.join(ROOT, "scenes", scene))
     dev = pkg.DeviceScene(host, 0)
     h = host.height_for(opts.width)
     stream = torch.cuda.current_stream().cuda_stream
@@ -42,7 +52,7 @@ def main():
             torch.cuda.synchronize()
             times.append((time.perf_counter() - t0) / 3 * 1e3)
         full = 1e3 if n == 1 else None
-        print(json.dumps({"flags": flags, "n": n, "shard_ms": [round(t, 2) for t in times],
+        print(json.dumps({"scene": scene, "flags": flags, "n": n, "shard_ms": [round(t, 2) for t in times],
                           "max_ms": round(max(times), 2)}),
               flush=True)
 
