@@ -2173,13 +2173,30 @@ __device__ __forceinline__ bool slot_pixel(const FrameParams& F, int64_t o, int&
 __global__ void __launch_bounds__(WG) reduce_kernel(const FrameParams* __restrict__ Fp, const double* __restrict__ sbuf,
                                                      uint8_t* __restrict__ rgb8, double* __restrict__ rgbf,
                                                      int64_t npix_slots) {
+  // one thread per sample, WG / spp pixels per workgroup: lane k reads sample
+  // k's sums (neighbouring lanes neighbouring samples, coalesced), the
+  // values meet in LDS and the pixel's first lane adds them in sample order
+  // (with one thread per pixel, each load instruction touched 64 lines
+  // spp * 24 B apart)
+  __shared__ double sv[WG * 3];
   const FrameParams& F = *Fp;
-  const int64_t o = static_cast<int64_t>(blockIdx.x) * WG + threadIdx.x;
-  if (o >= npix_slots) return;
+  const int spp = F.spp;
+  const int ppb = WG / spp;  // (spp <= 64: regular AA is capped at 8 x 8)
+  const int t = threadIdx.x;
+  const int pl = t / spp, q = t - pl * spp;
+  const int64_t o = static_cast<int64_t>(blockIdx.x) * ppb + pl;
   int i, j;
-  if (!slot_pixel(F, o, i, j)) return;
+  const bool own = pl < ppb && o < npix_slots && slot_pixel(F, o, i, j);
+  if (own) {
+    const dvec3 v = sample_value(F, sbuf, o * spp + q);
+    sv[t * 3 + 0] = v.x;
+    sv[t * 3 + 1] = v.y;
+    sv[t * 3 + 2] = v.z;
+  }
+  __syncthreads();
+  if (!own || q != 0) return;
   dvec3 acc = mk3(0.0, 0.0, 0.0);
-  for (int q = 0; q < F.spp; ++q) acc += sample_value(F, sbuf, o * F.spp + q);
+  for (int k = 0; k < spp; ++k) acc += mk3(sv[(t + k) * 3 + 0], sv[(t + k) * 3 + 1], sv[(t + k) * 3 + 2]);
   if (F.P.aa_mode != RTX_AA_NONE) acc = acc / double(F.s * F.s);
   if (rgb8) {
     rgb8[o * 3 + 0] = rtm::to_byte(acc.x);
@@ -3390,9 +3407,10 @@ rtx_status rtx_render(void* scene, const RtxRenderParams* params, uint8_t* rgb8,
     frame_events.push_back({e0, e1});
     return RTX_OK;
   };
-  if (!megakernel && !adaptive) {
-    if ((rc = run_wavefront(F, npix, true)) != RTX_OK) return rc;
-    const int64_t rblocks = (npix + WG - 1) / WG;
+  if (!adaptive) {
+    if (!megakernel && (rc = run_wavefront(F, npix, true)) != RTX_OK) return rc;
+    const int64_t ppb = WG / F.spp;
+    const int64_t rblocks = (npix + ppb - 1) / ppb;
     hipLaunchKernelGGL(reduce_kernel, dim3(rblocks), dim3(WG), 0, stream, st->d_frame, sb, d_rgb8, d_rgbf, npix);
     HIP_TRY(hipGetLastError());
   } else if (!megakernel) {
