@@ -6,6 +6,7 @@
 
 #include <algorithm>
 #include <climits>
+#include <cstdlib>
 #include <cmath>
 #include <cstring>
 #include <functional>
@@ -690,11 +691,17 @@ inline TBox tbox_empty() {
   return b;
 }
 
-// Binned SAH (16 bins, traversal cost 1.2 per node against 1 per item) over
-// item boxes.  Emits nodes in DFS pre-order (child0 = i + 1, right), leaves
-// [first, first + count) into `order`, a permutation of the items.
+// Binned SAH over item boxes (defaults: 16 bins, traversal cost 1.2 per node
+// against 1 per item; SahParams, A/B switches RTX_SAH_BINS / RTX_SAH_NODE /
+// RTX_SAH_ITEM / RTX_SAH_LEAF read by build_trav_trees).  Emits nodes in DFS
+// pre-order (child0 = i + 1, right), leaves [first, first + count) into
+// `order`, a permutation of the items.
+struct SahParams {
+  int bins = 16;
+  double c_node = 1.2, c_item = 1.0;
+};
 inline void tree_build(const std::vector<TBox>& box, int max_leaf, std::vector<RtxNode>& nodes,
-                       std::vector<int>& order) {
+                       std::vector<int>& order, const SahParams& sp = SahParams()) {
   const int n = static_cast<int>(box.size());
   order.resize(size_t(n));
   for (int i = 0; i < n; ++i) order[size_t(i)] = i;
@@ -703,7 +710,7 @@ inline void tree_build(const std::vector<TBox>& box, int max_leaf, std::vector<R
   std::vector<double> cen(size_t(n) * 3);
   for (int i = 0; i < n; ++i)
     for (int k = 0; k < 3; ++k) cen[size_t(i) * 3 + k] = 0.5 * (box[size_t(i)].lo[k] + box[size_t(i)].hi[k]);
-  const int NBIN = 16;
+  const int NBIN = sp.bins < 2 ? 2 : (sp.bins > 256 ? 256 : sp.bins);
   std::function<void(int, int, int)> rec = [&](int l, int r, int depth) {
     const int me = static_cast<int>(nodes.size());
     nodes.emplace_back();
@@ -739,8 +746,8 @@ inline void tree_build(const std::vector<TBox>& box, int max_leaf, std::vector<R
     for (int k = 0; k < 3; ++k) {
       const double ext = cb.hi[k] - cb.lo[k];
       if (!(ext > 0.0)) continue;
-      int bc[NBIN] = {0};
-      TBox bb[NBIN];
+      std::vector<int> bc(static_cast<size_t>(NBIN), 0);
+      std::vector<TBox> bb(static_cast<size_t>(NBIN));
       for (int q = 0; q < NBIN; ++q) bb[q] = tbox_empty();
       for (int i = l; i < r; ++i) {
         const int it = order[size_t(i)];
@@ -749,8 +756,8 @@ inline void tree_build(const std::vector<TBox>& box, int max_leaf, std::vector<R
         bc[q]++;
         tbox_grow(bb[q], box[size_t(it)]);
       }
-      double ra[NBIN];
-      int rc[NBIN];
+      std::vector<double> ra(static_cast<size_t>(NBIN));
+      std::vector<int> rc(static_cast<size_t>(NBIN));
       TBox acc = tbox_empty();
       int ac = 0;
       for (int q = NBIN - 1; q > 0; --q) {
@@ -774,8 +781,8 @@ inline void tree_build(const std::vector<TBox>& box, int max_leaf, std::vector<R
       }
     }
     const double area = tbox_area(b);
-    const double split_cost = area > 0.0 && bax >= 0 ? 1.2 + best / area : HUGE_VAL;
-    if (cnt <= max_leaf && cnt <= split_cost) {
+    const double split_cost = area > 0.0 && bax >= 0 ? sp.c_node + sp.c_item * best / area : HUGE_VAL;
+    if (cnt <= max_leaf && sp.c_item * cnt <= split_cost) {
       make_leaf();
       return;
     }
@@ -850,6 +857,14 @@ inline void hot_mesh_records(TravTrees& T, int cap) {
 
 inline bool build_trav_trees(const RtxSceneDesc* d, TravTrees& T) {
   std::memset(&T.sroot, 0, sizeof(T.sroot));
+  // mesh-tree SAH parameters (A/B switches; the walk's results do not depend
+  // on the tree, DESIGN.md "Traversal trees")
+  SahParams sp;
+  int mesh_leaf = 3;
+  if (const char* e = getenv("RTX_SAH_BINS")) sp.bins = atoi(e);
+  if (const char* e = getenv("RTX_SAH_NODE")) sp.c_node = atof(e);
+  if (const char* e = getenv("RTX_SAH_ITEM")) sp.c_item = atof(e);
+  if (const char* e = getenv("RTX_SAH_LEAF")) mesh_leaf = std::min(3, std::max(1, atoi(e)));  // (leaf codes hold <= 3)
   std::vector<RtxNode> nodes;
   std::vector<int> order;
   std::vector<TBox> boxes;
@@ -884,7 +899,7 @@ inline bool build_trav_trees(const RtxSceneDesc* d, TravTrees& T) {
         boxes[size_t(f)].hi[k] = fmax(fmax(F.v0[k], F.v1[k]), F.v2[k]);
       }
     }
-    tree_build(boxes, 3, nodes, order);
+    tree_build(boxes, mesh_leaf, nodes, order, sp);
     for (int j = 0; j < me.face_count; ++j) {
       T.tfaces[size_t(me.face_off + j)] = d->faces[me.face_off + order[size_t(j)]];
       T.trank[size_t(me.face_off + j)] = order[size_t(j)];
