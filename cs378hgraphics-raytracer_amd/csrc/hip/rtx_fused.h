@@ -402,16 +402,18 @@ __device__ __forceinline__ void cam_start(LaneRef& LR, const FrameParams& F, Rtx
 // registers add to the traversal's peak, and the backend fails on the
 // inlined STATS instantiation, "Subtarget requires even aligned vector
 // registers")
-template <bool STATS>
-__device__ __noinline__ bool cam_first_claim(LaneRef& LR, const FrameParams& F, Counters& C,
-                                             RtxHitRecord* __restrict__ hits, int slot, QRay& qr) {
+// (arguments by value: a reference would put the caller's LaneRef and
+// counters in scratch for the call)
+__device__ __noinline__ bool cam_first_claim(const LaneMem lm, int slot, const FrameParams& F,
+                                             RtxHitRecord* __restrict__ hits) {
+  LaneRef LR(lm, static_cast<size_t>(slot));
   lane_init(LR);
   claim_sample(LR, F, hits, slot);
   if (LR.st() == ST_IDLE) return false;
-  cam_start(LR, F, hits, qr.p, qr.d);
-  if (STATS) C.camera++;
-  qr.W = mk3(1.0, 1.0, 1.0);
-  qr.code = static_cast<int64_t>(pend_code(F.fork_on ? 1 : 0, F.P.depth, 0));
+  // ST_CAM's bookkeeping (the hit record's default, camk); the caller forms
+  // the ray itself (cam_first_ray)
+  dvec3 rp, rd;
+  cam_start(LR, F, hits, rp, rd);
   LR.top() = 0;     // the ray's own entry (never written: shading overwrites it with the children)
   LR.nrays()++;     // ST_POP
   LR.qmode() = Q_CLOSEST;

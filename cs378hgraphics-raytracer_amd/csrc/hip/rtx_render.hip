@@ -1925,7 +1925,12 @@ __global__ void __launch_bounds__(WG, !FUSED ? RTX_TRACE_WAVES : (MODE == Q_CLOS
     double w_bt = bt_in;
     int w_bo = bo_in, w_bs = bs_in;
     while (pend) {
-      const size_t k = kq;
+      // opaque record index: the record's field addresses are formed here
+      // from (uniform base, k) each time, instead of being hoisted out of
+      // the loop as a dozen 64-bit addresses that spill to scratch and come
+      // back as dependent scratch loads (the LaneRef::refresh idea)
+      size_t k = kq;
+      asm volatile("" : "+v"(k));
       const int li = Q.iv[1 * cap + k];
       const RtxLight& L = Sg->lights[li];
       const dvec3 pb = mk3(Q.d[QF_PX * cap + k], Q.d[QF_PY * cap + k], Q.d[QF_PZ * cap + k]);
@@ -2030,9 +2035,15 @@ __global__ void __launch_bounds__(WG, !FUSED ? RTX_TRACE_WAVES : (MODE == Q_CLOS
         } else if (MODE == Q_CLOSEST && cam) {  // claim the slot's first sample, its first camera ray
           const int slot = SA.slot_off + static_cast<int>(kq);
           LaneRef LR(lm, static_cast<size_t>(slot));
-          QRay qr;
-          noq = !cam_first_claim<STATS>(LR, *SA.Fp, C, SA.hits, slot, qr);
-          if (!noq) active = trav_init<STATS, MODE>(T, S, qr.p, qr.d, -RTX_INF, -1, -1, RTX_INF, -RTX_INF, C);
+          noq = !cam_first_claim(lm, slot, *SA.Fp, SA.hits);
+          if (!noq) {
+            if (STATS) C.camera++;
+            // the ray from the claim's (sx, sy), here rather than through an
+            // out-parameter of the out-of-line claim (a stack object: 80 B
+            // of scratch written and read per camera ray)
+            const QRay qr = cam_first_ray(LR, *SA.Fp);
+            active = trav_init<STATS, MODE>(T, S, qr.p, qr.d, -RTX_INF, -1, -1, RTX_INF, -RTX_INF, C);
+          }
         } else if (MODE == Q_CLOSEST) {  // fused closest record: the ray only
           const dvec3 P = mk3(Q.d[0 * cap + kq], Q.d[1 * cap + kq], Q.d[2 * cap + kq]);
           const dvec3 D = mk3(Q.d[3 * cap + kq], Q.d[4 * cap + kq], Q.d[5 * cap + kq]);
