@@ -141,26 +141,31 @@ __host__ __device__ __forceinline__ bool cone_good(const double* prm, const dvec
 // ------------------------------------------------------------------ slab
 // BoundingBox::intersect (bbox.cc:33-70), exact: same divisions, same
 // vd == 0 skip, same per-axis early outs.  Also returns tMin/tMax.
+// Branch-free form of bbox.cc's loop: the box is loaded whole before any
+// test (per-axis branches made each axis's loads a dependent round trip),
+// a d[a] == 0 axis is selected away instead of skipped, and the per-axis
+// early outs are decided once at the end — tMin only grows and tMax only
+// shrinks, so an early out taken at some axis holds at the end too, and the
+// comparisons are bbox.cc's own (NaN behaves the same).
 RT_HD bool slab(const double* bmin, const double* bmax, const dvec3& o, const dvec3& d,
                                      double& tMinOut, double& tMaxOut) {
+  const double lo[3] = {bmin[0], bmin[1], bmin[2]}, hi[3] = {bmax[0], bmax[1], bmax[2]};
   double tMin = -1.0e308, tMax = 1.0e308;
+  bool out = false;
 #pragma unroll
   for (int a = 0; a < 3; ++a) {
     const double vd = rtm::get(d, a);
-    if (vd == 0.0) continue;
     const double oa = rtm::get(o, a);
-    double t1 = (bmin[a] - oa) / vd;
-    double t2 = (bmax[a] - oa) / vd;
-    if (t1 > t2) {
-      double tt = t1;
-      t1 = t2;
-      t2 = tt;
-    }
-    if (t1 > tMin) tMin = t1;
-    if (t2 < tMax) tMax = t2;
-    if (tMin > tMax) return false;
-    if (tMax < RTX_RAY_EPS) return false;
+    const double u1 = (lo[a] - oa) / vd;
+    const double u2 = (hi[a] - oa) / vd;
+    const bool sw = u1 > u2;
+    const double t1 = sw ? u2 : u1, t2 = sw ? u1 : u2;
+    const bool on = !(vd == 0.0);
+    tMin = on && t1 > tMin ? t1 : tMin;
+    tMax = on && t2 < tMax ? t2 : tMax;
+    out = out || (on && (tMin > tMax || tMax < RTX_RAY_EPS));
   }
+  if (out) return false;
   tMinOut = tMin;
   tMaxOut = tMax;
   return true;
@@ -195,15 +200,17 @@ RT_HD RayInv ray_inv(const dvec3& d) {
 RT_HD bool box_test(const double* lo, const double* hi, const dvec3& o, const dvec3& d,
                                          const RayInv& ri, double& a, double& b) {
   if (!ri.fast) return slab(lo, hi, o, d, a, b);
+  // the box whole, then the axes branch-free (a d[k] == 0 axis selected away)
+  const double l[3] = {lo[0], lo[1], lo[2]}, h[3] = {hi[0], hi[1], hi[2]};
   double tmin = -1.0e308, tmax = 1.0e308;
 #pragma unroll
   for (int k = 0; k < 3; ++k) {
-    if (rtm::get(d, k) == 0.0) continue;
     const double iv = rtm::get(ri.inv, k), oa = rtm::get(o, k);
-    const double t1 = (lo[k] - oa) * iv;
-    const double t2 = (hi[k] - oa) * iv;
-    tmin = fmax(tmin, fmin(t1, t2));
-    tmax = fmin(tmax, fmax(t1, t2));
+    const double t1 = (l[k] - oa) * iv;
+    const double t2 = (h[k] - oa) * iv;
+    const bool on = !(rtm::get(d, k) == 0.0);
+    tmin = on ? fmax(tmin, fmin(t1, t2)) : tmin;
+    tmax = on ? fmin(tmax, fmax(t1, t2)) : tmax;
   }
   const double e1 = 1e-15 * fabs(tmin) + 1e-300, e2 = 1e-15 * fabs(tmax) + 1e-300;
   if (tmin - e1 > tmax + e2 || tmax + e2 < RTX_RAY_EPS) return false;  // certain miss
@@ -290,10 +297,12 @@ RT_HD RayF ray_f(const dvec3& o, const dvec3& d, const RayInv& ri) {
 // Conservative slab of a record entry in float (see RayF): never rejects a
 // box containing a hit point of the ray; a <= the entry distance, b >= the
 // exit distance.
-RT_HD bool box_cons32(const DevNode4& nd, int k, const RayF& r, float& a, float& b) {
-  const float t1x = (nd.lo[0][k] - r.olo[0]) * r.inv[0], t2x = (nd.hi[0][k] - r.ohi[0]) * r.inv[0];
-  const float t1y = (nd.lo[1][k] - r.olo[1]) * r.inv[1], t2y = (nd.hi[1][k] - r.ohi[1]) * r.inv[1];
-  const float t1z = (nd.lo[2][k] - r.olo[2]) * r.inv[2], t2z = (nd.hi[2][k] - r.ohi[2]) * r.inv[2];
+// (the entry's six bounds as values: visit4 loads the whole record first)
+RT_HD bool box_cons32v(float lox, float loy, float loz, float hix, float hiy, float hiz, const RayF& r, float& a,
+                       float& b) {
+  const float t1x = (lox - r.olo[0]) * r.inv[0], t2x = (hix - r.ohi[0]) * r.inv[0];
+  const float t1y = (loy - r.olo[1]) * r.inv[1], t2y = (hiy - r.ohi[1]) * r.inv[1];
+  const float t1z = (loz - r.olo[2]) * r.inv[2], t2z = (hiz - r.ohi[2]) * r.inv[2];
   const float tmin = fmaxf(fmaxf(fminf(t1x, t2x), fminf(t1y, t2y)), fminf(t1z, t2z));
   const float tmax = fminf(fminf(fmaxf(t1x, t2x), fmaxf(t1y, t2y)), fmaxf(t1z, t2z));
   // (err is finite; an infinite bound stays infinite, a miss stays a miss)
@@ -306,6 +315,10 @@ RT_HD bool box_cons32(const DevNode4& nd, int k, const RayF& r, float& a, float&
   // (no 1e-8 cut on the exit, as the double slab had none here; leaf_ok
   // applies the reference's)
   return !(a > b) && !(b < 0.0f);
+}
+
+RT_HD bool box_cons32(const DevNode4& nd, int k, const RayF& r, float& a, float& b) {
+  return box_cons32v(nd.lo[0][k], nd.lo[1][k], nd.lo[2][k], nd.hi[0][k], nd.hi[1][k], nd.hi[2][k], r, a, b);
 }
 
 // box_cons32 for entries 2p and 2p + 1 at once: the slab arithmetic on
@@ -467,10 +480,12 @@ __device__ dvec3 box_normal(const DevScene& S, const RtxMaterial& m, int bestInd
 // traverse); rejecting there only skips work, never changes a result.
 RT_HD bool tri_hit(const RtxFace& F, const dvec3& p, const dvec3& d, double tcap,
                                         double& tOut) {
+  // the face whole before the plane test (its vertices used to be loaded
+  // after it: a second dependent round trip per face)
   const dvec3 n = ld3(F.n);
+  const dvec3 v0 = ld3(F.v0), v1 = ld3(F.v1), v2 = ld3(F.v2);
   double t = rtm::dot(n, d);
   if (t < RTX_EPS32 && t > -RTX_EPS32) return false;
-  const dvec3 v0 = ld3(F.v0), v1 = ld3(F.v1), v2 = ld3(F.v2);
   t = rtm::dot(v0 - p, n) / t;
   if (t < RTX_EPS32 || t > tcap) return false;
   const dvec3 P = rtm::ray_at(p, d, t);

@@ -1169,7 +1169,7 @@ __device__ __forceinline__ void stats_add(const Counters& C, unsigned long long*
 // per-kernel work (rtx_last_work): queries, node visits, object and triangle
 // tests, shades of one kernel class at stats[base .. base + 4] (20 batched
 // closest-hit launches, 25 batched next-hit / walk launches, 30 tail launches)
-#define RTX_STATS_N 35
+#define RTX_STATS_N 39  // 35..38: the slowest wave of the last closest / next launch (RTX_DEBUG=2)
 __device__ __forceinline__ void stats_add_class(const Counters& C, unsigned long long* stats, int lane, int base) {
   const int64_t v[5] = {C.queries, C.nodes, C.objects, C.tris, C.shades};
 #pragma unroll
@@ -1910,6 +1910,10 @@ __global__ void __launch_bounds__(WG, !FUSED ? RTX_TRACE_WAVES : (MODE == Q_CLOS
   bool exhausted = false;
   int64_t wsteps = 0, lsteps = 0;
   int qsteps = 0;
+  // (STATS) the wave's start, its claims and walk restarts: the slowest
+  // wave of the launch is reported by RTX_DEBUG=2
+  const uint64_t wt0 = STATS ? wall_clock64() : 0;
+  unsigned int nclaims = 0, nrestart = 0;
   auto finish = [&]() {
     const size_t slot = static_cast<size_t>(Q.slot[kq]);
     lm.d[size_t(LD_bt) * lm.n + slot] = T.bt;
@@ -1974,6 +1978,7 @@ __global__ void __launch_bounds__(WG, !FUSED ? RTX_TRACE_WAVES : (MODE == Q_CLOS
         shadow_bounds(*Sg, L, pb, false, qlim, qblk);
         active = trav_init<STATS, MODE>(T, S, pb, sdir, bt, bo, bs, qlim, qblk, C);
         pend = !active;  // answered by the root test: the walk's next step
+        if (STATS) nrestart++;
         w_have = T.have;
         w_bt = T.bt;
         w_bo = T.bobj;
@@ -2015,6 +2020,7 @@ __global__ void __launch_bounds__(WG, !FUSED ? RTX_TRACE_WAVES : (MODE == Q_CLOS
         if (base >= nq) {
           exhausted = true;
         } else {
+          if (STATS) nclaims++;
           qnext = base;
           qend = base + 64u < nq ? base + 64u : nq;
         }
@@ -2098,6 +2104,12 @@ __global__ void __launch_bounds__(WG, !FUSED ? RTX_TRACE_WAVES : (MODE == Q_CLOS
     if (lane == 0) {
       atomicAdd(&stats[8 + 2 * (MODE - 1)], static_cast<unsigned long long>(wsteps));
       atomicAdd(&stats[9 + 2 * (MODE - 1)], static_cast<unsigned long long>(lsteps));
+      // the slowest wave (100 MHz wall clock ticks in the high word): its
+      // wave steps; its claims and walk restarts
+      const unsigned long long dur = static_cast<unsigned long long>(wall_clock64() - wt0) << 32;
+      atomicMax(&stats[35 + 2 * (MODE - 1)], dur | static_cast<unsigned long long>(wsteps & 0xffffffffll));
+      atomicMax(&stats[36 + 2 * (MODE - 1)],
+                dur | (static_cast<unsigned long long>(nclaims & 0xffffu) << 16) | (nrestart & 0xffffu));
     }
   }
   // clr >= 0 (the iteration's last launch): the last workgroup to finish
@@ -3205,6 +3217,14 @@ rtx_status rtx_render(void* scene, const RtxRenderParams* params, uint8_t* rgb8,
       const char* e = getenv("RTX_LEAF_K");
       if (e && atoi(e) > 0) leaf_k = std::min(65, atoi(e));
     }
+    // the same for the launches of batched iterations >= 1 (latency-bound
+    // on small frames: a wave holds one claim and waits for its slowest
+    // lane, so postponing a lane's costly units only lengthens its chain)
+    int leaf_k_late = leaf_k;
+    {
+      const char* e = getenv("RTX_LEAF_K_LATE");
+      if (e && atoi(e) > 0) leaf_k_late = std::min(65, atoi(e));
+    }
     hipEvent_t e0, e1;
     if ((rc = get_event(&e0)) != RTX_OK || (rc = get_event(&e1)) != RTX_OK) return rc;
     HIP_TRY(hipEventRecord(e0, stream));
@@ -3294,7 +3314,7 @@ rtx_status rtx_render(void* scene, const RtxRenderParams* params, uint8_t* rgb8,
                                  : tg;
         ShadeArgs sa;
         std::memset(&sa, 0, sizeof(sa));
-        sa.leaf_k = leaf_k;
+        sa.leaf_k = it == 0 ? leaf_k : leaf_k_late;
         if (fuse) {
           sa.Fp = st->d_frame;
           sa.hits = d_hits;
@@ -3314,6 +3334,7 @@ rtx_status rtx_render(void* scene, const RtxRenderParams* params, uint8_t* rgb8,
             if (dbg_level >= 2) {  // RTX_DEBUG=2: every iteration's queries and closest-hit time (synchronous)
               (void)(hipStreamSynchronize(sg));
               if (stats) (void)(hipMemset(st->d_stats + 12, 0, 4 * sizeof(unsigned long long)));
+              if (stats) (void)(hipMemset(st->d_stats + 35, 0, 4 * sizeof(unsigned long long)));
               (void)(hipEventCreate(&d0));
               (void)(hipEventCreate(&d1));
               (void)(hipEventRecord(d0, sg));
@@ -3326,18 +3347,20 @@ rtx_status rtx_render(void* scene, const RtxRenderParams* params, uint8_t* rgb8,
                                  st->d_scene, q0, cnt, A, st->stack_cap, st->d_stats, st->d_wterm, sa, -1);
             if (dbg_level >= 2) {
               unsigned int hc[CNT_PER_GROUP];
-              unsigned long long hs[4] = {0, 0, 0, 0};
+              unsigned long long hs[4] = {0, 0, 0, 0}, hw[4] = {0, 0, 0, 0};
               float ms = 0.f;
               (void)(hipEventRecord(d1, sg));
               (void)(hipStreamSynchronize(sg));
               (void)(hipEventElapsedTime(&ms, d0, d1));
               (void)(hipMemcpy(hc, cnt, sizeof(hc), hipMemcpyDeviceToHost));
               if (stats) (void)(hipMemcpy(hs, st->d_stats + 12, sizeof(hs), hipMemcpyDeviceToHost));
+              if (stats) (void)(hipMemcpy(hw, st->d_stats + 35, sizeof(hw), hipMemcpyDeviceToHost));
               fprintf(stderr,
                       "rtx group %d iter %d: closest %u walks %u forks %u | closest-hit launch %.3f ms, max steps "
-                      "%llu, queries over 100 steps %llu\n",
+                      "%llu, queries over 100 steps %llu | slowest wave %.1f us, %llu wave steps, %llu claims\n",
                       g, it, cam_it ? static_cast<unsigned>(cam_n[size_t(g)]) : hc[CNT_Q], hc[CNT_Q + CNT_LINE],
-                      hc[CNT_FORK], ms, hs[0], hs[2]);
+                      hc[CNT_FORK], ms, hs[0], hs[2], (hw[0] >> 32) * 0.01, hw[0] & 0xffffffffull,
+                      (hw[1] >> 16) & 0xffffull);
               (void)(hipEventDestroy(d0));
               (void)(hipEventDestroy(d1));
             }
@@ -3350,10 +3373,17 @@ rtx_status rtx_render(void* scene, const RtxRenderParams* params, uint8_t* rgb8,
                                cnt, A, st->stack_cap, st->d_stats, st->d_wterm, sa, clr_next);
             if (dbg_level >= 2) {
               float ms = 0.f;
+              unsigned long long hw[4] = {0, 0, 0, 0}, hs2[4] = {0, 0, 0, 0};
               (void)(hipEventRecord(d1, sg));
               (void)(hipStreamSynchronize(sg));
               (void)(hipEventElapsedTime(&ms, d0, d1));
-              fprintf(stderr, "rtx group %d iter %d: walk launch %.3f ms\n", g, it, ms);
+              if (stats) (void)(hipMemcpy(hw, st->d_stats + 35, sizeof(hw), hipMemcpyDeviceToHost));
+              if (stats) (void)(hipMemcpy(hs2, st->d_stats + 12, sizeof(hs2), hipMemcpyDeviceToHost));
+              fprintf(stderr,
+                      "rtx group %d iter %d: walk launch %.3f ms | max steps per query %llu | slowest wave %.1f us, "
+                      "%llu wave steps, %llu claims, %llu walk restarts\n",
+                      g, it, ms, hs2[1], (hw[2] >> 32) * 0.01, hw[2] & 0xffffffffull, (hw[3] >> 16) & 0xffffull,
+                      hw[3] & 0xffffull);
               (void)(hipEventDestroy(d0));
               (void)(hipEventDestroy(d1));
             }

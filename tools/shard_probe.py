@@ -3,7 +3,8 @@
 GPU: rank r of N renders tiles t % N == r (what bench.py --gpus N runs on
 each GPU).  The slowest shard's time bounds the N-GPU frame (plus the RCCL
 gather of a few MB).  Prints one JSON line per N.
-usage (GPU box): python tools/shard_probe.py [--scene NAME.ray] [--flags "-w 1920 ..."] [N ...]
+usage (GPU box): python tools/shard_probe.py [--scene NAME.ray] [--flags "-w 1920 ..."] [--rank R] [N ...]
+(--rank R: only rank R of each N > 1, e.g. for a kernel trace of one shard)
 (dragon.ray, C5's scene, is generated when missing: tools/gen_scenes.py --dragon)"""
 import json
 import os
@@ -23,9 +24,12 @@ def main():
     args = sys.argv[1:]
     flags = "-w 1920 -r 5 -O r -A 4"
     scene = "trimesh2.ray"
-    while args and args[0] in ("--flags", "--scene"):
+    only_rank = None
+    while args and args[0] in ("--flags", "--scene", "--rank"):
         if args[0] == "--flags":
             flags = args[1]
+        elif args[0] == "--rank":
+            only_rank = int(args[1])
         else:
             scene = args[1]
         args = args[2:]
@@ -41,6 +45,8 @@ def main():
     for n in ns:
         times = []
         for r in range(n):
+            if only_rank is not None and n > 1 and r != only_rank:
+                continue
             tile = 32 if n > 1 else 0
             npix = pkg.shard_pixels(opts, h, tile, r, n, n > 1)
             out = torch.zeros(npix * 3, dtype=torch.uint8, device="cuda")
