@@ -23,6 +23,21 @@
 
 namespace rtxd {
 
+// Materialise loaded values here (an empty asm that uses them): the loads
+// of a record, box or face are issued as one burst and waited for once,
+// instead of the compiler sinking each into the branch that first needs it
+// (one dependent round trip per branch for a wave stepping alone).  Device
+// code only; the host build of the traversal (tests/native) has no VGPRs.
+#if defined(__HIP_DEVICE_COMPILE__)
+__device__ __forceinline__ void pin(double x) { asm volatile("" ::"v"(x)); }
+__device__ __forceinline__ void pin(float x) { asm volatile("" ::"v"(x)); }
+__device__ __forceinline__ void pin(int x) { asm volatile("" ::"v"(x)); }
+#else
+inline void pin(double) {}
+inline void pin(float) {}
+inline void pin(int) {}
+#endif
+
 using rtm::dvec2;
 using rtm::dvec3;
 using rtm::mk3;
@@ -150,6 +165,11 @@ __host__ __device__ __forceinline__ bool cone_good(const double* prm, const dvec
 RT_HD bool slab(const double* bmin, const double* bmax, const dvec3& o, const dvec3& d,
                                      double& tMinOut, double& tMaxOut) {
   const double lo[3] = {bmin[0], bmin[1], bmin[2]}, hi[3] = {bmax[0], bmax[1], bmax[2]};
+#pragma unroll
+  for (int a = 0; a < 3; ++a) {
+    pin(lo[a]);
+    pin(hi[a]);
+  }
   double tMin = -1.0e308, tMax = 1.0e308;
   bool out = false;
 #pragma unroll
@@ -202,6 +222,11 @@ RT_HD bool box_test(const double* lo, const double* hi, const dvec3& o, const dv
   if (!ri.fast) return slab(lo, hi, o, d, a, b);
   // the box whole, then the axes branch-free (a d[k] == 0 axis selected away)
   const double l[3] = {lo[0], lo[1], lo[2]}, h[3] = {hi[0], hi[1], hi[2]};
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    pin(l[k]);
+    pin(h[k]);
+  }
   double tmin = -1.0e308, tmax = 1.0e308;
 #pragma unroll
   for (int k = 0; k < 3; ++k) {
@@ -484,6 +509,8 @@ RT_HD bool tri_hit(const RtxFace& F, const dvec3& p, const dvec3& d, double tcap
   // after it: a second dependent round trip per face)
   const dvec3 n = ld3(F.n);
   const dvec3 v0 = ld3(F.v0), v1 = ld3(F.v1), v2 = ld3(F.v2);
+  pin(n.x), pin(n.y), pin(n.z), pin(v0.x), pin(v0.y), pin(v0.z);
+  pin(v1.x), pin(v1.y), pin(v1.z), pin(v2.x), pin(v2.y), pin(v2.z);
   double t = rtm::dot(n, d);
   if (t < RTX_EPS32 && t > -RTX_EPS32) return false;
   t = rtm::dot(v0 - p, n) / t;
