@@ -21,6 +21,10 @@
 #include "../common/rt_math.h"
 #include "rtx.h"
 
+// RtxObject.pad slot the device upload fills: the object is opaque to
+// shadow walks (rtx_scene_create; walk_hit)
+#define RTX_OBJ_WOPAQUE 0
+
 namespace rtxd {
 
 // Materialise loaded values here (an empty asm that uses them): the loads

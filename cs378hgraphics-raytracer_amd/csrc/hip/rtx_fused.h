@@ -55,14 +55,24 @@ __device__ __forceinline__ bool walk_hit(const DevScene& S, const RtxLight& L, c
   }
   const double t = bt - w.last_t;
   w.last_t = bt;
-  const HitRef R = resolve_hit(S, pb, sdir, bobj, bsub, nullptr, nullptr);
-  const bool is_inside = rtm::dot(R.N, sdir) > 0;
   w.wpos = rtm::ray_at(w.wpos, sdir, t);
   // sattnLimitCheck with the relative t (U14); directional lights never trip it
   if (L.type == RTX_LIGHT_POINT && rtm::dot(ld3(L.pos) - rtm::ray_at(w.wpos, sdir, t), sdir) <= 0) {
     res = w.sattn;
     return true;
   }
+  // An object opaque to walks (not transmissive, kt a constant 0, no
+  // per-vertex materials): entered from outside the walk returns 0; left
+  // from inside, sattn *= 0^t = +0 (t > 0) and, every kt in [0, 1]
+  // (skip_dark), every later factor keeps it +0 — the walk's answer is +0
+  // either way, so it ends here without the hit's normal (resolve_hit's
+  // dependent loads) or its remaining queries.
+  if (S.skip_dark && t > 0.0 && S.objs[bobj].pad[RTX_OBJ_WOPAQUE]) {
+    res = mk3(0.0, 0.0, 0.0);
+    return true;
+  }
+  const HitRef R = resolve_hit(S, pb, sdir, bobj, bsub, nullptr, nullptr);
+  const bool is_inside = rtm::dot(R.N, sdir) > 0;
   const bool next_trans = is_inside ? true : ((hit_flags(S, R) & RTX_MF_TRANS) != 0);
   if (!next_trans) {
     res = mk3(0.0, 0.0, 0.0);

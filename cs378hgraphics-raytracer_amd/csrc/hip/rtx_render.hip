@@ -2563,7 +2563,23 @@ rtx_status rtx_scene_create(int device, const RtxSceneDesc* d, void** out) {
 #define UP(src, n, dst) \
   if ((rc = upload(*st, src, size_t(n), &dst)) != RTX_OK) { rtx_scene_destroy(st); return rc; }
   UP(d->scene_nodes, d->n_scene_nodes, S.snodes);
-  UP(d->objects, d->n_objects, S.objs);
+  // objects as the loader flattened them, plus pad[RTX_OBJ_WOPAQUE]: 1 when
+  // a shadow walk that hits the object cannot carry light past it — its
+  // material is not transmissive and its kt a constant (0, 0, 0), with no
+  // per-vertex materials (walk_hit's shortcut, rtx_fused.h)
+  std::vector<RtxObject> objs(d->objects, d->objects + d->n_objects);
+  for (RtxObject& o : objs) {
+    bool op = o.material >= 0 && o.material < d->n_materials;
+    if (op) {
+      const RtxMaterial& m = d->materials[o.material];
+      const RtxParam& kt = m.p[RTX_P_KT];
+      op = !(m.flags & RTX_MF_TRANS) && kt.tex < 0 && kt.v[0] == 0.0 && kt.v[1] == 0.0 && kt.v[2] == 0.0;
+    }
+    if (op && o.type == RTX_OBJ_TRIMESH)
+      op = o.mesh >= 0 && o.mesh < d->n_meshes && !d->meshes[o.mesh].has_vmats;
+    o.pad[RTX_OBJ_WOPAQUE] = op ? 1 : 0;
+  }
+  UP(objs.data(), d->n_objects, S.objs);
   UP(d->obj_params, size_t(d->n_objects) * RTX_OBJ_PARAMS, S.oprm);
   UP(d->materials, d->n_materials, S.mats);
   UP(d->meshes, d->n_meshes, S.meshes);
