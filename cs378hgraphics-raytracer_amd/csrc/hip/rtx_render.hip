@@ -3203,11 +3203,21 @@ rtx_status rtx_render(void* scene, const RtxRenderParams* params, uint8_t* rgb8,
     if (per_cu < 1) per_cu = 1;
     int64_t tgrid = static_cast<int64_t>(st->n_cu) * per_cu;
     {
-      // RTX_TGRID_DIV (A/B): persistent trace grids of 1/div of the resident
-      // workgroups, so the groups' kernels can share the GPU instead of each
-      // filling it
+      // Persistent trace grids of 1/div of the resident workgroups, so the
+      // groups' kernels share the GPU instead of each filling it: on small
+      // frames (a shard of a multi-GPU frame: at most RTX_TGRID_SMALL samples,
+      // default 10 M), div = G — there the groups' launches are mostly
+      // latency-bound and a group's advance launch otherwise waits for CU
+      // space behind the other groups' persistent kernels (8-way headline
+      // shard 7.85-8.08 -> 7.61 ms; the whole frame 36.9 -> 38.4 ms, so not
+      // there).  RTX_TGRID_DIV overrides (1: whole-GPU grids).
+      int64_t small = 10000000;
+      const char* es = getenv("RTX_TGRID_SMALL");
+      if (es) small = atoll(es);
+      int div = F.n_samples <= small ? G : 1;
       const char* e = getenv("RTX_TGRID_DIV");
-      if (e && atoi(e) > 1) tgrid = std::max<int64_t>(1, tgrid / atoi(e));
+      if (e && atoi(e) > 0) div = atoi(e);
+      if (div > 1) tgrid = std::max<int64_t>(1, tgrid / div);
     }
     if (tgrid > per) tgrid = per;
     // the fused kernels' own residency (their launch bounds differ:
