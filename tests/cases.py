@@ -56,4 +56,9 @@ CASES = [
     ("trimesh2_adaptive", "trimesh2.ray", "-w 32 -r 5 -O a -A 4 -B 0.03"),
     ("adaptive_dof", "trimesh2.ray", "-w 24 -r 3 -O a -A 2 -B 0.05 -O d -A 2.5 -B 4 -C 0.05"),
     ("adaptive_anaglyph", "spheres_overlap.ray", "-w 24 -r 3 -O g -O a -A 2 -B 0.05"),
+    # shadow walks ending at objects opaque to them (walk_hit's shortcut):
+    # exits from inside an opaque box, a coincident second box (exits at the
+    # same t), an opaque cube inside a glass sphere
+    ("walk_opaque", "walk_opaque.ray", "-w 32 -r 4"),
+    ("walk_opaque_aa", "walk_opaque.ray", "-w 24 -r 5 -O r -A 2"),
 ]
