@@ -8,6 +8,10 @@ RCCL) the frame is cut into 32x32 tiles dealt round-robin along rotated rows
 (diagonal stripes, deal index % N == rank),
 each rank renders its tiles into a packed HBM buffer and rank 0 gathers them
 over xGMI (dist.gather) — total work is fixed, so scaling is strong.
+`python3 bench.py --gpus N` starts the N ranks itself (launch_ranks: child
+processes, rendezvous on 127.0.0.1, the first failing rank ends the job);
+under `torch.distributed.run --nproc-per-node N ... bench.py --gpus N` the
+launcher's ranks are used as they are.
 
 value = rays of the whole frame (camera + reflection/refraction + shadow
 queries) / frame wall time, taken as the max over ranks between
@@ -25,6 +29,11 @@ import subprocess
 import sys
 import time
 
+# The CPU leg's OpenMP threads stay on their cores (one per core, packed):
+# set before any OpenMP runtime (torch's or the oracle's) initialises
+os.environ.setdefault("OMP_PROC_BIND", "close")
+os.environ.setdefault("OMP_PLACES", "cores")
+
 ROOT = os.path.dirname(os.path.abspath(__file__))
 METRIC = "Mrays/sec + frame ms, trimesh2.ray 1920×1080 depth-5 4×AA; 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
@@ -32,12 +41,12 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 # record, triangle record, material record per shade
 # (a BVH box test reads one 32-B entry of a 128-B 4-wide float record)
 B_RAY, B_NODE, B_OBJ, B_TRI, B_SHADE = 48 + 72, 32, 224, 96, 176
-# VALU issue ceiling (MI355X_MICROARCH.md: 256 CUs x 4 SIMDs at 2.4 GHz; a
-# wave64 VALU instruction issues over 2 cycles on a SIMD-32, an FP64 one at
-# half the FP32 rate, i.e. 4 cycles): wave-instructions per second
+# VALU issue ceiling (MI355X_MICROARCH.md: 256 CUs x 4 SIMDs at 2.4 GHz).  A
+# CDNA SIMD is 16 lanes wide, so every non-packed wave64 VALU instruction —
+# FP32, FP64 or integer — occupies it for 4 cycles (78.6 TF FP64 vector =
+# 256 x 4 x 16 lanes x 2.4 GHz x 2): wave-instructions per second
 N_CU, SIMD_PER_CU, CLOCK_HZ = 256, 4, 2.4e9
-VALU_PEAK_F64 = N_CU * SIMD_PER_CU * CLOCK_HZ / 4   # every instruction priced as FP64
-VALU_PEAK_ISSUE = N_CU * SIMD_PER_CU * CLOCK_HZ / 2  # every instruction at the 2-cycle issue rate
+VALU_PEAK = N_CU * SIMD_PER_CU * CLOCK_HZ / 4
 
 
 def kernel_bytes(w):
@@ -149,6 +158,8 @@ def cpu_baseline(pkg, path, opts, height, budget_s=10.0, repeats=3):
     return {"value": med, "unit": "Mrays/s", "cores": threads, "kind": "port",
             "cpu_model": model, "host_cpus": ncpu, "affinity_cpus": aff, "cgroup_cpu_quota": quota,
             "runs_mrays_s": [round(x, 3) for x in rates], "full_frame": band >= height,
+            "spread": round((rates[-1] - rates[0]) / med, 4),
+            "omp": {"proc_bind": os.environ.get("OMP_PROC_BIND"), "places": os.environ.get("OMP_PLACES")},
             "sample": f"CPU restatement (oracle/, g++ -O2, OpenMP {threads} threads) on {what}, median of {repeats} runs",
             "_band": band, "_threads": threads}
 
@@ -194,9 +205,109 @@ def parity_block(pkg, dev, path, opts, height, band, threads):
     return m
 
 
+def _free_port():
+    import socket
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(n, argv, probe=False, grace_s=10.0):
+    """`bench.py --gpus N` without an external launcher: start N rank
+    processes of this script (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* set,
+    rendezvous on 127.0.0.1) and return the job's exit code.  The parent
+    touches neither HIP nor torch.cuda beyond counting devices (which does not
+    initialise the runtime) and never execs: the ranks are children.  The
+    first rank to fail ends the others (SIGTERM, then SIGKILL after
+    `grace_s`), and its exit code is the job's — the counterpart of the
+    product driver's failure path (csrc/host/multi_gpu.cpp)."""
+    import signal
+
+    if not probe:
+        import torch
+
+        ndev = torch.cuda.device_count()
+        if ndev < n:
+            print(f"bench.py: --gpus {n} needs {n} visible GPUs, {ndev} visible", file=sys.stderr, flush=True)
+            return 3
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + argv, env=env))
+
+    def stop_all(sig):
+        for p in procs:
+            if p.poll() is None:
+                try:
+                    p.send_signal(sig)
+                except OSError:
+                    pass
+
+    def on_term(signum, _frame):  # the job's own time limit: take the ranks along
+        stop_all(signal.SIGKILL)
+        sys.exit(128 + signum)
+
+    old = signal.signal(signal.SIGTERM, on_term)
+    rc = 0
+    try:
+        live = set(range(n))
+        while live and rc == 0:
+            for r in sorted(live):
+                c = procs[r].poll()
+                if c is None:
+                    continue
+                live.discard(r)
+                if c != 0:
+                    print(f"bench.py: rank {r} of {n} exited with {c}; ending the other ranks", file=sys.stderr,
+                          flush=True)
+                    rc = c if c > 0 else 128 - c
+                    break
+            time.sleep(0.05)
+        if rc != 0:
+            stop_all(signal.SIGTERM)
+            t_end = time.monotonic() + grace_s
+            while any(p.poll() is None for p in procs) and time.monotonic() < t_end:
+                time.sleep(0.05)
+            stop_all(signal.SIGKILL)
+        for p in procs:
+            p.wait()
+    finally:
+        signal.signal(signal.SIGTERM, old)
+    return rc
+
+
+def launch_probe(args):
+    """Rank body of `--launch-probe` (CPU test of launch_ranks): report the
+    rendezvous environment, run one gloo all-reduce over the ranks, and fail
+    on request — no device is touched."""
+    import torch
+    import torch.distributed as dist
+
+    rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
+    if rank == args.launch_probe_fail:
+        sys.exit(7)
+    if args.launch_probe_fail >= 0:
+        time.sleep(600)  # another rank fails: the launcher must end this one
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    t = torch.tensor([rank + 1])
+    dist.all_reduce(t)
+    if rank == 0:
+        print(json.dumps({"n_gpus": world, "rank_sum": int(t.item()), "master": os.environ["MASTER_ADDR"],
+                          "local_ranks": world}), flush=True)
+    dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="GPUs of this node, one rank each (default 1; under torch.distributed.run: WORLD_SIZE)")
+    ap.add_argument("--launch-probe", action="store_true", help=argparse.SUPPRESS)
+    ap.add_argument("--launch-probe-fail", type=int, default=-1, help=argparse.SUPPRESS)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--scene", default=os.path.join(ROOT, "scenes", "trimesh2.ray"))
@@ -209,9 +320,28 @@ def main():
                     help="PMC-measured HBM bytes per launch (tools/profile_traffic.sh output)")
     args = ap.parse_args()
 
+    if "WORLD_SIZE" not in os.environ:
+        # no launcher around us: --gpus N > 1 starts the N ranks itself
+        n = 1 if args.gpus is None else args.gpus
+        if n < 1:
+            print("bench.py: --gpus must be >= 1", file=sys.stderr)
+            sys.exit(2)
+        if n > 1 or args.launch_probe:
+            if not args.launch_probe:  # host-only preparation, before any rank starts
+                ensure_built(os.path.join(ROOT, "cs378hgraphics-raytracer_amd"))
+                if not os.path.exists(args.scene):
+                    subprocess.run([sys.executable, os.path.join(ROOT, "tools", "gen_scenes.py")], check=True,
+                                   stdout=subprocess.DEVNULL)
+            sys.exit(launch_ranks(n, sys.argv[1:], probe=args.launch_probe))
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.gpus is not None and args.gpus != world:
+        print(f"bench.py: --gpus {args.gpus} but the launcher started {world} ranks", file=sys.stderr)
+        sys.exit(2)
+    if args.launch_probe:
+        launch_probe(args)
+        return
     pkg_dir = os.path.join(ROOT, "cs378hgraphics-raytracer_amd")
     if rank == 0 or world == 1:
         ensure_built(pkg_dir)
@@ -324,10 +454,10 @@ def main():
                 traffic = None
         # VALU issue ceiling (SURVEY 8(d)'s FP64-VALU secondary bound), from
         # the same stamped PMC passes: VALU wave-instructions of one frame /
-        # the frame's GPU time / the issue peak
+        # the frame's GPU time / the issue peak = the measured share of VALU
+        # issue cycles
         valu = totals.get("SQ_INSTS_VALU")
-        frac_valu = round(valu / (avg_kernel_ms * 1e-3) / VALU_PEAK_F64, 4) if valu else None
-        frac_valu_issue = round(valu / (avg_kernel_ms * 1e-3) / VALU_PEAK_ISSUE, 4) if valu else None
+        frac_valu = round(valu / (avg_kernel_ms * 1e-3) / VALU_PEAK, 4) if valu else None
         f64 = sum(totals.get(k, 0.0) for k in ("SQ_INSTS_VALU_ADD_F64", "SQ_INSTS_VALU_MUL_F64",
                                                  "SQ_INSTS_VALU_FMA_F64", "SQ_INSTS_VALU_TRANS_F64"))
         frac_hbm = round(traffic / (avg_kernel_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4) if traffic else None
@@ -354,11 +484,11 @@ def main():
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                          # measured: PMC HBM bytes of a frame / the frame's GPU time / peak
                          "frac_hbm": frac_hbm,
-                         # measured: VALU wave-instructions of a frame / GPU time / issue peak,
-                         # priced as FP64 (4 cycles) and at the 2-cycle issue rate
-                         "frac_valu": frac_valu, "frac_valu_issue": frac_valu_issue,
+                         # measured: VALU wave-instructions of a frame / GPU time / issue
+                         # peak (4 cycles per wave64 instruction on a 16-lane SIMD)
+                         "frac_valu": frac_valu,
                          "valu_insts": valu, "valu_f64_insts": f64 or None,
-                         "valu_peak_per_s": {"f64": VALU_PEAK_F64, "issue": VALU_PEAK_ISSUE},
+                         "valu_peak_per_s": VALU_PEAK,
                          "traffic_source": traffic_src,
                          "kernel": ("render_kernel<false,false> (megakernel, 1 launch per frame)" if mega else
                                     "frame span: advance_kernel + trace_kernel<false,1|2> iterations on 3 streams"),

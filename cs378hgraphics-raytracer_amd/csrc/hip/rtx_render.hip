@@ -2430,6 +2430,11 @@ struct SceneState {
   unsigned int* h_counters = nullptr;  // pinned
   DevScene* d_scene = nullptr;         // device copy of S_launch (shadow early-out)
   unsigned int* d_acnt = nullptr;      // adaptive AA: regions to subdivide, emit cursor
+  // adaptive AA: one buffer per level (values, first-quarter index, mask,
+  // regions), grown on demand and reused by later frames (no hipMalloc /
+  // hipFree, which synchronises the device, per level per frame)
+  std::vector<void*> d_level;
+  std::vector<size_t> level_bytes;
   int64_t last_work[RTX_STATS_N] = {};  // raw counters of the last counting render (rtx_last_work)
   std::vector<hipEvent_t> ev_pool;
   size_t ev_used = 0;
@@ -2671,6 +2676,8 @@ rtx_status rtx_scene_destroy(void* scene) {
   if (st->d_work) (void)hipFree(st->d_work);
   if (st->d_stats) (void)hipFree(st->d_stats);
   if (st->d_acnt) (void)hipFree(st->d_acnt);
+  for (void* p : st->d_level)
+    if (p) (void)hipFree(p);
   if (st->d_picks) (void)hipFree(st->d_picks);
   if (st->d_offv) (void)hipFree(st->d_offv);
   if (st->d_sbuf) (void)hipFree(st->d_sbuf);
@@ -3487,20 +3494,17 @@ rtx_status rtx_render(void* scene, const RtxRenderParams* params, uint8_t* rgb8,
     F.adapt = 1;
     F.aregs = nullptr;
     if ((rc = run_wavefront(F, npix, true)) != RTX_OK) return rc;
-    struct LevelBufs {
-      void* p = nullptr;
-      ~LevelBufs() {
-        if (p) (void)hipFree(p);
-      }
-    };
-    std::vector<std::unique_ptr<LevelBufs>> held_levels;
+    size_t nlevel = 0;  // level buffers handed out this frame
     auto level_alloc = [&](int64_t n, bool regs, ALevel& lv) -> rtx_status {
       auto al = [](size_t x) { return (x + 255) & ~size_t(255); };
       const size_t bv = al(size_t(n) * sizeof(dvec3)), bi = al(size_t(n) * sizeof(int));
       const size_t br = regs ? al(size_t(n) * sizeof(ARegion)) : 0;
-      held_levels.emplace_back(new LevelBufs());
-      HIP_TRY(hipMalloc(&held_levels.back()->p, bv + 2 * bi + br + 256));
-      char* b = static_cast<char*>(held_levels.back()->p);
+      if (st->d_level.size() <= nlevel) {
+        st->d_level.push_back(nullptr);
+        st->level_bytes.push_back(0);
+      }
+      if ((rc = ensure(&st->d_level[nlevel], &st->level_bytes[nlevel], bv + 2 * bi + br + 256)) != RTX_OK) return rc;
+      char* b = static_cast<char*>(st->d_level[nlevel++]);
       lv.val = reinterpret_cast<dvec3*>(b);
       lv.first = reinterpret_cast<int*>(b + bv);
       lv.mask = reinterpret_cast<int*>(b + bv + bi);

@@ -23,6 +23,7 @@
 #include <chrono>
 #include <csignal>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <iostream>
 #include <string>
@@ -53,13 +54,32 @@ struct Rendezvous {
 // that publishes it here, and the others return instead of waiting for it
 // forever.  (Failures after the collectives started are ended by the
 // parent, which terminates the remaining ranks on the first non-zero exit.)
+// How long a rank waits for the others (RTX_RANK_WAIT_S seconds, default 600;
+// 0: no limit — the parent still ends every rank when one fails).  Each rank
+// builds its scene's trees on the CPU before it joins, so a large scene on
+// many ranks at once can take a while.
+static long rank_wait_s() {
+  const char* e = getenv("RTX_RANK_WAIT_S");
+  if (e && *e) {
+    char* end = nullptr;
+    const long v = strtol(e, &end, 10);
+    if (end && *end == 0 && v >= 0) return v;
+  }
+  return 600;
+}
+
+static bool waited_too_long(std::chrono::steady_clock::time_point t0) {
+  const long lim = rank_wait_s();
+  return lim > 0 && std::chrono::steady_clock::now() - t0 > std::chrono::seconds(lim);
+}
+
 bool rendezvous_join(Rendezvous* rv, int rank, int nranks) {
   rv->joined.fetch_add(1);
   const auto t0 = std::chrono::steady_clock::now();
   for (;;) {
     if (rv->failed.load()) return false;
     if (rv->joined.load() >= nranks) return true;
-    if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(120)) {
+    if (waited_too_long(t0)) {
       std::cerr << "rank " << rank << ": the other ranks did not come up" << std::endl;
       rv->failed.store(1);
       return false;
@@ -102,7 +122,7 @@ int run_rank(const rtxh::CliOptions& o, void* hs, int rank, int nranks, Rendezvo
   } else {
     const auto t0 = std::chrono::steady_clock::now();
     while (rv->id_ready.load(std::memory_order_acquire) == 0) {
-      if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(120)) {
+      if (waited_too_long(t0)) {
         std::cerr << "rank " << rank << ": no communicator id from rank 0" << std::endl;
         return 3;
       }

@@ -61,4 +61,8 @@ CASES = [
     # same t), an opaque cube inside a glass sphere
     ("walk_opaque", "walk_opaque.ray", "-w 32 -r 4"),
     ("walk_opaque_aa", "walk_opaque.ray", "-w 24 -r 5 -O r -A 2"),
+    # R1 at parity size: the headline geometry with reflective / transmissive
+    # materials (ray trees that fork at every level, RayTracer.cpp:127-165)
+    ("r1_glass_aa4", "trimesh2_glass.ray", "-w 32 -r 5 -O r -A 4"),
+    ("r1_glass_r8", "trimesh2_glass.ray", "-w 40 -r 8"),
 ]

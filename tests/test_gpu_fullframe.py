@@ -7,6 +7,10 @@
                       (2.07 M samples, 35.3 M camera rays)
 * a C5 band           dragon.ray -w 3840 -r 5 -O a -A 8: one 32-row band of
                       the 3840x2160 frame (7.9 M top-level samples)
+* R1                  trimesh2_glass.ray -w 1920 -r 5 -O r -A 4: the headline
+                      geometry with reflective / transmissive materials
+                      (recursion-heavy: ~3x as many reflection / refraction
+                      rays as camera rays, RayTracer.cpp:127-165)
 
 RayTracer::traceImage (RayTracer.cpp:279-314) is the unit compared: RGB
 within 1e-4, rgb8 equal off the truncation boundary, object / face /
@@ -28,6 +32,7 @@ FRAMES = [
     ("headline", "trimesh2.ray", "-w 1920 -r 5 -O r -A 4"),
     ("c3", "trimesh2_square.ray", "-w 1024 -r 5 -O r -A 4"),
     ("c4_dof16", "trimesh2.ray", "-w 1920 -r 5 -O d -A 2.5 -B 16 -C 0.05"),
+    ("r1_glass", "trimesh2_glass.ray", "-w 1920 -r 5 -O r -A 4"),
 ]
 
 
@@ -44,6 +49,8 @@ def test_full_frame_parity(pkg, orc, name, scene, flags):
     assert_parity(m)
     for k in ("camera_rays", "secondary_rays", "shadow_rays"):
         assert gpu["stats"][k] == ref["stats"][k], (k, gpu["stats"][k], ref["stats"][k])
+    if name == "r1_glass":  # the config's point: the ray trees fork
+        assert gpu["stats"]["secondary_rays"] >= gpu["stats"]["camera_rays"]
 
 
 def _dragon():

@@ -8,6 +8,8 @@ Configs (BASELINE.json "configs"):
   C3 trimesh2 1024x1024 -r 5 -O r -A 4      (square-aspect stand-in)
   C4 trimesh2 1920x1080 -r 5 DoF fd 2.5, 16 rays, aperture 0.05
   C5 dragon (1M triangles) 3840x2160 -r 5 -O a -A 8
+  R1 trimesh2_glass 1920x1080 -r 5 -O r -A 4 (recursion-heavy: the headline
+     geometry with reflective / transmissive materials; not a BASELINE config)
 The headline (trimesh2 1920x1080 -r 5 -O r -A 4) is bench.py's.
 usage: python tools/bench_configs.py [C1 C2 ...]  (on the GPU box)
 """
@@ -26,6 +28,7 @@ CONFIGS = {
     "C3": ("trimesh2_square.ray", "-w 1024 -r 5 -O r -A 4"),
     "C4": ("trimesh2.ray", "-w 1920 -r 5 -O d -A 2.5 -B 16 -C 0.05"),
     "C5": ("dragon.ray", "-w 3840 -r 5 -O a -A 8"),
+    "R1": ("trimesh2_glass.ray", "-w 1920 -r 5 -O r -A 4"),
 }
 
 

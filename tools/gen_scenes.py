@@ -15,7 +15,9 @@ fixes:
                   index 1.33, one reflective glass wall, a displaced
                   sculpture), ~60k triangles in <= 20 trimeshes (seed 2);
                   2 point lights + ambient; aspect 16:9 (headline) —
-                  trimesh2_square.ray is the same scene at aspect 1.
+                  trimesh2_square.ray is the same scene at aspect 1,
+                  trimesh2_glass.ray the same geometry with reflective /
+                  transmissive materials (recursion-heavy config R1).
   dragon.ray      1M-triangle displaced subdivided mesh (seed 7), 2 point
                   lights, aspect 16:9 (generated on demand, not committed).
 
@@ -183,7 +185,11 @@ def sphere_mesh(c, r, nu, nv, amp, rng):
     return v, f
 
 
-def trimesh2(path, aspect, tris_target=60000):
+def trimesh2(path, aspect, tris_target=60000, glass=False):
+    """glass=True: trimesh2_glass.ray, the same geometry with polished,
+    reflective and transmissive materials, so the depth-5 ray trees fork
+    (RayTracer.cpp:127-165): more reflection / refraction rays than camera
+    rays at -r 5 (the recursion-heavy full-frame config)."""
     rng = np.random.default_rng(2)
     scale = tris_target / 60000.0
     meshes = []
@@ -193,6 +199,15 @@ def trimesh2(path, aspect, tris_target=60000):
     mat_water = "{ diffuse = (0.05, 0.2, 0.3); specular = (0.8, 0.8, 0.8); shininess = 120; transmissive = (0.75, 0.9, 0.95); reflective = (0.15, 0.15, 0.15); index = 1.33; }"
     mat_glass = "{ diffuse = (0.02, 0.03, 0.04); specular = (0.9, 0.9, 0.9); shininess = 200; reflective = (0.7, 0.75, 0.8); }"
     mat_sculpt = "{ diffuse = (0.7, 0.25, 0.15); ambient = (0.2, 0.08, 0.05); specular = (0.7, 0.6, 0.5); shininess = 80; reflective = (0.2, 0.2, 0.2); }"
+    if glass:
+        mat_stone = ("{ diffuse = (0.45, 0.44, 0.4); ambient = (0.15, 0.15, 0.15); specular = (0.5, 0.5, 0.5); "
+                     "shininess = 90; reflective = (0.35, 0.35, 0.33); }")
+        mat_wood = ("{ diffuse = (0.45, 0.28, 0.15); ambient = (0.12, 0.08, 0.04); specular = (0.6, 0.6, 0.6); "
+                    "shininess = 70; reflective = (0.25, 0.2, 0.15); }")
+        mat_pillar = ("{ diffuse = (0.1, 0.12, 0.12); specular = (0.9, 0.9, 0.9); shininess = 150; "
+                      "reflective = (0.3, 0.32, 0.32); transmissive = (0.6, 0.7, 0.7); index = 1.5; }")
+        mat_sculpt = ("{ diffuse = (0.08, 0.03, 0.02); specular = (0.9, 0.85, 0.8); shininess = 160; "
+                      "reflective = (0.25, 0.2, 0.2); transmissive = (0.7, 0.5, 0.45); index = 1.45; }")
     # slab (terrain-ish floor grid)
     n = max(8, int(60 * math.sqrt(scale)))
     meshes.append((grid_mesh(-14, 14, -18, 6, 0.0, n, n, 0.01, rng), mat_stone, False))
@@ -301,6 +316,7 @@ def main():
     hitchcock(os.path.join(outdir, "hitchcock.ray"))
     n = trimesh2(os.path.join(outdir, "trimesh2.ray"), 1.7777777777777777, tris)
     trimesh2(os.path.join(outdir, "trimesh2_square.ray"), 1.0, tris)
+    trimesh2(os.path.join(outdir, "trimesh2_glass.ray"), 1.7777777777777777, tris, glass=True)
     print("trimesh2 triangles:", n)
     if "--dragon" in sys.argv:
         print("dragon triangles:", dragon(os.path.join(outdir, "dragon.ray")))

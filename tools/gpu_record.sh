@@ -10,7 +10,7 @@
 #            passes, stamped with this build), then the bench again so its
 #            line carries this build's traffic and VALU fractions, and
 #            tools/kernel_roofline.py (per-kernel roofline; needs prof)
-#   shards   tools/shard_probe.py: headline, C4 and C5 at 1 and 8 shards
+#   shards   tools/shard_probe.py: headline, C4, R1 and C5 at 1 and 8 shards
 #   configs  tools/bench_configs.py (BASELINE C1-C5)
 # usage: bash tools/gpu_record.sh TAG step...
 set -o pipefail
@@ -54,6 +54,8 @@ for step in "$@"; do
       for fl in "-w 1920 -r 5 -O r -A 4" "-w 1920 -r 5 -O d -A 2.5 -B 16 -C 0.05"; do
         timeout -k 10 300 python tools/shard_probe.py --flags "$fl" 1 8 >> gpurun_out/shards_$TAG.jsonl || exit 1
       done
+      timeout -k 10 300 python tools/shard_probe.py --scene trimesh2_glass.ray --flags "-w 1920 -r 5 -O r -A 4" 1 8 \
+        >> gpurun_out/shards_$TAG.jsonl || exit 1
       timeout -k 10 400 python tools/shard_probe.py --scene dragon.ray --flags "-w 3840 -r 5 -O a -A 8" 1 8 \
         >> gpurun_out/shards_$TAG.jsonl || exit 1
       cat gpurun_out/shards_$TAG.jsonl ;;
