@@ -164,7 +164,7 @@ HIP_SYMBOLS = ["rtx_last_error", "rtx_device_count", "rtx_scene_create", "rtx_sc
                "rtx_shard_pixels", "rtx_kernel_time", "rtx_last_work"]
 HOST_SYMBOLS = ["rtx_host_last_error", "rtx_host_load", "rtx_host_desc", "rtx_host_info", "rtx_host_free",
                 "rtx_host_cubemap", "rtx_write_image", "rtx_image_height", "rtx_read_image", "rtx_shard_tiles",
-                "rtx_unpack_tiles", "rtx_host_tokens"]
+                "rtx_unpack_tiles", "rtx_host_tokens", "rtx_host_raw_records"]
 
 
 def _check_host(rc, what):

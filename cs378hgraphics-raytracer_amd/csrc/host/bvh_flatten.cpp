@@ -23,6 +23,7 @@
 #include <string>
 
 #include "../../../include/rtx_host.h"
+#include "raw_records.h"
 #include "scene_model.h"
 
 namespace rtxh {
@@ -457,6 +458,28 @@ rtx_status rtx_host_tokens(const char* ray_path, char* out, int64_t cap, int64_t
   if (out) {
     if (cap < *need) {
       g_host_err = "rtx_host_tokens: output buffer too small";
+      return RTX_ERR_INVALID;
+    }
+    std::memcpy(out, t.c_str(), t.size() + 1);
+  }
+  return RTX_OK;
+}
+
+rtx_status rtx_host_raw_records(const char* ray_path, char* out, int64_t cap, int64_t* need) {
+  if (!ray_path || !need) {
+    g_host_err = "rtx_host_raw_records: null argument";
+    return RTX_ERR_INVALID;
+  }
+  std::string t;
+  try {
+    t = rtxh::dump_raw_records(rtxh::parse_ray_file_raw(ray_path));
+  } catch (const std::exception& e) {
+    t = std::string("ERROR\t") + e.what() + "\n";
+  }
+  *need = static_cast<int64_t>(t.size()) + 1;
+  if (out) {
+    if (cap < *need) {
+      g_host_err = "rtx_host_raw_records: output buffer too small";
       return RTX_ERR_INVALID;
     }
     std::memcpy(out, t.c_str(), t.size() + 1);

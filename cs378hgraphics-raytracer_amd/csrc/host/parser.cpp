@@ -222,17 +222,21 @@ class Tokenizer {
       started_ = true;
       li_ = 0;
       ci_ = 0;
-      if (lines_.empty()) {
+      if (lines_.empty()) {  // the first GetLine already fails: LineNumber 1
         eof_ = true;
         cur_ = '\0';
+        line_ = 1;
         return;
       }
     } else {
       ++li_;
       ci_ = 0;
       if (li_ >= lines_.size()) {
+        // Buffer::GetLine counts the failing read at EOF as a line too
+        // (buffer.cpp:91-98: LineNumber++ before the stream is tested)
         eof_ = true;
         cur_ = '\0';
+        line_ = static_cast<int>(li_) + 1;
         return;
       }
     }

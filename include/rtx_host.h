@@ -72,6 +72,13 @@ rtx_status rtx_unpack_tiles(const void* packed, int32_t width, int32_t height, i
  * after the tokens read before a syntax error.  `out` (capacity `cap`
  * bytes, NUL-terminated) may be NULL to query `*need`. */
 rtx_status rtx_host_tokens(const char* ray_path, char* out, int64_t cap, int64_t* need);
+/* The raw parse records of a .ray file (Parser::parseScene's output before
+ * any scene-build arithmetic: transform chains, material copies, mesh
+ * vertex / face / normal lists, light attributes, camera ops) as canonical
+ * text (csrc/host/raw_records.h), or "ERROR\t<the loader's message>" when
+ * the parse fails.  Diagnostic: tests compare it with the checker's own
+ * restated parser.  `out` may be NULL to query `*need`. */
+rtx_status rtx_host_raw_records(const char* ray_path, char* out, int64_t cap, int64_t* need);
 /* height the CLI derives from -w (CommandLineUI.cpp:156) */
 int32_t rtx_image_height(int32_t width, double aspect);
 

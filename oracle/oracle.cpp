@@ -14,12 +14,21 @@
 #include <algorithm>
 #include <cmath>
 #include <cstring>
+#include <fstream>
+#include <sstream>
 #include <memory>
 #include <numeric>
 #include <string>
 #include <vector>
 
+#include "../cs378hgraphics-raytracer_amd/csrc/host/raw_records.h"
 #include "../cs378hgraphics-raytracer_amd/csrc/host/scene_model.h"
+
+// the checker's own .ray loader (parse_restated.cpp; the product's parser is
+// not linked)
+rtxh::SceneModel oracle_parse_ray_file(const std::string& path);
+std::string oracle_token_dump(const std::string& text);
+bool oracle_load_cubemap(const std::string& file, rtxh::Texture faces[6], std::string& err);
 
 using rtm::dvec2;
 using rtm::dvec3;
@@ -1250,10 +1259,10 @@ struct Tracer {
 
 std::unique_ptr<Scene> build_scene(const std::string& path) {
   std::unique_ptr<Scene> S(new Scene());
-  // the parser's raw records; every derived quantity (transforms, world
+  // the raw records of the oracle's own parser; every derived quantity (transforms, world
   // boxes, camera basis, face records, light axes) is this oracle's own
   // restatement of the scene build (scene_build_restated.cpp)
-  S->model = rtxh::parse_ray_file_raw(path);
+  S->model = oracle_parse_ray_file(path);
   restate_scene_build(S->model);
   rtxh::SceneModel& M = S->model;
   for (const auto& t : M.textures) S->texs.push_back(Tex{&t});
@@ -1344,7 +1353,7 @@ const char* oracle_last_error(void) { return orc::g_err.c_str(); }
 
 int oracle_scene_dump(const char* ray_path, double* objs, int32_t cap, int32_t* n, double* cam) {
   try {
-    rtxh::SceneModel m = rtxh::parse_ray_file_raw(ray_path);
+    rtxh::SceneModel m = oracle_parse_ray_file(ray_path);
     orc::restate_scene_build(m);
     *n = static_cast<int32_t>(m.objects.size());
     if (cam) {
@@ -1376,9 +1385,42 @@ int oracle_scene_dump(const char* ray_path, double* objs, int32_t cap, int32_t* 
   }
 }
 
+static int copy_text(const std::string& t, char* out, int64_t cap, int64_t* need) {
+  *need = static_cast<int64_t>(t.size()) + 1;
+  if (out) {
+    if (cap < *need) {
+      orc::g_err = "output buffer too small";
+      return -1;
+    }
+    std::memcpy(out, t.c_str(), t.size() + 1);
+  }
+  return 0;
+}
+
+int oracle_raw_records(const char* ray_path, char* out, int64_t cap, int64_t* need) {
+  std::string t;
+  try {
+    t = rtxh::dump_raw_records(oracle_parse_ray_file(ray_path));
+  } catch (const std::exception& e) {
+    t = std::string("ERROR\t") + e.what() + "\n";
+  }
+  return copy_text(t, out, cap, need);
+}
+
+int oracle_tokens(const char* ray_path, char* out, int64_t cap, int64_t* need) {
+  std::ifstream f(ray_path, std::ios::binary);
+  if (!f) {
+    orc::g_err = std::string("Error: couldn't read scene file ") + ray_path;
+    return -1;
+  }
+  std::stringstream ss;
+  ss << f.rdbuf();
+  return copy_text(oracle_token_dump(ss.str()), out, cap, need);
+}
+
 double oracle_aspect(const char* ray_path) {
   try {
-    rtxh::SceneModel m = rtxh::parse_ray_file_raw(ray_path);
+    rtxh::SceneModel m = oracle_parse_ray_file(ray_path);
     orc::restate_scene_build(m);
     return m.camera.aspectRatio;
   } catch (const std::exception& e) {
@@ -1393,7 +1435,7 @@ int oracle_render(const char* ray_path, const char* cubemap_file, const RtxRende
     std::unique_ptr<orc::Scene> S = orc::build_scene(ray_path);
     if (cubemap_file && cubemap_file[0]) {  // TraceUI::smartLoadCubemap: failure => stderr, no cube map
       std::string err;
-      if (rtxh::load_cubemap(cubemap_file, S->cube_faces, err))
+      if (oracle_load_cubemap(cubemap_file, S->cube_faces, err))
         S->use_cube = true;
       else
         std::fprintf(stderr, "%s\n", err.c_str());

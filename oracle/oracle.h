@@ -53,6 +53,13 @@ int oracle_bvh_hash(const char* ray_path, uint64_t* scene_hash, uint64_t* mesh_h
 int oracle_probe(const char* ray_path, const double p[3], const double d[3], double* t, double n[3],
                  int32_t* object, int32_t* face);
 
+/* The raw parse records of the oracle's own loader (parse_restated.cpp) in
+ * the canonical text of csrc/host/raw_records.h ("ERROR\t<message>" on a
+ * parse error), and its tokenizer's stream in rtx_host_tokens' format.
+ * `out` may be NULL to query `*need`. */
+int oracle_raw_records(const char* ray_path, char* out, int64_t cap, int64_t* need);
+int oracle_tokens(const char* ray_path, char* out, int64_t cap, int64_t* need);
+
 /* Batched closest-hit (mode 0) or sorted all-hits (mode 1, kmax per ray)
  * queries for the traversal unit test. */
 int oracle_query_batch(const char* ray_path, int32_t n, const double* P, const double* D, int32_t mode,

@@ -50,8 +50,31 @@ def lib(pkg):
                                    C.POINTER(C.c_int32)]
         L.oracle_query_batch.argtypes = [C.c_char_p, C.c_int32, C.c_void_p, C.c_void_p, C.c_int32, C.c_int32,
                                          C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]
+        for fn in (L.oracle_raw_records, L.oracle_tokens):
+            fn.argtypes = [C.c_char_p, C.c_char_p, C.c_int64, C.POINTER(C.c_int64)]
         _lib = L
     return _lib
+
+
+def _text(fn, path: str) -> str:
+    need = C.c_int64()
+    if fn(path.encode(), None, 0, C.byref(need)) != 0:
+        raise RuntimeError("oracle text query failed")
+    buf = C.create_string_buffer(need.value)
+    if fn(path.encode(), buf, need.value, C.byref(need)) != 0:
+        raise RuntimeError("oracle text query failed")
+    return buf.value.decode("latin-1")
+
+
+def raw_records(pkg, path: str) -> str:
+    """The raw parse records of the oracle's own loader (parse_restated.cpp),
+    canonical text (csrc/host/raw_records.h); "ERROR\t<message>" on failure."""
+    return _text(lib(pkg).oracle_raw_records, path)
+
+
+def tokens(pkg, path: str) -> str:
+    """The oracle tokenizer's stream (rtx_host_tokens format)."""
+    return _text(lib(pkg).oracle_tokens, path)
 
 
 def query_batch(pkg, path: str, P, D, mode: int, kmax: int = 1):

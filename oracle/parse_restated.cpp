@@ -1,0 +1,1021 @@
+// parse_restated.cpp — the checker's own .ray loader.
+//
+// TEST INFRASTRUCTURE ONLY (see oracle.h).  The oracle used to link the
+// product's parser (csrc/host/parser.cpp), so a parse-semantics error above
+// the token stream — transform-chain order, material inheritance, scale(s)
+// vs scale(x, y, z), camera attribute order — would have been shared by
+// checker and product and invisible to every parity test.  This file
+// restates the reference loader independently, straight from its sources:
+//
+//   Buffer           ray/src/fileio/buffer.cpp:29-98  (std::getline per line,
+//                    '\n' re-appended, LineNumber bumped on every GetLine —
+//                    also the failing one at EOF — '\0' once the stream fails)
+//   Tokenizer        ray/src/parser/Tokenizer.cpp:70-376 (lazy scan, one
+//                    pushed-back token, Peek / Read / CondRead)
+//   reserved words   ray/src/parser/Token.cpp:121-196, token names :9-92
+//   Parser           ray/src/parser/Parser.cpp:26-1308
+//   exceptions       ParserException.cpp:5-19, RayTracer.cpp:216-234 (the
+//                    messages RayTracer::loadScene reports)
+//   Cone ctor        ray/src/SceneObjects/Cone.h:11-37
+//   Trimesh          trimesh.cpp:25-67 (addFace range check, doubleCheck)
+//   Material         scene/material.h:152-163, 216-243, 272-276 (which
+//                    setters run setBools)
+//   cube-map files   ray/src/ui/TraceUI.cc:87-167 (matchCubemapFiles,
+//                    smartLoadCubemap)
+//
+// It fills the raw records of scene_model.h, which the oracle's own scene
+// build (scene_build_restated.cpp) turns into transforms, boxes and the
+// camera basis.  tests/test_oracle_parser.py checks that the product parser
+// and this one agree record for record on every .ray fixture and on the
+// error messages of malformed inputs; tests/test_ref_pins.py pins this
+// tokenizer against the reference's own, compiled unmodified.
+#include <dirent.h>
+
+#include <cctype>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <fstream>
+#include <list>
+#include <map>
+#include <memory>
+#include <sstream>
+#include <string>
+#include <vector>
+
+#include "../cs378hgraphics-raytracer_amd/csrc/host/scene_model.h"
+
+// material.h:272-276 (the oracle no longer links parser.cpp, which defines it
+// for the product)
+void rtxh::Material::setBools() {
+  auto zero = [](const MatParam& q) { return std::sqrt(rtm::dot(q.v, q.v)) == 0.0; };
+  refl = !zero(p[P_KR]);
+  trans = !zero(p[P_KT]);
+  recur = refl || trans;
+  spec = refl || !zero(p[P_KS]);
+  both = refl && trans;
+}
+
+namespace orcparse {
+
+using rtxh::dvec3;
+using rtxh::ParseError;
+
+// Token kinds (Token.h's SYMBOL, the ones the grammar uses)
+enum Kind {
+  K_EOF, K_SBT, K_IDENT, K_SCALAR, K_TRUE, K_FALSE, K_LPAREN, K_RPAREN, K_LBRACE, K_RBRACE, K_COMMA, K_EQUALS,
+  K_SEMI, K_CAMERA, K_AMBIENT_LIGHT, K_POINT_LIGHT, K_DIRECTIONAL_LIGHT, K_AREA_RECT, K_AREA_CIRC, K_SPOT,
+  K_CATT, K_LATT, K_QATT, K_SPHERE, K_BOX, K_SQUARE, K_CYLINDER, K_CONE, K_TRIMESH, K_POSITION, K_VIEWDIR,
+  K_UPDIR, K_ASPECT, K_FOV, K_COLOR, K_DIRECTION, K_CAPPED, K_HEIGHT, K_WIDTH, K_ANGLE, K_BOTTOM_RADIUS,
+  K_TOP_RADIUS, K_RADIUS, K_QUAT, K_POINTS, K_NORMALS, K_MATERIALS, K_FACES, K_GENNORMALS, K_TRANSLATE,
+  K_SCALE, K_ROTATE, K_TRANSFORM, K_MATERIAL, K_EMISSIVE, K_AMBIENT, K_SPECULAR, K_REFLECTIVE, K_DIFFUSE,
+  K_TRANSMISSIVE, K_SHININESS, K_INDEX, K_NAME, K_MAP, K_BUMP, K_GLOSS
+};
+
+// lookupReservedWord (Token.cpp:121-196)
+Kind reserved_or_ident(const std::string& w) {
+  static const std::map<std::string, Kind> table = [] {
+    std::map<std::string, Kind> t;
+    const std::pair<const char*, Kind> rows[] = {
+        {"ambient_light", K_AMBIENT_LIGHT}, {"ambient", K_AMBIENT}, {"aspectratio", K_ASPECT},
+        {"bottom_radius", K_BOTTOM_RADIUS}, {"box", K_BOX}, {"camera", K_CAMERA}, {"capped", K_CAPPED},
+        {"color", K_COLOR}, {"colour", K_COLOR}, {"cone", K_CONE}, {"constant_attenuation_coeff", K_CATT},
+        {"cylinder", K_CYLINDER}, {"diffuse", K_DIFFUSE}, {"direction", K_DIRECTION},
+        {"directional_light", K_DIRECTIONAL_LIGHT}, {"emissive", K_EMISSIVE}, {"faces", K_FACES},
+        {"false", K_FALSE}, {"fov", K_FOV}, {"gennormals", K_GENNORMALS}, {"height", K_HEIGHT},
+        {"index", K_INDEX}, {"linear_attenuation_coeff", K_LATT}, {"material", K_MATERIAL},
+        {"materials", K_MATERIALS}, {"map", K_MAP}, {"name", K_NAME}, {"normals", K_NORMALS},
+        {"point_light", K_POINT_LIGHT}, {"points", K_POINTS}, {"polymesh", K_TRIMESH},
+        {"position", K_POSITION}, {"quadratic_attenuation_coeff", K_QATT}, {"quaternian", K_QUAT},
+        {"reflective", K_REFLECTIVE}, {"rotate", K_ROTATE}, {"SBT-raytracer", K_SBT}, {"scale", K_SCALE},
+        {"shininess", K_SHININESS}, {"specular", K_SPECULAR}, {"sphere", K_SPHERE}, {"square", K_SQUARE},
+        {"top_radius", K_TOP_RADIUS}, {"transform", K_TRANSFORM}, {"translate", K_TRANSLATE},
+        {"transmissive", K_TRANSMISSIVE}, {"trimesh", K_TRIMESH}, {"true", K_TRUE}, {"updir", K_UPDIR},
+        {"viewdir", K_VIEWDIR}, {"bump", K_BUMP}, {"gloss", K_GLOSS}, {"angle", K_ANGLE}, {"width", K_WIDTH},
+        {"radius", K_RADIUS}, {"area_light_rect", K_AREA_RECT}, {"area_light_circ", K_AREA_CIRC},
+        {"spot_light", K_SPOT}};
+    for (const auto& r : rows) t[r.first] = r.second;
+    return t;
+  }();
+  const auto it = table.find(w);
+  return it == table.end() ? K_IDENT : it->second;
+}
+
+// getNameForToken (Token.cpp:9-92) for the kinds Read() is asked for
+const char* kind_name(Kind k) {
+  switch (k) {
+    case K_EOF: return "EOF";
+    case K_SBT: return "SBT-raytracer";
+    case K_IDENT: return "Identifier";
+    case K_SCALAR: return "Scalar";
+    case K_TRUE: return "true";
+    case K_FALSE: return "false";
+    case K_LPAREN: return "Left paren";
+    case K_RPAREN: return "Right paren";
+    case K_LBRACE: return "Left brace";
+    case K_RBRACE: return "Right brace";
+    case K_COMMA: return "Comma";
+    case K_EQUALS: return "Equals";
+    case K_SEMI: return "Semicolon";
+    case K_CAMERA: return "camera";
+    case K_MATERIAL: return "material";
+    case K_MATERIALS: return "materials";
+    case K_NORMALS: return "normals";
+    case K_FACES: return "faces";
+    case K_POINTS: return "points";
+    case K_GENNORMALS: return "Unknown token type";  // not in tokenNames
+    case K_NAME: return "name";
+    case K_TRIMESH: return "trimesh";
+    case K_TRANSLATE: return "translate";
+    case K_ROTATE: return "rotate";
+    case K_SCALE: return "scale";
+    case K_TRANSFORM: return "transform";
+    case K_SPHERE: return "sphere";
+    case K_BOX: return "box";
+    case K_SQUARE: return "square";
+    case K_CYLINDER: return "cylinder";
+    case K_CONE: return "cone";
+    case K_AMBIENT_LIGHT: return "ambient_light";
+    case K_POINT_LIGHT: return "point_light";
+    case K_DIRECTIONAL_LIGHT: return "directional_light";
+    case K_AREA_RECT: return "area_light_rect";
+    case K_AREA_CIRC: return "area_light_circ";
+    case K_SPOT: return "spot_light";
+    default: return "Unknown token type";
+  }
+}
+
+// Token::toString's name (getNameForToken) for the token dump: a reserved
+// word prints itself (its canonical spelling: "trimesh", "color"); fov and
+// gennormals, which tokenNames lacks, print their word too (as
+// oracle/ref_harness.cpp prints the reference's)
+std::string dump_name(Kind k) {
+  if (k <= K_SEMI) return kind_name(k);
+  static const std::map<Kind, std::string> words = [] {
+    std::map<Kind, std::string> m;
+    for (const char* w :
+         {"ambient_light", "ambient", "aspectratio", "bottom_radius", "box", "camera", "capped", "color", "cone",
+          "constant_attenuation_coeff", "cylinder", "diffuse", "direction", "directional_light", "emissive",
+          "faces", "fov", "gennormals", "height", "index", "linear_attenuation_coeff", "material", "materials",
+          "map", "name", "normals", "point_light", "points", "position", "quadratic_attenuation_coeff",
+          "quaternian", "reflective", "rotate", "scale", "shininess", "specular", "sphere", "square",
+          "top_radius", "transform", "translate", "transmissive", "trimesh", "updir", "viewdir", "bump", "gloss",
+          "angle", "width", "radius", "area_light_rect", "area_light_circ", "spot_light"})
+      m[reserved_or_ident(w)] = w;
+    return m;
+  }();
+  const auto it = words.find(k);
+  return it == words.end() ? "Unknown token type" : it->second;
+}
+
+struct Token {
+  Kind kind = K_EOF;
+  double value = 0.0;
+  std::string ident;
+};
+
+// Buffer + Tokenizer as the reference runs them: characters are pulled one
+// at a time from std::getline'd lines, tokens are scanned only when the
+// grammar asks for one (so a lexical error after the point where the
+// grammar fails is never reported, and the line number of an error is the
+// buffer's line at that moment).
+class Scanner {
+ public:
+  explicit Scanner(const std::string& text) : in_(text) {}
+
+  // Tokenizer::Get
+  Token get() {
+    if (have_back_) {
+      have_back_ = false;
+      return back_;
+    }
+    return scan();
+  }
+  // Tokenizer::Peek
+  const Token& peek() {
+    if (!have_back_) {
+      back_ = scan();
+      have_back_ = true;
+    }
+    return back_;
+  }
+  // Tokenizer::Read
+  Token read(Kind k) {
+    Token t = get();
+    if (t.kind != k) fail(std::string(kind_name(k)) + " expected");
+    return t;
+  }
+  // Tokenizer::CondRead
+  bool cond(Kind k) {
+    if (peek().kind != k) return false;
+    get();
+    return true;
+  }
+  // SyntaxErrorException's "Line N: syntax error: msg" (ParserException.cpp:5-19)
+  [[noreturn]] void fail(const std::string& msg) const {
+    throw ParseError("Line " + std::to_string(line_) + ": syntax error: " + msg);
+  }
+
+ private:
+  // Buffer::GetCh / GetLine (buffer.cpp:29-98)
+  char buffer_getch() {
+    if (!in_) return '\0';
+    if (!line_text_.empty() && pos_ != line_text_.size()) ++pos_;
+    while (pos_ == line_text_.size() || line_text_.empty()) {
+      std::getline(in_, line_text_);
+      line_text_.append("\n");
+      pos_ = 0;
+      ++line_;
+      if (!in_) return '\0';
+    }
+    return line_text_[pos_];
+  }
+  void next_ch() { ch_ = buffer_getch(); }
+  bool at_eof() const { return !in_; }
+
+  // SkipWhiteSpace (Tokenizer.cpp:136-187), the tail recursion as a loop
+  void skip_blank() {
+    for (;;) {
+      while (std::isspace(static_cast<unsigned char>(ch_))) next_ch();
+      if (ch_ != '/') return;
+      next_ch();
+      if (ch_ == '/') {
+        while (ch_ != '\n') next_ch();
+      } else if (ch_ == '*') {
+        const int first = line_;
+        for (;;) {
+          next_ch();
+          if (ch_ == '*') {
+            next_ch();
+            if (ch_ == '/') {
+              next_ch();
+              break;
+            }
+            if (at_eof()) fail("Unterminated comment in line " + std::to_string(first));
+          } else if (at_eof()) {
+            fail("Unterminated comment in line " + std::to_string(first));
+          }
+        }
+      } else {
+        fail(std::string("unexpected character: '") + ch_ + "'");
+      }
+    }
+  }
+
+  // GetNext (Tokenizer.cpp:70-127)
+  Token scan() {
+    skip_blank();
+    Token t;
+    if (at_eof()) return t;  // EOFSYM
+    const unsigned char c = static_cast<unsigned char>(ch_);
+    if (std::isalpha(c) || ch_ == '_') {  // GetIdent + SearchReserved
+      std::string w;
+      while (std::isalnum(static_cast<unsigned char>(ch_)) || ch_ == '_' || ch_ == '-') {
+        w.push_back(ch_);
+        next_ch();
+      }
+      t.kind = reserved_or_ident(w);
+      if (t.kind == K_IDENT) t.ident = w;
+    } else if (ch_ == '"') {  // GetQuotedIdent
+      next_ch();
+      std::string w;
+      while (ch_ != '"') {
+        if (ch_ == '\n') fail("Unterminated string constant");
+        w.push_back(ch_);
+        next_ch();
+      }
+      next_ch();
+      t.kind = K_IDENT;
+      t.ident = w;
+    } else if (std::isdigit(c) || ch_ == '-' || ch_ == '.') {  // GetScalar
+      std::string s;
+      while (std::isdigit(static_cast<unsigned char>(ch_)) || ch_ == '-' || ch_ == '.' || ch_ == 'e') {
+        s.push_back(ch_);
+        next_ch();
+      }
+      t.kind = K_SCALAR;
+      t.value = std::atof(s.c_str());
+    } else {  // GetPunct
+      static const char punct[] = "(){},=;";
+      static const Kind kinds[] = {K_LPAREN, K_RPAREN, K_LBRACE, K_RBRACE, K_COMMA, K_EQUALS, K_SEMI};
+      const char* hit = ch_ ? std::strchr(punct, ch_) : nullptr;
+      if (!hit) fail(std::string("unexpected character: '") + ch_ + "'");
+      t.kind = kinds[hit - punct];
+      next_ch();
+    }
+    return t;
+  }
+
+  std::istringstream in_;
+  std::string line_text_;
+  size_t pos_ = 0;
+  int line_ = 0;
+  char ch_ = ' ';  // Tokenizer ctor: CurrentCh = ' '
+  Token back_;
+  bool have_back_ = false;
+};
+
+[[noreturn]] void fatal(const std::string& msg) { throw ParseError("Parser: fatal exception " + msg); }
+
+// A node of the transform tree (TransformNode::createChild): its raw
+// operation and its parent; nullptr is transformRoot (identity).
+struct XNode {
+  const XNode* up;
+  rtxh::XformOp op;
+};
+
+class Grammar {
+ public:
+  Grammar(Scanner& s, std::string base) : s_(s), base_(std::move(base)) {}
+
+  // Parser::parseScene (Parser.cpp:26-95)
+  rtxh::SceneModel scene() {
+    out_.base_path = base_;
+    s_.read(K_SBT);
+    const Token ver = s_.read(K_SCALAR);
+    if (ver.value > 1.1) {
+      std::ostringstream m;
+      m << "SBT-raytracer version number " << ver.value << " too high; only able to parse v1.1 and below.";
+      fatal(m.str());
+    }
+    rtxh::Material current;  // new Material
+    for (;;) {
+      const Kind k = s_.peek().kind;
+      if (starts_transformable(k) || k == K_LBRACE) {
+        transformable(nullptr, current);
+      } else if (k == K_POINT_LIGHT || k == K_DIRECTIONAL_LIGHT || k == K_AREA_RECT || k == K_AREA_CIRC ||
+                 k == K_SPOT) {
+        out_.lights.push_back(light(k));
+      } else if (k == K_AMBIENT_LIGHT) {
+        ambient();
+      } else if (k == K_CAMERA) {
+        camera();
+      } else if (k == K_MATERIAL) {
+        current = material_expression(current);
+      } else if (k == K_SEMI) {
+        s_.read(K_SEMI);
+      } else if (k == K_EOF) {
+        return std::move(out_);
+      } else {
+        s_.fail("Expected: geometry, camera, or light information");
+      }
+    }
+  }
+
+ private:
+  static bool starts_transformable(Kind k) {
+    switch (k) {
+      case K_SPHERE: case K_BOX: case K_SQUARE: case K_CYLINDER: case K_CONE: case K_TRIMESH:
+      case K_TRANSLATE: case K_ROTATE: case K_SCALE: case K_TRANSFORM:
+        return true;
+      default:
+        return false;
+    }
+  }
+
+  // ---- values (Parser.cpp:1060-1186)
+  double scalar() { return s_.read(K_SCALAR).value; }
+  dvec3 vec3() {
+    s_.read(K_LPAREN);
+    double v[3];
+    for (int i = 0; i < 3; ++i) {
+      if (i) s_.read(K_COMMA);
+      v[i] = scalar();
+    }
+    s_.read(K_RPAREN);
+    return dvec3{v[0], v[1], v[2]};
+  }
+  std::array<double, 4> vec4() {
+    s_.read(K_LPAREN);
+    std::array<double, 4> v{};
+    for (int i = 0; i < 4; ++i) {
+      if (i) s_.read(K_COMMA);
+      v[size_t(i)] = scalar();
+    }
+    s_.read(K_RPAREN);
+    return v;
+  }
+  // "<attr> = <value> [;]": the attribute token itself is thrown away
+  void attr_eq() {
+    s_.get();
+    s_.read(K_EQUALS);
+  }
+  double scalar_expr() {
+    attr_eq();
+    const double v = scalar();
+    s_.cond(K_SEMI);
+    return v;
+  }
+  dvec3 vec3_expr() {
+    attr_eq();
+    const dvec3 v = vec3();
+    s_.cond(K_SEMI);
+    return v;
+  }
+  std::array<double, 4> vec4_expr() {
+    attr_eq();
+    const auto v = vec4();
+    s_.cond(K_SEMI);
+    return v;
+  }
+  bool bool_expr() {
+    attr_eq();
+    bool v = false;
+    if (s_.peek().kind == K_TRUE) {
+      s_.read(K_TRUE);
+      v = true;
+    } else if (s_.peek().kind == K_FALSE) {
+      s_.read(K_FALSE);
+    } else {
+      s_.fail("Expected boolean");
+    }
+    s_.cond(K_SEMI);
+    return v;
+  }
+  void ident_expr() {
+    attr_eq();
+    s_.read(K_IDENT);
+    s_.cond(K_SEMI);
+  }
+  // "( a, b, ... )", possibly empty
+  template <class F>
+  void paren_list(F item) {
+    s_.read(K_LPAREN);
+    if (s_.peek().kind != K_RPAREN) {
+      item();
+      while (s_.peek().kind != K_RPAREN) {
+        s_.read(K_COMMA);
+        item();
+      }
+    }
+    s_.read(K_RPAREN);
+  }
+
+  // ---- camera (Parser.cpp:97-154): the attributes in file order; viewdir +
+  // updir become one setLook at the block's end
+  void camera() {
+    s_.read(K_CAMERA);
+    s_.read(K_LBRACE);
+    bool got_view = false, got_up = false;
+    dvec3 view{0, 0, 0}, up{0, 0, 0};
+    auto push = [&](int kind, std::initializer_list<double> v) {
+      rtxh::CamOp op;
+      op.kind = kind;
+      int i = 0;
+      for (double x : v) op.v[i++] = x;
+      out_.camera.ops.push_back(op);
+    };
+    for (;;) {
+      switch (s_.peek().kind) {
+        case K_POSITION: out_.camera.eye = vec3_expr(); break;
+        case K_FOV: push(rtxh::CAM_FOV, {scalar_expr()}); break;
+        case K_QUAT: {
+          const auto q = vec4_expr();
+          push(rtxh::CAM_QUAT, {q[0], q[1], q[2], q[3]});
+          break;
+        }
+        case K_ASPECT: push(rtxh::CAM_ASPECT, {scalar_expr()}); break;
+        case K_VIEWDIR: view = vec3_expr(); got_view = true; break;
+        case K_UPDIR: up = vec3_expr(); got_up = true; break;
+        case K_RBRACE:
+          if (got_view && !got_up) s_.fail("Expected: 'updir'");
+          if (!got_view && got_up) s_.fail("Expected: 'viewdir'");
+          if (got_view) push(rtxh::CAM_LOOK, {view.x, view.y, view.z, up.x, up.y, up.z});
+          s_.read(K_RBRACE);
+          return;
+        default: s_.fail("Expected: camera attribute");
+      }
+    }
+  }
+
+  // ---- geometry (Parser.cpp:156-518)
+  void transformable(const XNode* at, const rtxh::Material& mat) {
+    const Kind k = s_.peek().kind;
+    if (starts_transformable(k)) geometry(at, mat);
+    else if (k == K_LBRACE) group(at, mat);
+    else s_.fail("Expected: transformable element");
+  }
+
+  void group(const XNode* at, const rtxh::Material& mat) {
+    s_.read(K_LBRACE);
+    for (;;) {
+      const Kind k = s_.peek().kind;
+      if (starts_transformable(k) || k == K_LBRACE) {
+        transformable(at, mat);  // (the group's own material is never set: see below)
+      } else if (k == K_RBRACE) {
+        s_.read(K_RBRACE);
+        return;
+      } else {
+        // a `material` inside a group is parsed, then the case falls through
+        // into the default branch (Parser.cpp:202-208)
+        if (k == K_MATERIAL) material_expression(mat);
+        s_.fail("Expected: '}' or geometry");
+      }
+    }
+  }
+
+  const XNode* child_of(const XNode* at, int kind, const double* v, int n) {
+    auto nd = std::make_unique<XNode>();
+    nd->up = at;
+    nd->op.kind = kind;
+    for (int i = 0; i < n; ++i) nd->op.v[i] = v[i];
+    nodes_.push_back(std::move(nd));
+    return nodes_.back().get();
+  }
+
+  void geometry(const XNode* at, const rtxh::Material& mat) {
+    switch (s_.peek().kind) {
+      case K_SPHERE: primitive(at, mat, K_SPHERE, rtxh::OBJ_SPHERE, "sphere"); return;
+      case K_BOX: primitive(at, mat, K_BOX, rtxh::OBJ_BOX, "box"); return;
+      case K_SQUARE: primitive(at, mat, K_SQUARE, rtxh::OBJ_SQUARE, "square"); return;
+      case K_CYLINDER: primitive(at, mat, K_CYLINDER, rtxh::OBJ_CYLINDER, "cylinder"); return;
+      case K_CONE: primitive(at, mat, K_CONE, rtxh::OBJ_CONE, "cone"); return;
+      case K_TRIMESH: trimesh(at, mat); return;
+      case K_TRANSLATE: {  // glm::translate(dvec3(x, y, z))
+        s_.read(K_TRANSLATE);
+        s_.read(K_LPAREN);
+        double v[3];
+        for (double& x : v) {
+          x = scalar();
+          s_.read(K_COMMA);
+        }
+        transformable(child_of(at, rtxh::XF_TRANSLATE, v, 3), mat);
+        break;
+      }
+      case K_ROTATE: {  // glm::rotate(w, dvec3(x, y, z))
+        s_.read(K_ROTATE);
+        s_.read(K_LPAREN);
+        double v[4];
+        for (double& x : v) {
+          x = scalar();
+          s_.read(K_COMMA);
+        }
+        transformable(child_of(at, rtxh::XF_ROTATE, v, 4), mat);
+        break;
+      }
+      case K_SCALE: {  // scale(s, ...) or scale(x, y, z, ...)
+        s_.read(K_SCALE);
+        s_.read(K_LPAREN);
+        double v[3];
+        v[0] = scalar();
+        s_.read(K_COMMA);
+        if (s_.peek().kind == K_SCALAR) {
+          v[1] = scalar();
+          s_.read(K_COMMA);
+          v[2] = scalar();
+          s_.read(K_COMMA);
+        } else {
+          v[1] = v[2] = v[0];
+        }
+        transformable(child_of(at, rtxh::XF_SCALE, v, 3), mat);
+        break;
+      }
+      case K_TRANSFORM: {  // glm::transpose(dmat4x4(row1, .., row4)): rows as written
+        s_.read(K_TRANSFORM);
+        s_.read(K_LPAREN);
+        double v[16];
+        for (int r = 0; r < 4; ++r) {
+          const auto row = vec4();
+          for (int c = 0; c < 4; ++c) v[r * 4 + c] = row[size_t(c)];
+          s_.read(K_COMMA);
+        }
+        transformable(child_of(at, rtxh::XF_MATRIX, v, 16), mat);
+        break;
+      }
+      default: fatal("Unrecognized geometry type.");
+    }
+    s_.read(K_RPAREN);
+    s_.cond(K_SEMI);
+  }
+
+  static std::vector<rtxh::XformOp> chain_to(const XNode* n) {
+    std::vector<rtxh::XformOp> rev;
+    for (; n; n = n->up) rev.push_back(n->op);
+    return std::vector<rtxh::XformOp>(rev.rbegin(), rev.rend());
+  }
+
+  // Scene::add of a MaterialSceneObject: the object owns its material copy
+  void add_object(rtxh::Object o, const rtxh::Material& m) {
+    o.material = static_cast<int>(out_.materials.size());
+    out_.materials.push_back(m);
+    out_.objects.push_back(std::move(o));
+  }
+
+  // sphere / box / square / cylinder / cone blocks (Parser.cpp:348-518)
+  void primitive(const XNode* at, const rtxh::Material& mat, Kind kw, int type, const char* what) {
+    s_.read(kw);
+    s_.read(K_LBRACE);
+    std::unique_ptr<rtxh::Material> own;  // newMat (the last material attribute wins)
+    double bottom = 1.0, top = 0.0, height = 1.0;
+    bool capped = true;  // parseCone: capped by default
+    for (;;) {
+      const Kind k = s_.peek().kind;
+      if (k == K_MATERIAL) {
+        own = std::make_unique<rtxh::Material>(material_expression(mat));
+      } else if (k == K_NAME) {
+        ident_expr();
+      } else if (type == rtxh::OBJ_CONE && k == K_CAPPED) {
+        capped = bool_expr();
+      } else if (type == rtxh::OBJ_CONE && k == K_BOTTOM_RADIUS) {
+        bottom = scalar_expr();
+      } else if (type == rtxh::OBJ_CONE && k == K_TOP_RADIUS) {
+        top = scalar_expr();
+      } else if (type == rtxh::OBJ_CONE && k == K_HEIGHT) {
+        height = scalar_expr();
+      } else if (k == K_RBRACE) {
+        s_.read(K_RBRACE);
+        rtxh::Object o = rtxh::Object();
+        o.type = type;
+        o.chain = chain_to(at);
+        if (type == rtxh::OBJ_CONE) cone_shape(o, height, bottom, top, capped);
+        add_object(std::move(o), own ? *own : mat);
+        return;
+      } else {
+        s_.fail(std::string("Expected: ") + what + " attributes");
+      }
+    }
+  }
+
+  // Cone::Cone (Cone.h:11-37)
+  static void cone_shape(rtxh::Object& o, double h, double br, double tr, bool cap) {
+    double b_radius = (br < 0.0f) ? -br : br;
+    double t_radius = (tr < 0.0f) ? -tr : tr;
+    if (b_radius < 0.0001) b_radius = 0.0001;
+    if (t_radius < 0.0001) t_radius = 0.0001;
+    double beta = (t_radius - b_radius) / h;
+    if (std::fabs(beta) < 0.001) beta = 0.001;
+    double gamma = beta < 0.0 ? t_radius / beta : b_radius / beta;
+    const double beta_squared = beta * beta;
+    if (gamma < 0.0) gamma = gamma - h;
+    o.cone_h = h;
+    o.cone_br = b_radius;
+    o.cone_tr = t_radius;
+    o.cone_b2 = beta_squared;
+    o.cone_g = gamma;
+    o.cone_capped = cap;
+  }
+
+  // Parser::parseTrimesh (Parser.cpp:520-653) + Trimesh::addFace /
+  // doubleCheck (trimesh.cpp:38-67)
+  void trimesh(const XNode* at, const rtxh::Material& mat) {
+    rtxh::Material mesh_mat = mat;  // new Trimesh(scene, new Material(mat), transform)
+    s_.read(K_TRIMESH);
+    s_.read(K_LBRACE);
+    bool gen = false;
+    std::list<dvec3> fan;  // faces as the parser collects them (doubles)
+    rtxh::Mesh me;
+    std::vector<rtxh::Material> vm;
+    auto list_attr = [&](Kind k, auto item) {
+      s_.read(k);
+      s_.read(K_EQUALS);
+      paren_list(item);
+      s_.read(K_SEMI);
+    };
+    for (;;) {
+      switch (s_.peek().kind) {
+        case K_GENNORMALS:
+          s_.read(K_GENNORMALS);
+          s_.read(K_SEMI);
+          gen = true;
+          break;
+        case K_MATERIAL: mesh_mat = material_expression(mat); break;  // setMaterial(...(scene, mat))
+        case K_NAME: ident_expr(); break;
+        case K_MATERIALS: list_attr(K_MATERIALS, [&] { vm.push_back(material(mesh_mat)); }); break;
+        case K_NORMALS: list_attr(K_NORMALS, [&] { me.raw_normals.push_back(vec3()); }); break;
+        case K_FACES: list_attr(K_FACES, [&] { faces(fan); }); break;
+        case K_POINTS: list_attr(K_POINTS, [&] { me.verts.push_back(vec3()); }); break;
+        case K_RBRACE: {
+          s_.read(K_RBRACE);
+          const int nv = static_cast<int>(me.verts.size());
+          for (const dvec3& f : fan) {
+            // addFace(int, int, int): the doubles truncate; indices past the
+            // vertex list fail.  (A negative index is undefined behaviour in
+            // the reference — vertices[-1] — and rejected here, decision U25.)
+            const int a = static_cast<int>(f.x), b = static_cast<int>(f.y), c = static_cast<int>(f.z);
+            if (a >= nv || b >= nv || c >= nv || a < 0 || b < 0 || c < 0) {
+              std::ostringstream m;
+              m << "Bad face in trimesh: (" << f.x << ", " << f.y << ", " << f.z << ")";
+              fatal(m.str());
+            }
+            me.raw_faces.push_back({a, b, c});
+          }
+          me.gennormals = gen;
+          // doubleCheck after generateNormals (which sizes the normals to
+          // the vertex count)
+          if (!vm.empty() && vm.size() != me.verts.size()) fatal("Bad Trimesh: Wrong number of materials.");
+          const size_t nn = gen ? me.verts.size() : me.raw_normals.size();
+          if (nn != 0 && nn != me.verts.size()) fatal("Bad Trimesh: Wrong number of normals.");
+          me.vmats = std::move(vm);
+          rtxh::Object o = rtxh::Object();
+          o.type = rtxh::OBJ_TRIMESH;
+          o.chain = chain_to(at);
+          o.mesh = static_cast<int>(out_.meshes.size());
+          out_.meshes.push_back(std::move(me));
+          add_object(std::move(o), mesh_mat);
+          return;
+        }
+        default: s_.fail("Expected: trimesh attributes");
+      }
+    }
+  }
+
+  // Parser::parseFaces (Parser.cpp:655-671): a fan over the polygon
+  void faces(std::list<dvec3>& fan) {
+    std::vector<double> pts;
+    paren_list([&] { pts.push_back(scalar()); });
+    if (pts.size() < 3) s_.fail("Faces must have at least 3 vertices.");
+    for (size_t i = 2; i < pts.size(); ++i) fan.push_back(dvec3{pts[0], pts[i - 1], pts[i]});
+  }
+
+  // ---- lights (Parser.cpp:673-1058)
+  void ambient() {
+    s_.read(K_AMBIENT_LIGHT);
+    s_.read(K_LBRACE);
+    if (s_.peek().kind != K_COLOR) s_.fail("Expected color attribute");
+    out_.ambient = out_.ambient + vec3_expr();
+    s_.read(K_RBRACE);
+  }
+
+  rtxh::Light light(Kind kw) {
+    // which attributes each light kind takes, and the order of its
+    // "Expected: ..." checks at the closing brace
+    struct Spec {
+      int type;
+      bool radius, angle, rect, atten;
+    };
+    Spec sp{};
+    switch (kw) {
+      case K_POINT_LIGHT: sp = {rtxh::L_POINT, false, false, false, true}; break;
+      case K_DIRECTIONAL_LIGHT: sp = {rtxh::L_DIRECTIONAL, false, false, false, false}; break;
+      case K_AREA_RECT: sp = {rtxh::L_AREA_RECT, false, false, true, true}; break;
+      case K_AREA_CIRC: sp = {rtxh::L_AREA_CIRC, true, false, false, true}; break;
+      default: sp = {rtxh::L_SPOT, true, true, false, true}; break;
+    }
+    const bool point = kw == K_POINT_LIGHT, dirl = kw == K_DIRECTIONAL_LIGHT;
+    rtxh::Light L;
+    L.type = sp.type;
+    float catt = 0.0f, latt = 0.0f, qatt = 1.0f;  // "the 'default' system"
+    std::map<Kind, bool> seen;
+    auto once = [&](Kind k, const char* name) {
+      if (seen[k]) s_.fail(std::string("Repeated '") + name + "' attribute");
+      seen[k] = true;
+    };
+    const char* other = dirl ? "expecting 'position' or 'color' attribute"
+                             : "expecting 'position' or 'color' attribute, or 'constant_attenuation_coeff', "
+                               "'linear_attenuation_coeff', or 'quadratic_attenuation_coeff'";
+    s_.read(kw);
+    s_.read(K_LBRACE);
+    for (;;) {
+      const Kind k = s_.peek().kind;
+      if (k == K_POSITION && !dirl) {
+        once(k, "position");
+        L.pos = vec3_expr();
+      } else if (k == K_DIRECTION && !point) {
+        once(k, "direction");
+        L.raw_dir = vec3_expr();
+      } else if (k == K_COLOR) {
+        once(k, "color");
+        L.color = vec3_expr();
+      } else if (k == K_RADIUS && sp.radius) {
+        once(k, "radius");
+        L.radius = scalar_expr();
+      } else if (k == K_ANGLE && sp.angle) {
+        once(k, "angle");
+        L.angle = scalar_expr();
+      } else if (k == K_WIDTH && sp.rect) {
+        once(k, "width");
+        L.width = scalar_expr();
+      } else if (k == K_HEIGHT && sp.rect) {
+        once(k, "height");
+        L.height = scalar_expr();
+      } else if (k == K_UPDIR && sp.rect) {
+        once(k, "updir");
+        L.raw_up = vec3_expr();
+      } else if (sp.atten && (k == K_CATT || k == K_LATT || k == K_QATT)) {
+        // stored as float (light.h:86-88)
+        const float v = static_cast<float>(scalar_expr());
+        (k == K_CATT ? catt : k == K_LATT ? latt : qatt) = v;
+      } else if (k == K_RBRACE) {
+        // the closing checks in each parse*Light's order
+        std::vector<std::pair<Kind, const char*>> need;
+        if (sp.rect) need = {{K_WIDTH, "width"}, {K_HEIGHT, "height"}, {K_UPDIR, "updir"}};
+        if (sp.angle) need.push_back({K_ANGLE, "angle"});
+        if (sp.radius) need.push_back({K_RADIUS, "radius"});
+        need.push_back({K_COLOR, "color"});
+        // (parseDirectionalLight reports a missing direction as 'position')
+        need.push_back({dirl ? K_DIRECTION : K_POSITION, "position"});
+        if (!point && !dirl) need.push_back({K_DIRECTION, "direction"});
+        for (const auto& n : need)
+          if (!seen[n.first]) s_.fail(std::string("Expected: '") + n.second + "'");
+        s_.read(K_RBRACE);
+        L.c = catt;
+        L.l = latt;
+        L.q = qatt;
+        return L;
+      } else {
+        s_.fail(other);
+      }
+    }
+  }
+
+  // ---- materials (Parser.cpp:1095-1308)
+  rtxh::Material material_expression(const rtxh::Material& parent) {
+    s_.read(K_MATERIAL);
+    s_.read(K_EQUALS);
+    rtxh::Material m = material(parent);
+    s_.cond(K_SEMI);
+    return m;
+  }
+
+  rtxh::Material material(const rtxh::Material& parent) {
+    if (s_.peek().kind == K_IDENT) {
+      // new Material(materials[name]): the identifier is not consumed (the
+      // caller trips over it); an unknown name yields a default Material
+      const auto it = named_.find(s_.peek().ident);
+      return it == named_.end() ? rtxh::Material() : it->second;
+    }
+    s_.read(K_LBRACE);
+    rtxh::Material m = parent;  // new Material(parent)
+    std::string name;
+    for (;;) {
+      const Kind k = s_.peek().kind;
+      switch (k) {
+        case K_EMISSIVE: m.p[rtxh::P_KE] = vec3_param(); break;
+        case K_AMBIENT: m.p[rtxh::P_KA] = vec3_param(); break;
+        case K_SPECULAR: m.p[rtxh::P_KS] = vec3_param(); break;  // setSpecular(MaterialParameter): no setBools
+        case K_DIFFUSE: m.p[rtxh::P_KD] = vec3_param(); break;
+        case K_REFLECTIVE:
+          m.p[rtxh::P_KR] = vec3_param();
+          m.setBools();
+          break;
+        case K_TRANSMISSIVE:
+          m.p[rtxh::P_KT] = vec3_param();
+          m.setBools();
+          break;
+        case K_INDEX: m.p[rtxh::P_INDEX] = scalar_param(); break;
+        case K_SHININESS: m.p[rtxh::P_SHININESS] = scalar_param(); break;
+        case K_GLOSS: m.p[rtxh::P_GLOSS] = scalar_param(); break;
+        case K_BUMP: m.p[rtxh::P_BUMP] = vec3_param(); break;
+        case K_NAME:
+          s_.read(K_NAME);
+          name = s_.read(K_IDENT).ident;
+          s_.read(K_SEMI);
+          break;
+        case K_RBRACE:
+          s_.read(K_RBRACE);
+          if (!name.empty()) {
+            if (named_.count(name)) s_.fail("Redefinition of material '" + name + "'.");
+            named_[name] = m;
+          }
+          return m;
+        default: s_.fail("Expected: material attribute");
+      }
+    }
+  }
+
+  // parseVec3dMaterialParameter: map(file) relative to the scene's directory
+  rtxh::MatParam vec3_param() {
+    attr_eq();
+    rtxh::MatParam q;
+    if (s_.cond(K_MAP)) {
+      s_.read(K_LPAREN);
+      const std::string file = base_ + "/" + s_.read(K_IDENT).ident;
+      s_.read(K_RPAREN);
+      s_.cond(K_SEMI);
+      q.tex = texture(file);  // MaterialParameter(TextureMap*): _value stays (0, 0, 0)
+    } else {
+      q.v = vec3();
+      s_.cond(K_SEMI);
+    }
+    return q;
+  }
+  // parseScalarMaterialParameter: map(file) taken as written (no base path)
+  rtxh::MatParam scalar_param() {
+    attr_eq();
+    rtxh::MatParam q;
+    if (s_.cond(K_MAP)) {
+      s_.read(K_LPAREN);
+      const std::string file = s_.read(K_IDENT).ident;
+      s_.read(K_RPAREN);
+      s_.cond(K_SEMI);
+      q.tex = texture(file);
+    } else {
+      const double x = scalar();
+      q.v = dvec3{x, x, x};  // MaterialParameter(double)
+      s_.cond(K_SEMI);
+    }
+    return q;
+  }
+
+  // Scene::getTexture (scene.cpp:199-206) + TextureMap ctor (material.cpp:70-81)
+  int texture(const std::string& file) {
+    const auto it = tex_ids_.find(file);
+    if (it != tex_ids_.end()) return it->second;
+    rtxh::Texture t;
+    t.path = file;
+    t.data = rtxh::read_image(file, t.width, t.height);
+    if (t.data.empty())
+      throw ParseError("Texture mapping exception: Unable to load texture map '" + file + "'.");
+    const int id = static_cast<int>(out_.textures.size());
+    out_.textures.push_back(std::move(t));
+    tex_ids_[file] = id;
+    return id;
+  }
+
+  Scanner& s_;
+  std::string base_;
+  rtxh::SceneModel out_;
+  std::map<std::string, rtxh::Material> named_;
+  std::map<std::string, int> tex_ids_;
+  std::vector<std::unique_ptr<XNode>> nodes_;
+};
+
+}  // namespace orcparse
+
+// RayTracer::loadScene's parse (RayTracer.cpp:196-240): the scene file's
+// directory is the base path of its texture maps
+rtxh::SceneModel oracle_parse_ray_file(const std::string& path) {
+  std::ifstream f(path);
+  if (!f) throw rtxh::ParseError("Error: couldn't read scene file " + path);
+  std::stringstream all;
+  all << f.rdbuf();
+  const size_t cut = path.find_last_of("\\/");
+  const std::string base = cut == std::string::npos ? std::string(".") : path.substr(0, cut);
+  orcparse::Scanner sc(all.str());
+  orcparse::Grammar g(sc, base);
+  return g.scene();
+}
+
+// The scanner's token stream, one token per line, in the format of
+// rtx_host_tokens (tests/test_ref_pins.py compares it with the reference
+// tokenizer's).
+std::string oracle_token_dump(const std::string& text) {
+  std::ostringstream o;
+  try {
+    orcparse::Scanner sc(text);
+    for (;;) {
+      const orcparse::Token t = sc.get();
+      o << orcparse::dump_name(t.kind);
+      if (t.kind == orcparse::K_IDENT) o << '\t' << t.ident;
+      if (t.kind == orcparse::K_SCALAR) {
+        char b[40];
+        std::snprintf(b, sizeof(b), "%.17g", t.value);
+        o << '\t' << b;
+      }
+      o << '\n';
+      if (t.kind == orcparse::K_EOF) break;
+    }
+  } catch (const rtxh::ParseError&) {
+    o << "ERROR\n";
+  }
+  return o.str();
+}
+
+// TraceUI::matchCubemapFiles + smartLoadCubemap (TraceUI.cc:87-167): the six
+// faces +x, -x, +y, -y, +z, -z of the directory of `file`
+bool oracle_load_cubemap(const std::string& file, rtxh::Texture faces[6], std::string& err) {
+  static const char* const want[6][2] = {{"pos", "x"}, {"neg", "x"}, {"pos", "y"},
+                                         {"neg", "y"}, {"pos", "z"}, {"neg", "z"}};
+  const std::string dir = file.substr(0, file.find_last_of('/'));
+  DIR* d = opendir(dir.c_str());
+  if (!d) {
+    err = "Couldn't open the directory " + dir;
+    return false;
+  }
+  std::string got[6];
+  int n = 0;
+  for (struct dirent* e = readdir(d); e && n < 6; e = readdir(d)) {
+    const std::string name(e->d_name);
+    for (int i = 0; i < 6; ++i) {
+      // find_first_of: ANY character of "pos" / "neg", then the axis letter after it
+      const size_t p0 = name.find_first_of(want[i][0]);
+      if (p0 == std::string::npos || name.find_first_of(want[i][1], p0) == std::string::npos) continue;
+      if (!got[i].empty()) {
+        closedir(d);
+        err = std::string(want[i][0]) + want[i][1] + " matches " + got[i] + " and " + name +
+              ", stop smartload to avoid confliction";
+        return false;
+      }
+      got[i] = name;
+      ++n;
+      break;
+    }
+  }
+  closedir(d);
+  if (n != 6) {
+    err = "Cannot locate all six cubemap files";
+    return false;
+  }
+  for (int i = 0; i < 6; ++i) {
+    rtxh::Texture t;
+    t.path = dir + "/" + got[i];
+    t.data = rtxh::read_image(t.path, t.width, t.height);
+    if (t.data.empty()) {
+      err = "Unable to load texture map '" + t.path + "'.";
+      return false;
+    }
+    faces[i] = std::move(t);
+  }
+  return true;
+}

@@ -61,12 +61,20 @@ def _ray_fixtures():
     return out
 
 
+@pytest.fixture(scope="module")
+def orc_tokens(pkg, orc):
+    orc.lib(pkg)
+    return orc.lib(pkg).oracle_tokens
+
+
 @pytest.mark.parametrize("path", _ray_fixtures(), ids=lambda p: os.path.relpath(p, ROOT))
-def test_token_stream_matches_reference(ref, host, path):
+def test_token_stream_matches_reference(ref, host, orc_tokens, path):
+    """Both tokenizers, the product's (parser.cpp) and the checker's own
+    (oracle/parse_restated.cpp), against the reference's."""
     want = _tokens(ref.ref_tokens, path)
-    got = _tokens(host.rtx_host_tokens, path)
     assert want[-1] == "EOF"
-    assert got == want
+    assert _tokens(host.rtx_host_tokens, path) == want
+    assert _tokens(orc_tokens, path) == want
 
 
 # edge cases of the scanner: comments, quoted identifiers, aliases, scalars
@@ -88,12 +96,12 @@ EDGE_TEXTS = {
 
 
 @pytest.mark.parametrize("name", list(EDGE_TEXTS))
-def test_token_edge_cases_match_reference(ref, host, tmp_path, name):
+def test_token_edge_cases_match_reference(ref, host, orc_tokens, tmp_path, name):
     p = tmp_path / f"{name}.ray"
     p.write_bytes(EDGE_TEXTS[name].encode())
     want = _tokens(ref.ref_tokens, str(p))
-    got = _tokens(host.rtx_host_tokens, str(p))
-    assert got == want
+    assert _tokens(host.rtx_host_tokens, str(p)) == want
+    assert _tokens(orc_tokens, str(p)) == want
 
 
 def _read(host, path):
