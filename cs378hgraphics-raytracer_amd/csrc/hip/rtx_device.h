@@ -21,9 +21,22 @@
 #include "../common/rt_math.h"
 #include "rtx.h"
 
-// RtxObject.pad slot the device upload fills: the object is opaque to
-// shadow walks (rtx_scene_create; walk_hit)
+// RtxObject.pad slots the device copy of an object carries:
+//   WOPAQUE   the object is opaque to shadow walks (rtx_scene_create; walk_hit)
+//   FACE_OFF, NODE_OFF, VERT_OFF, MFLAGS: a trimesh's RtxMesh fields
+//             (face_off, node_off, vert_off; MFLAGS bit 0 node_count > 0,
+//             bit 1 has_normals, bit 2 has_vmats), so the traversal's mesh
+//             entry and resolve_hit read them with the object record instead
+//             of a dependent load of the mesh record (augment_objects,
+//             rtx_traverse.h)
 #define RTX_OBJ_WOPAQUE 0
+#define RTX_OBJ_FACE_OFF 1
+#define RTX_OBJ_NODE_OFF 2
+#define RTX_OBJ_VERT_OFF 3
+#define RTX_OBJ_MFLAGS 4
+#define RTX_MESH_TREE 1
+#define RTX_MESH_NORMALS 2
+#define RTX_MESH_VMATS 4
 
 namespace rtxd {
 
@@ -89,6 +102,14 @@ struct DevRoot {
   int32_t pad[3];
 };                     // 64 bytes
 
+// Per face in traversal-tree leaf order (tfaces): its reference rank (index
+// in faces / fids) and its reference leaf node (global index in mnodes) —
+// loaded with the face, so leaf_ok needs one dependent load (the leaf box),
+// not three (rank, face ids, leaf box).
+struct TMeta {
+  int32_t rank, leaf;
+};
+
 struct DevScene {
   const DevNode4* snode4;  // scene BVH records
   const DevNode4* mnode4;  // all mesh BVHs' records (global indices)
@@ -105,6 +126,7 @@ struct DevScene {
   const RtxFaceIds* fids;
   const RtxFace* tfaces;   // faces in traversal-tree leaf order (per mesh)
   const int32_t* trank;    // reference rank (index in faces) of each tfaces entry
+  const TMeta* tmeta;      // rank + reference leaf node of each tfaces entry
   const double* vnormals;
   const RtxVertexMaterial* vmats;
   const RtxLight* lights;

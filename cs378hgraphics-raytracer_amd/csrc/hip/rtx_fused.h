@@ -246,8 +246,7 @@ __device__ __forceinline__ void shade_hit(LaneRef& LR, const DevScene& S, const 
       hr->scene_leaf = o.leaf;
       hr->t = bt;
       if (o.type == RTX_OBJ_TRIMESH) {
-        const RtxMesh me = S.meshes[o.mesh];
-        const RtxFaceIds fi = S.fids[me.face_off + bsub];
+        const RtxFaceIds fi = S.fids[o.pad[RTX_OBJ_FACE_OFF] + bsub];
         hr->face = fi.orig_id;
         hr->mesh_leaf = fi.leaf;
       }

@@ -206,23 +206,25 @@ __device__ RTX_RESOLVE_ATTR HitRef resolve_hit(const DevScene& S, const dvec3& P
     *rec_mleaf = -1;
   }
   if (o.type == RTX_OBJ_TRIMESH) {
-    const RtxMesh me = S.meshes[o.mesh];
-    const RtxFace F = S.faces[me.face_off + sub];
-    const RtxFaceIds fi = S.fids[me.face_off + sub];
+    // the mesh's fields ride in the object record (augment_objects)
+    const int face_off = o.pad[RTX_OBJ_FACE_OFF], vert_off = o.pad[RTX_OBJ_VERT_OFF];
+    const int mflags = o.pad[RTX_OBJ_MFLAGS];
+    const RtxFace F = S.faces[face_off + sub];
+    const RtxFaceIds fi = S.fids[face_off + sub];
     double tl = 0.0;
     tri_hit(F, pos, dir, RTX_INF, tl);
     const dvec3 bary = tri_bary(F, pos, dir, tl);
-    if (me.has_normals) {  // trimesh.cpp:166-172
-      const dvec3 n0 = ld3(S.vnormals + size_t(me.vert_off + fi.vi[0]) * 3);
-      const dvec3 n1 = ld3(S.vnormals + size_t(me.vert_off + fi.vi[1]) * 3);
-      const dvec3 n2 = ld3(S.vnormals + size_t(me.vert_off + fi.vi[2]) * 3);
+    if (mflags & RTX_MESH_NORMALS) {  // trimesh.cpp:166-172
+      const dvec3 n0 = ld3(S.vnormals + size_t(vert_off + fi.vi[0]) * 3);
+      const dvec3 n1 = ld3(S.vnormals + size_t(vert_off + fi.vi[1]) * 3);
+      const dvec3 n2 = ld3(S.vnormals + size_t(vert_off + fi.vi[2]) * 3);
       const double mm[9] = {n0.x, n0.y, n0.z, n1.x, n1.y, n1.z, n2.x, n2.y, n2.z};
       nl = rtm::normalize(rtm::mat3_mul(mm, bary));
     } else {
       nl = ld3(F.n);
     }
     r.bary = bary;
-    r.vm_off = me.has_vmats ? me.vert_off : -1;
+    r.vm_off = (mflags & RTX_MESH_VMATS) ? vert_off : -1;
     r.vi0 = fi.vi[0];
     r.vi1 = fi.vi[1];
     r.vi2 = fi.vi[2];
@@ -956,8 +958,7 @@ __device__ __forceinline__ void advance_lane(LaneRef& LR, const DevScene& S, con
             hr->scene_leaf = o.leaf;
             hr->t = LR.bt();
             if (o.type == RTX_OBJ_TRIMESH) {
-              const RtxMesh me = S.meshes[o.mesh];
-              const RtxFaceIds fi = S.fids[me.face_off + LR.bsub()];
+              const RtxFaceIds fi = S.fids[o.pad[RTX_OBJ_FACE_OFF] + LR.bsub()];
               hr->face = fi.orig_id;
               hr->mesh_leaf = fi.leaf;
             }
@@ -1810,7 +1811,7 @@ __device__ __noinline__ bool shadow_blocks(const DevScene* __restrict__ Sg, cons
                                            int sb) {
   const DevScene& S = *Sg;
   const RtxObject& o = S.objs[oi];
-  const bool vmats = o.type == RTX_OBJ_TRIMESH && S.meshes[o.mesh].has_vmats;  // flags 0 (decision U2)
+  const bool vmats = o.type == RTX_OBJ_TRIMESH && (o.pad[RTX_OBJ_MFLAGS] & RTX_MESH_VMATS);  // flags 0 (decision U2)
   if (!vmats && (S.mats[o.material].flags & RTX_MF_TRANS)) return false;
   const HitRef R = resolve_hit(S, P, D, oi, sb, nullptr, nullptr);
   return !(rtm::dot(R.N, D) > 0);
@@ -2568,11 +2569,13 @@ rtx_status rtx_scene_create(int device, const RtxSceneDesc* d, void** out) {
 #define UP(src, n, dst) \
   if ((rc = upload(*st, src, size_t(n), &dst)) != RTX_OK) { rtx_scene_destroy(st); return rc; }
   UP(d->scene_nodes, d->n_scene_nodes, S.snodes);
-  // objects as the loader flattened them, plus pad[RTX_OBJ_WOPAQUE]: 1 when
-  // a shadow walk that hits the object cannot carry light past it — its
-  // material is not transmissive and its kt a constant (0, 0, 0), with no
-  // per-vertex materials (walk_hit's shortcut, rtx_fused.h)
-  std::vector<RtxObject> objs(d->objects, d->objects + d->n_objects);
+  // objects as the loader flattened them, with their mesh fields in pad
+  // (augment_objects) and pad[RTX_OBJ_WOPAQUE]: 1 when a shadow walk that
+  // hits the object cannot carry light past it — its material is not
+  // transmissive and its kt a constant (0, 0, 0), with no per-vertex
+  // materials (walk_hit's shortcut, rtx_fused.h)
+  std::vector<RtxObject> objs;
+  augment_objects(d, objs);
   for (RtxObject& o : objs) {
     bool op = o.material >= 0 && o.material < d->n_materials;
     if (op) {
@@ -2617,6 +2620,7 @@ rtx_status rtx_scene_create(int device, const RtxSceneDesc* d, void** out) {
     UP(tt.mroots.data(), tt.mroots.size(), S.mroots);
     UP(tt.tfaces.data(), tt.tfaces.size(), S.tfaces);
     UP(tt.trank.data(), tt.trank.size(), S.trank);
+    UP(tt.tmeta.data(), tt.tmeta.size(), S.tmeta);
 #undef UP
   }
   for (int k = 0; k < 6; ++k) {

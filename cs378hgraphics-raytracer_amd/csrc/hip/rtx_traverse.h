@@ -84,8 +84,9 @@ struct NoBlocker {
 // A face hit counts only if its mesh-BVH leaf box passes the exact slab test
 // in the mesh's local frame (KdTree::intersectList collects the items of hit
 // leaves, kdTree.h:100-117): the walk's internal tests are conservative.
-RT_HD bool leaf_ok(const Trav& T, const DevScene& S, int f) {
-  const RtxNode& lf = S.mnodes[T.mnoff + S.fids[T.mfoff + f].leaf];
+// `leaf`: the face's reference leaf node (TMeta.leaf, a global mnodes index).
+RT_HD bool leaf_ok(const Trav& T, const DevScene& S, int leaf) {
+  const RtxNode& lf = S.mnodes[leaf];
   double a, b;
   return slab(lf.bmin, lf.bmax, T.lp, T.ld, a, b);
 }
@@ -287,7 +288,7 @@ RT_HD bool trav_step(Trav& T, const DevScene& S, int* __restrict__ stk, const in
       const double ln = rtm::length(dir);
       dir = rtm::normalize(dir);
       if (o.type == RTX_OBJ_TRIMESH) {
-        if (S.meshes[o.mesh].node_count > 0) {
+        if (o.pad[RTX_OBJ_MFLAGS] & RTX_MESH_TREE) {
           const DevRoot& mr = S.mroots[o.mesh];
           const RayInv mri = ray_inv(dir);
           if (STATS) C.nodes++;
@@ -301,8 +302,8 @@ RT_HD bool trav_step(Trav& T, const DevScene& S, int* __restrict__ stk, const in
             T.len = ln;
             T.moi = oi;
             T.mbase = sp;
-            T.mfoff = S.meshes[o.mesh].face_off;
-            T.mnoff = S.meshes[o.mesh].node_off;
+            T.mfoff = o.pad[RTX_OBJ_FACE_OFF];
+            T.mnoff = o.pad[RTX_OBJ_NODE_OFF];
             ref = mr.ref;
             T.mhave = false;
             T.mbest = RTX_INF;
@@ -493,17 +494,23 @@ RT_HD bool trav_step(Trav& T, const DevScene& S, int* __restrict__ stk, const in
     for (int f = f0; f < f1; ++f) {
       if (STATS) C.tris++;
       double tf;
-      if (tri_hit(S.tfaces[T.mfoff + f], T.lp, T.ld, tcap, tf)) {
-        const int rk = S.trank[T.mfoff + f];  // the face's reference rank (ties, answer)
+      // the face's reference rank (ties, answer) and leaf, issued before the
+      // face's own loads so they arrive in the same burst
+      const TMeta meta = S.tmeta[T.mfoff + f];
+      const bool hit = tri_hit(S.tfaces[T.mfoff + f], T.lp, T.ld, tcap, tf);
+      pin(meta.rank);
+      pin(meta.leaf);
+      if (hit) {
+        const int rk = meta.rank;
         if (closest) {
-          if ((!T.mhave || tf < T.mbest || (tf == T.mbest && rk < T.mface)) && leaf_ok(T, S, rk)) {
+          if ((!T.mhave || tf < T.mbest || (tf == T.mbest && rk < T.mface)) && leaf_ok(T, S, meta.leaf)) {
             T.mbest = tf;
             T.mface = rk;
             T.mhave = true;
           }
         } else {
           const double tw = tf / len;
-          if (key_less(tp, rp, sq, tw, T.moi, rk) && tw <= tlimit && leaf_ok(T, S, rk)) {
+          if (key_less(tp, rp, sq, tw, T.moi, rk) && tw <= tlimit && leaf_ok(T, S, meta.leaf)) {
             if (tw < T.tblock && blocker(T, T.moi, rk)) {
               bt = tw;
               bobj = T.moi;
@@ -822,6 +829,8 @@ struct TravTrees {
   DevRoot sroot;
   std::vector<RtxFace> tfaces;
   std::vector<int32_t> trank;
+  std::vector<TMeta> tmeta;
+  std::vector<RtxObject> objs;  // the objects with their mesh fields in pad (augment_objects)
   int sneed = 0, mneed = 0;
   int n_mhot = 0;  // mesh records [0, n_mhot) are the hot ones (renumbered first)
 };
@@ -863,8 +872,26 @@ inline void hot_mesh_records(TravTrees& T, int cap) {
   T.n_mhot = static_cast<int>(hot.size());
 }
 
+// The device copy of the objects: a trimesh's mesh fields (face_off,
+// node_off, vert_off, flags) in RtxObject.pad (RTX_OBJ_*), read with the
+// object record.  pad[RTX_OBJ_WOPAQUE] is left 0 (rtx_scene_create sets it).
+inline void augment_objects(const RtxSceneDesc* d, std::vector<RtxObject>& objs) {
+  objs.assign(d->objects, d->objects + d->n_objects);
+  for (RtxObject& o : objs) {
+    for (int k = 0; k < 5; ++k) o.pad[k] = 0;
+    if (o.type != RTX_OBJ_TRIMESH || o.mesh < 0 || o.mesh >= d->n_meshes) continue;
+    const RtxMesh& me = d->meshes[o.mesh];
+    o.pad[RTX_OBJ_FACE_OFF] = me.face_off;
+    o.pad[RTX_OBJ_NODE_OFF] = me.node_off;
+    o.pad[RTX_OBJ_VERT_OFF] = me.vert_off;
+    o.pad[RTX_OBJ_MFLAGS] = (me.node_count > 0 ? RTX_MESH_TREE : 0) | (me.has_normals ? RTX_MESH_NORMALS : 0) |
+                            (me.has_vmats ? RTX_MESH_VMATS : 0);
+  }
+}
+
 inline bool build_trav_trees(const RtxSceneDesc* d, TravTrees& T) {
   std::memset(&T.sroot, 0, sizeof(T.sroot));
+  augment_objects(d, T.objs);
   // mesh-tree SAH parameters (A/B switches; the walk's results do not depend
   // on the tree, DESIGN.md "Traversal trees")
   SahParams sp;
@@ -895,6 +922,7 @@ inline bool build_trav_trees(const RtxSceneDesc* d, TravTrees& T) {
   T.mroots.assign(size_t(d->n_meshes), DevRoot());
   T.tfaces.assign(size_t(d->n_faces), RtxFace());
   T.trank.assign(size_t(d->n_faces), 0);
+  T.tmeta.assign(size_t(d->n_faces), TMeta{0, 0});
   for (int m = 0; m < d->n_meshes; ++m) {
     const RtxMesh& me = d->meshes[m];
     std::memset(&T.mroots[size_t(m)], 0, sizeof(DevRoot));
@@ -911,6 +939,7 @@ inline bool build_trav_trees(const RtxSceneDesc* d, TravTrees& T) {
     for (int j = 0; j < me.face_count; ++j) {
       T.tfaces[size_t(me.face_off + j)] = d->faces[me.face_off + order[size_t(j)]];
       T.trank[size_t(me.face_off + j)] = order[size_t(j)];
+      T.tmeta[size_t(me.face_off + j)] = TMeta{order[size_t(j)], me.node_off + d->face_ids[me.face_off + order[size_t(j)]].leaf};
     }
     int need = 0;
     if (!build_node4(nodes.data(), static_cast<int>(nodes.size()), T.mn4, T.mroots[size_t(m)], need)) return false;

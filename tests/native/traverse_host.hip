@@ -36,7 +36,8 @@ bool make_scene(const RtxSceneDesc* d, HostScene& H) {
   S.tfaces = H.T.tfaces.data();
   S.trank = H.T.trank.data();
   S.snodes = d->scene_nodes;
-  S.objs = d->objects;
+  S.objs = H.T.objs.data();  // with the mesh fields in pad (augment_objects)
+  S.tmeta = H.T.tmeta.data();
   S.oprm = d->obj_params;
   S.mats = d->materials;
   S.meshes = d->meshes;
