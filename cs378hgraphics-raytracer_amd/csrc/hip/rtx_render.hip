@@ -1170,7 +1170,15 @@ __device__ __forceinline__ void stats_add(const Counters& C, unsigned long long*
 // per-kernel work (rtx_last_work): queries, node visits, object and triangle
 // tests, shades of one kernel class at stats[base .. base + 4] (20 batched
 // closest-hit launches, 25 batched next-hit / walk launches, 30 tail launches)
-#define RTX_STATS_N 39  // 35..38: the slowest wave of the last closest / next launch (RTX_DEBUG=2)
+// 35..38: the slowest wave of the last closest / next launch (RTX_DEBUG=2);
+// 39 + 20 * (MODE - 1) ..: the trace kernels' cycle breakdown (STATS
+// instantiations only): [c] core cycles of the wave steps whose stepping
+// lanes were at the unit classes of bit mask c (1 record, 2 object or the
+// step into a leaf's objects, 4 mesh leaf), [8 + c] their count, [16] / [17]
+// cycles / runs of the per-query work between traversals (FUSED: shading,
+// walk steps), [18] cycles the waves spent in all (RTX_DEBUG report)
+#define RTX_STATS_PROF 39
+#define RTX_STATS_N 79
 __device__ __forceinline__ void stats_add_class(const Counters& C, unsigned long long* stats, int lane, int base) {
   const int64_t v[5] = {C.queries, C.nodes, C.objects, C.tris, C.shades};
 #pragma unroll
@@ -1914,6 +1922,9 @@ __global__ void __launch_bounds__(WG, !FUSED ? RTX_TRACE_WAVES : (MODE == Q_CLOS
   // (STATS) the wave's start, its claims and walk restarts: the slowest
   // wave of the launch is reported by RTX_DEBUG=2
   const uint64_t wt0 = STATS ? wall_clock64() : 0;
+  // (STATS) cycle breakdown by unit class (RTX_STATS_PROF)
+  uint64_t pcyc[8] = {0, 0, 0, 0, 0, 0, 0, 0}, pcnt[8] = {0, 0, 0, 0, 0, 0, 0, 0}, xcyc = 0, xcnt = 0;
+  const uint64_t pt0 = STATS ? clock64() : 0;
   unsigned int nclaims = 0, nrestart = 0;
   auto finish = [&]() {
     const size_t slot = static_cast<size_t>(Q.slot[kq]);
@@ -1988,6 +1999,7 @@ __global__ void __launch_bounds__(WG, !FUSED ? RTX_TRACE_WAVES : (MODE == Q_CLOS
     }
   };
   for (;;) {
+    const uint64_t xt0 = STATS ? clock64() : 0;
     if (FUSED) {
       // Every lane is idle here (RTX_REFILL 1: the step loop below runs until
       // no lane is active), so the walk state is dead: resetting it to
@@ -2070,6 +2082,10 @@ __global__ void __launch_bounds__(WG, !FUSED ? RTX_TRACE_WAVES : (MODE == Q_CLOS
       qnext += take;
       idle = __ballot(!active && !pend);
     }
+    if (STATS) {
+      xcyc += clock64() - xt0;
+      xcnt++;
+    }
     if (__ballot(active || pend) == 0ull) break;  // nothing claimed and nothing left
     const int thresh = exhausted ? 1 : RTX_REFILL;
     do {
@@ -2080,9 +2096,15 @@ __global__ void __launch_bounds__(WG, !FUSED ? RTX_TRACE_WAVES : (MODE == Q_CLOS
       // lane's own sequence of units is unchanged (results identical).
       const unsigned long long at_rec = __ballot(active && trav_at_record(T));
       const bool go = active && (static_cast<int>(__popcll(at_rec)) < SA.leaf_k || trav_at_record(T));
+      uint64_t st0 = 0;
+      int combo = 0;
       if (STATS) {  // SIMD efficiency of the walk (RTX_DEBUG report)
         wsteps++;
         lsteps += __popcll(__ballot(go));
+        const int cls = !go ? 0 : (trav_at_record(T) ? 1 : (T.mode == 2 ? 4 : 2));
+        combo = static_cast<int>((__ballot(cls == 1) ? 1 : 0) | (__ballot(cls == 2) ? 2 : 0) |
+                                 (__ballot(cls == 4) ? 4 : 0));
+        st0 = clock64();
       }
       if (go) {
         if (STATS) qsteps++;
@@ -2097,7 +2119,27 @@ __global__ void __launch_bounds__(WG, !FUSED ? RTX_TRACE_WAVES : (MODE == Q_CLOS
           qsteps = 0;
         }
       }
+      if (STATS) {
+        const uint64_t dt = clock64() - st0;
+#pragma unroll
+        for (int c = 0; c < 8; ++c)
+          if (c == combo) {
+            pcyc[c] += dt;
+            pcnt[c]++;
+          }
+      }
     } while (static_cast<int>(__popcll(__ballot(active))) >= thresh);
+  }
+  if (STATS && lane == 0) {
+    unsigned long long* pr = stats + RTX_STATS_PROF + 20 * (MODE - 1);
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+      atomicAdd(&pr[c], static_cast<unsigned long long>(pcyc[c]));
+      atomicAdd(&pr[8 + c], static_cast<unsigned long long>(pcnt[c]));
+    }
+    atomicAdd(&pr[16], static_cast<unsigned long long>(xcyc));
+    atomicAdd(&pr[17], static_cast<unsigned long long>(xcnt));
+    atomicAdd(&pr[18], static_cast<unsigned long long>(clock64() - pt0));
   }
   if (STATS) {
     stats_add(C, stats, lane);  // traversal counts (and the shading's, FUSED Q_CLOSEST)
@@ -3048,7 +3090,20 @@ rtx_status rtx_render(void* scene, const RtxRenderParams* params, uint8_t* rgb8,
       const size_t npos = (size_t(1) << (fork_depth + 1)) - 2;
       const size_t bucket_need = fork_ok ? nunit_out * (npos * 3 * sizeof(double) + sizeof(unsigned)) : 0;
       if (bucket_need > avail / 2) fork_ok = false;  // buckets would crowd out the slots: plain accumulation
-      const size_t slot_budget = std::min<size_t>(size_t(96) << 30, avail - (fork_ok ? bucket_need : 0));
+      size_t slot_budget = std::min<size_t>(size_t(96) << 30, avail - (fork_ok ? bucket_need : 0));
+      // Frame-memory cap (RTX_MEM_GB, default 40; 0: none): the slot pool
+      // gets what the cap leaves after the sample sums and the buckets.  The
+      // buckets keep their size — whether a frame has buckets must not
+      // depend on the cap, the image would change with it — so the cap only
+      // sets how many samples are in flight at once (the rest are claimed
+      // as slots free up, kdone).
+      size_t cap_gb = 40;
+      if (const char* e = getenv("RTX_MEM_GB")) cap_gb = static_cast<size_t>(atoll(e));
+      if (cap_gb > 0) {
+        const size_t cap_b = cap_gb << 30, fixed = sbuf_need + (fork_ok ? bucket_need : 0);
+        const size_t min_slots = size_t(G) * 16 * WG;  // never below 16 workgroups per group
+        slot_budget = std::min(slot_budget, std::max(cap_b > fixed ? cap_b - fixed : 0, min_slots * per_slot));
+      }
       const int64_t cap = static_cast<int64_t>(slot_budget / per_slot);
       if (fork_ok && !(ns_env && atoll(ns_env) > 0)) {
         // one slot per sample plus half as many fork slots (headline frame:
@@ -3058,9 +3113,12 @@ rtx_status rtx_render(void* scene, const RtxRenderParams* params, uint8_t* rgb8,
       }
       if (nslot64 > cap && !(ns_env && atoll(ns_env) > 0)) nslot64 = std::max<int64_t>(cap, int64_t(G) * 4 * WG);
     }
-    const bool fork = fork_ok && F.n_samples * 4 <= nslot64 * 3;  // spare slots for forked sub-trees
+    // spare slots for forked sub-trees: a third of the pool when it cannot
+    // give every sample a slot of its own plus half as many spares
+    const bool fork = fork_ok && nslot64 >= int64_t(G) * 8 * WG;
     int64_t gsamp = (F.n_samples + G - 1) / G;  // sample slots per group
-    if (gsamp > (nslot64 + G - 1) / G) gsamp = (nslot64 + G - 1) / G;
+    const int64_t gcap = fork && F.n_samples * 4 > nslot64 * 3 ? nslot64 * 2 / 3 : nslot64;
+    if (gsamp > (gcap + G - 1) / G) gsamp = (gcap + G - 1) / G;
     gsamp = (gsamp + 63) / 64 * 64;  // whole 64-unit runs (slot_unit)
     int64_t gspare = 0;
     if (fork) gspare = std::min<int64_t>(gsamp / 2 + WG, nslot64 / G - gsamp);
@@ -3160,6 +3218,9 @@ rtx_status rtx_render(void* scene, const RtxRenderParams* params, uint8_t* rgb8,
     // ms at 200k / 400k / 1M; sequential machine: 92.6 / 91.0 / 99.5 ms at
     // 65k / 200k / 400k)
     int64_t tail_slots = 1000000;
+    // (a capped pool, fewer slots than units: the same share of a group's
+    // slots as 1 M is of the uncapped headline frame's 16.6 M)
+    if (int64_t(F.wf_nslot) < F.n_samples) tail_slots = std::min<int64_t>(tail_slots, gslots * 6 / 100);
     const char* tail_env = getenv("RTX_TAIL");
     if (tail_env) tail_slots = atoll(tail_env);
     // RTX_TAIL_ITER=k: the tail kernel takes over at batched iteration k
@@ -3171,6 +3232,10 @@ rtx_status rtx_render(void* scene, const RtxRenderParams* params, uint8_t* rgb8,
     int tail_iter = 5;
     const char* ti_env = getenv("RTX_TAIL_ITER");
     if (ti_env) tail_iter = std::max(0, atoi(ti_env));
+    // (only when every unit has its sample slot from the start: with fewer
+    // slots than units, iteration 5 comes long before the units are all
+    // claimed, and the switch waits for the live count instead)
+    if (int64_t(F.wf_nslot) < F.n_samples && !ti_env) tail_iter = 0;
     F.qchunk = 64;
     // First iteration without an advance launch (fused frames): the closest-
     // hit launch claims each sample slot's first sample and queries its first
@@ -3589,6 +3654,17 @@ rtx_status rtx_render(void* scene, const RtxRenderParams* params, uint8_t* rgb8,
         fprintf(stderr, "rtx trace steps per query: max closest %llu next %llu; queries over 100 steps: %llu / %llu\n",
                 c[12], c[13], c[14], c[15]);
         fprintf(stderr, "rtx tail: slowest chain %llu cycles, longest chain %llu queries\n", c[16], c[17]);
+        for (int m = 0; m < 2; ++m) {  // cycle breakdown of the trace kernels by unit class
+          const unsigned long long* pr = c + RTX_STATS_PROF + 20 * m;
+          const double tot = pr[18] ? double(pr[18]) : 1.0;
+          fprintf(stderr, "rtx %s kernel cycles %.4g: between traversals %.3f (%llu runs, %.0f cyc/run)",
+                  m ? "next" : "closest", double(pr[18]), pr[16] / tot, pr[17], pr[17] ? double(pr[16]) / pr[17] : 0.0);
+          static const char* nm[8] = {"idle", "R", "O", "RO", "L", "RL", "OL", "ROL"};
+          for (int k = 1; k < 8; ++k)
+            fprintf(stderr, "; %s %.3f (%llu steps, %.0f cyc)", nm[k], pr[k] / tot, pr[8 + k],
+                    pr[8 + k] ? double(pr[k]) / pr[8 + k] : 0.0);
+          fprintf(stderr, "\n");
+        }
       }
     }
     std::memset(stats, 0, sizeof(*stats));

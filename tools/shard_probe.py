@@ -42,6 +42,7 @@ def main():
     dev = pkg.DeviceScene(host, 0)
     h = host.height_for(opts.width)
     stream = torch.cuda.current_stream().cuda_stream
+    free0 = torch.cuda.mem_get_info()[0]
     for n in ns:
         times = []
         for r in range(n):
@@ -57,9 +58,10 @@ def main():
                 dev.render_device(opts, out.data_ptr(), 0, stream, tile=tile, shard=r, nshards=n, packed=n > 1)
             torch.cuda.synchronize()
             times.append((time.perf_counter() - t0) / 3 * 1e3)
-        full = 1e3 if n == 1 else None
+        # HBM the library holds beyond the scene (frame buffers grown so far)
+        held = (free0 - torch.cuda.mem_get_info()[0]) / 2**30
         print(json.dumps({"scene": scene, "flags": flags, "n": n, "shard_ms": [round(t, 2) for t in times],
-                          "max_ms": round(max(times), 2)}),
+                          "max_ms": round(max(times), 2), "frame_buffers_gb": round(held, 2)}),
               flush=True)
 
 
