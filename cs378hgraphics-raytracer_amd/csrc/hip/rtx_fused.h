@@ -322,6 +322,9 @@ __device__ __forceinline__ void shade_hit(LaneRef& LR, const DevScene& S, const 
   const bool node = pos > 0 && P.depth - rdepth == ilog2i(pos);
   const int node_refl = node && 2 * pos < F.fork_npos + 2 ? 2 * pos : 0;
   const int node_refr = node && 2 * pos + 1 < F.fork_npos + 2 ? 2 * pos + 1 : 0;
+  // the unit's bucket set, taken by its root before the first child exists
+  if (F.fork_on && pos == 1)
+    bucket_alloc(F, LR.bunit(), (node_refl || node_refr) && ((next_trans && !tir) || (flags & RTX_MF_REFL) || tir));
   // push refraction first so that reflection is traced first (the entry at
   // `top` is this ray's own, read above: it is overwritten)
   if (next_trans && !tir && LR.top() < pend_cap) {

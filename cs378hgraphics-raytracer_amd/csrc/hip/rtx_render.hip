@@ -29,6 +29,7 @@
 #include <memory>
 #include <string>
 #include <type_traits>
+#include <map>
 #include <vector>
 
 #include "rtx_device.h"
@@ -106,6 +107,17 @@ struct FrameParams {
   int fork_on, fork_npos;
   double* fbuf;
   unsigned int* fmask;
+  // Bucket sets are pooled: only a unit whose root ray has a child (a node
+  // at heap position 2 or 3) has buckets, and it takes set bidx[unit] from
+  // the pool when its root is shaded (bucket_alloc: once per unit, by the
+  // unit's own lane, before any child exists — so the count is the same on
+  // every render of the same frame).  fbuf holds bcap sets; *bcnt counts
+  // the sets taken; *bover is set if one is refused (the host sizes bcap
+  // from the last render of the same frame, full size otherwise).
+  int* bidx;
+  unsigned int* bcnt;
+  unsigned int* bover;
+  int bcap;
   // fused shadow walks (rtx_fused.h): the finished terms of the walks,
   // wterm[(light * nslot + slot) * 3 + c]
   int fuse;
@@ -379,12 +391,20 @@ struct Pending {
 // has to hold the whole state in VGPRs: the state machine touches only the
 // fields of its current step, and the traversal's registers are not shared
 // with it.  LaneRef gives a lane's fields as accessors (LR.st(), LR.acc(), ...).
-#define LANE_INT_FIELDS(X) X(st) X(sample_slot) X(rec_on) X(pass) X(camk) X(nrays) X(top) X(rdepth) X(rkind) \
-  X(first_query) X(cam_end) X(sobj) X(ssub) X(m_flags) X(li) X(pick) X(qmode) X(qrp) X(qsq) X(kdone) X(bobj) X(bsub) X(bhave) \
-  X(dret) X(dpass) X(dpush) X(dhead) X(dtot) X(dlast) X(dopq) X(mo_trans) X(wobj) X(wsub) X(fpos) X(rpos) X(wmask) X(bunit)
+// The fields the fused machine (rtx_fused.h, claim_sample, lane_init) uses
+// come first in each list: a fused frame allocates only those
+// (LANE_*_FUSED of each type: 16 ints, 2 doubles, 3 vectors = 152 B per
+// slot instead of 668), the others are the sequential machine's.
+#define LANE_INT_FIELDS(X) X(st) X(sample_slot) X(rec_on) X(pass) X(camk) X(nrays) X(top) X(first_query) X(cam_end) \
+  X(qmode) X(kdone) X(fpos) X(rpos) X(wmask) X(bunit) X(dret) \
+  X(rdepth) X(rkind) X(sobj) X(ssub) X(m_flags) X(li) X(pick) X(qrp) X(qsq) X(bobj) X(bsub) X(bhave) \
+  X(dpass) X(dpush) X(dhead) X(dtot) X(dlast) X(dopq) X(mo_trans) X(wobj) X(wsub)
 #define LANE_DBL_FIELDS(X) X(sx) X(sy) X(st_t) X(m_sh) X(dattn) X(last_t) X(qtp) X(bt) X(mo_idx) X(wt) X(wtr)
-#define LANE_VEC_FIELDS(X) X(acc) X(rp) X(rd) X(W) X(N) X(i_out) X(dscomp) X(m_kd) X(m_ks) X(area_sum) X(sdir) \
+#define LANE_VEC_FIELDS(X) X(acc) X(W) X(i_out) X(rp) X(rd) X(N) X(dscomp) X(m_kd) X(m_ks) X(area_sum) X(sdir) \
   X(wpos) X(sattn) X(dpos) X(ddir) X(dkt) X(didx) X(mo_kt)
+#define LANE_INT_FUSED 16
+#define LANE_DBL_FUSED 2
+#define LANE_VEC_FUSED 3
 
 enum {
 #define E_(f) LI_##f,
@@ -405,27 +425,36 @@ enum {
   LV_COUNT
 };
 
+static_assert(LI_dret < LANE_INT_FUSED && LI_bunit < LANE_INT_FUSED && LI_qmode < LANE_INT_FUSED &&
+                  LI_rdepth == LANE_INT_FUSED,
+              "fused lane fields first");
+static_assert(LD_sy < LANE_DBL_FUSED && LD_st_t == LANE_DBL_FUSED, "fused lane fields first");
+static_assert(LV_i_out < LANE_VEC_FUSED && LV_rp == LANE_VEC_FUSED, "fused lane fields first");
+
 struct LaneMem {
-  int* i;     // [LI_COUNT][n]
-  double* d;  // [LD_COUNT][n]
-  dvec3* v;   // [LV_COUNT][n]
+  int* i;     // [LI_COUNT][n]  (fused frames: [LANE_INT_FUSED][n])
+  double* d;  // [LD_COUNT][n]  (LANE_DBL_FUSED)
+  dvec3* v;   // [LV_COUNT][n]  (LANE_VEC_FUSED)
   size_t n;   // lanes
 };
 
-__host__ __device__ inline size_t lane_mem_bytes(size_t n) {
-  return n * (LI_COUNT * sizeof(int) + LD_COUNT * sizeof(double) + LV_COUNT * sizeof(dvec3)) + 512;
+// fused: only the fused machine's fields (the leading ones of each list)
+__host__ __device__ inline size_t lane_mem_bytes(size_t n, bool fused = false) {
+  return n * ((fused ? LANE_INT_FUSED : LI_COUNT) * sizeof(int) + (fused ? LANE_DBL_FUSED : LD_COUNT) * sizeof(double) +
+              (fused ? LANE_VEC_FUSED : LV_COUNT) * sizeof(dvec3)) +
+         512;
 }
 
 // carve a LaneMem out of one allocation (256-byte aligned pieces)
-inline LaneMem lane_mem_at(void* base, size_t n) {
+inline LaneMem lane_mem_at(void* base, size_t n, bool fused = false) {
   auto al = [](size_t x) { return (x + 255) & ~size_t(255); };
   char* p = static_cast<char*>(base);
   LaneMem m;
   m.n = n;
   m.d = reinterpret_cast<double*>(p);
-  p += al(n * LD_COUNT * sizeof(double));
+  p += al(n * (fused ? LANE_DBL_FUSED : LD_COUNT) * sizeof(double));
   m.v = reinterpret_cast<dvec3*>(p);
-  p += al(n * LV_COUNT * sizeof(dvec3));
+  p += al(n * (fused ? LANE_VEC_FUSED : LV_COUNT) * sizeof(dvec3));
   m.i = reinterpret_cast<int*>(p);
   return m;
 }
@@ -684,7 +713,12 @@ __device__ __forceinline__ double pend_code(int pos, int depth, int kind) {
 // one lane at a time, in that lane's ray order; the fmask bit says whether
 // the bucket already holds a sum)
 __device__ __forceinline__ void bucket_add(const FrameParams& F, int s, int b, const dvec3& c) {
-  double* f = F.fbuf + (static_cast<int64_t>(s) * F.fork_npos + (b - 2)) * 3;
+  const int set = F.bidx[s];
+  if (set < 0) {  // (never: the root takes the set before its children exist)
+    atomicOr(F.bover, 2u);
+    return;
+  }
+  double* f = F.fbuf + (static_cast<int64_t>(set) * F.fork_npos + (b - 2)) * 3;
   const unsigned int bit = 1u << (b - 2);
   const unsigned int old = atomicOr(&F.fmask[s], bit);
   if (old & bit) {
@@ -695,6 +729,27 @@ __device__ __forceinline__ void bucket_add(const FrameParams& F, int s, int b, c
     f[0] = c.x;
     f[1] = c.y;
     f[2] = c.z;
+  }
+}
+
+// A bucket set for unit s (lanes with `want`: a root ray about to push a
+// node child), wave-aggregated like fork_claim.  Past the pool's capacity
+// the unit gets none and *bover says so (bucket_add then drops its colours:
+// the host re-renders with a full-size pool, rtx_render).
+__device__ __forceinline__ void bucket_alloc(const FrameParams& F, int s, bool want) {
+  const unsigned long long m = __ballot(want);
+  if (m == 0ull) return;
+  const int leader = __builtin_ctzll(m);
+  unsigned int base = 0;
+  if (static_cast<int>(threadIdx.x & 63) == leader) base = atomicAdd(F.bcnt, static_cast<unsigned int>(__popcll(m)));
+  base = __shfl(base, leader);
+  if (!want) return;
+  const unsigned int idx = base + lane_prefix(m);
+  if (idx < static_cast<unsigned int>(F.bcap)) {
+    F.bidx[s] = static_cast<int>(idx);
+  } else {
+    F.bidx[s] = -1;
+    atomicOr(F.bover, 1u);
   }
 }
 
@@ -782,6 +837,10 @@ __device__ __forceinline__ void advance_lane(LaneRef& LR, const DevScene& S, con
     const int node_refr = node && 2 * pb + 1 < F.fork_npos + 2 ? 2 * pb + 1 : 0;
     const int pos_refl = node_refl ? node_refl : pb;
     const int pos_refr = node_refr ? node_refr : pb;
+    // the unit's bucket set, taken by its root before the first child exists
+    if (F.fork_on && pb == 1)
+      bucket_alloc(F, LR.bunit(),
+                   (node_refl || node_refr) && ((next_trans && !tir) || (LR.m_flags() & RTX_MF_REFL) || tir));
     // push refraction first so that reflection is traced first
     if (next_trans && !tir && LR.top() < pend_cap) {
       const dvec3 tp = rtm::ray_at(LR.rp(), LR.rd(), LR.st_t() + RTX_RAY_EPS);
@@ -1587,7 +1646,10 @@ __device__ __forceinline__ void claim_sample(LaneRef& L, const FrameParams& F, R
     L.sample_slot() = static_cast<int>(oidx * F.spp + smp);
     // the buckets' owner: the sample, or with the DoF split its camera ray
     L.bunit() = F.cam_split ? L.sample_slot() * F.ncam + cam0 : L.sample_slot();
-    if (F.fork_on) F.fmask[L.bunit()] = 0u;  // no bucket written yet (forks come later)
+    if (F.fork_on) {  // no bucket written yet (forks come later), no set taken
+      F.fmask[L.bunit()] = 0u;
+      F.bidx[L.bunit()] = -1;
+    }
     L.rec_on() = rec;
     L.pass() = 0;
     L.camk() = cam0;
@@ -2196,10 +2258,11 @@ __device__ __forceinline__ dvec3 sample_value(const FrameParams& F, const double
     dvec3 u = mk3(r[0], r[1], r[2]);
     if (F.fork_on) {
       unsigned int m = F.fmask[uid];
+      const int64_t set = m ? F.bidx[uid] : 0;
       while (m) {
         const int b = __builtin_ctz(m);
         m &= m - 1;
-        const double* f = F.fbuf + (uid * F.fork_npos + b) * 3;
+        const double* f = F.fbuf + (set * F.fork_npos + b) * 3;
         u += mk3(f[0], f[1], f[2]);
       }
     }
@@ -2473,6 +2536,18 @@ struct SceneState {
   unsigned int* h_counters = nullptr;  // pinned
   DevScene* d_scene = nullptr;         // device copy of S_launch (shadow early-out)
   unsigned int* d_acnt = nullptr;      // adaptive AA: regions to subdivide, emit cursor
+  // pooled bucket sets (FrameParams.bidx): per unit its set index; pool
+  // counters [taken, refused]; the sets each frame (key: its parameters and
+  // its place in the render) took on its last render, read back once
+  int* d_bidx = nullptr;
+  size_t bidx_bytes = 0;
+  unsigned int* d_bstat = nullptr;
+  unsigned int* h_bstat = nullptr;  // pinned
+  hipEvent_t bstat_ev = nullptr;
+  bool bstat_pending = false;
+  uint64_t bstat_key = 0;
+  std::map<uint64_t, uint32_t> bucket_hist;
+  int wf_call = 0;  // run_wavefront calls of the current rtx_render
   // adaptive AA: one buffer per level (values, first-quarter index, mask,
   // regions), grown on demand and reused by later frames (no hipMalloc /
   // hipFree, which synchronises the device, per level per frame)
@@ -2722,6 +2797,10 @@ rtx_status rtx_scene_destroy(void* scene) {
   if (st->d_work) (void)hipFree(st->d_work);
   if (st->d_stats) (void)hipFree(st->d_stats);
   if (st->d_acnt) (void)hipFree(st->d_acnt);
+  if (st->d_bidx) (void)hipFree(st->d_bidx);
+  if (st->d_bstat) (void)hipFree(st->d_bstat);
+  if (st->h_bstat) (void)hipHostFree(st->h_bstat);
+  if (st->bstat_ev) (void)hipEventDestroy(st->bstat_ev);
   for (void* p : st->d_level)
     if (p) (void)hipFree(p);
   if (st->d_picks) (void)hipFree(st->d_picks);
@@ -2975,6 +3054,7 @@ rtx_status rtx_render(void* scene, const RtxRenderParams* params, uint8_t* rgb8,
   };
   double* sb = adaptive && megakernel ? nullptr : st->d_sbuf;
   std::vector<std::pair<hipEvent_t, hipEvent_t>> frame_events;
+  st->wf_call = 0;
 
   if (megakernel) {
     const int cslots = adaptive ? (F.spp > 64 ? F.spp : 64) : 0;
@@ -3076,8 +3156,37 @@ rtx_status rtx_render(void* scene, const RtxRenderParams* params, uint8_t* rgb8,
     const size_t rec_c = sizeof(int) + QL_D * sizeof(double) + 2 * sizeof(int);
     const size_t rec_n = fuse ? sizeof(int) + QF_D * sizeof(double) + QF_I * sizeof(int) : rec_c;
     const size_t nrec_n = fuse ? std::max<size_t>(1, nl) : 1;
-    const size_t per_slot = lane_mem_bytes(1) - 512 + size_t(pend_cap) * 13 * sizeof(double) + rec_c + nrec_n * rec_n +
-                            2 * sizeof(int) + nl * 3 * sizeof(double);
+    const size_t per_slot = lane_mem_bytes(1, fuse) - 512 + size_t(pend_cap) * 13 * sizeof(double) + rec_c +
+                            nrec_n * rec_n + 2 * sizeof(int) + nl * 3 * sizeof(double);
+    // the bucket-set pool: as many sets as this frame took on its last
+    // render (deterministic: one per unit whose root has a node child), the
+    // full count (a set per unit) the first time.  Whether the frame has
+    // buckets at all was decided above on the full count, so the image never
+    // depends on the pool.
+    const size_t npos_b = (size_t(1) << (fork_depth + 1)) - 2;  // (as npos below)
+    size_t bcap = nunit_out;
+    uint64_t bkey = 1469598103934665603ull;
+    {
+      auto mix = [&](const void* p, size_t n) {
+        const unsigned char* c = static_cast<const unsigned char*>(p);
+        for (size_t k = 0; k < n; ++k) bkey = (bkey ^ c[k]) * 1099511628211ull;
+      };
+      mix(&F.P, sizeof(F.P));
+      const int64_t ks[6] = {F.n_samples, nout, level0 ? 1 : 0, st->wf_call, int64_t(npos_b), int64_t(nunit_out)};
+      mix(ks, sizeof(ks));
+      if (st->bstat_pending) {  // the last first-time frame's count (long done by now)
+        HIP_TRY(hipEventSynchronize(st->bstat_ev));
+        if (st->h_bstat[1] == 0u) {
+          st->bucket_hist[st->bstat_key] = st->h_bstat[0];
+        } else {
+          fprintf(stderr, "rtx_render: bucket pool refused a set (%u taken); frame pool reset\n", st->h_bstat[0]);
+          st->bucket_hist.erase(st->bstat_key);
+        }
+        st->bstat_pending = false;
+      }
+      const auto it = st->bucket_hist.find(bkey);
+      if (it != st->bucket_hist.end()) bcap = std::min<size_t>(nunit_out, size_t(it->second) + 64);
+    }
     {
       // memory budget: what the device has free plus the frame buffers this
       // scene already holds (they are reused or replaced), less a reserve
@@ -3090,17 +3199,19 @@ rtx_status rtx_render(void* scene, const RtxRenderParams* params, uint8_t* rgb8,
       const size_t npos = (size_t(1) << (fork_depth + 1)) - 2;
       const size_t bucket_need = fork_ok ? nunit_out * (npos * 3 * sizeof(double) + sizeof(unsigned)) : 0;
       if (bucket_need > avail / 2) fork_ok = false;  // buckets would crowd out the slots: plain accumulation
-      size_t slot_budget = std::min<size_t>(size_t(96) << 30, avail - (fork_ok ? bucket_need : 0));
-      // Frame-memory cap (RTX_MEM_GB, default 40; 0: none): the slot pool
+      // what the pooled sets take (bcap sets, a mask and a set index per unit)
+      const size_t pool_need = fork_ok ? bcap * npos * 3 * sizeof(double) + nunit_out * 2 * sizeof(unsigned) : 0;
+      size_t slot_budget = std::min<size_t>(size_t(96) << 30, avail - pool_need);
+      // Frame-memory cap (RTX_MEM_GB GiB, default none): the slot pool
       // gets what the cap leaves after the sample sums and the buckets.  The
       // buckets keep their size — whether a frame has buckets must not
       // depend on the cap, the image would change with it — so the cap only
       // sets how many samples are in flight at once (the rest are claimed
       // as slots free up, kdone).
-      size_t cap_gb = 40;
+      size_t cap_gb = 0;
       if (const char* e = getenv("RTX_MEM_GB")) cap_gb = static_cast<size_t>(atoll(e));
       if (cap_gb > 0) {
-        const size_t cap_b = cap_gb << 30, fixed = sbuf_need + (fork_ok ? bucket_need : 0);
+        const size_t cap_b = cap_gb << 30, fixed = sbuf_need + pool_need;
         const size_t min_slots = size_t(G) * 16 * WG;  // never below 16 workgroups per group
         slot_budget = std::min(slot_budget, std::max(cap_b > fixed ? cap_b - fixed : 0, min_slots * per_slot));
       }
@@ -3134,16 +3245,33 @@ rtx_status rtx_render(void* scene, const RtxRenderParams* params, uint8_t* rgb8,
     F.fork_npos = fork_ok ? (1 << (fork_depth + 1)) - 2 : 0;
     F.fbuf = nullptr;
     F.fmask = nullptr;
+    F.bidx = nullptr;
+    F.bcnt = F.bover = nullptr;
+    F.bcap = 0;
     if (fork_ok) {
       const size_t nsamp_out = size_t(nout) * F.spp;
-      if ((rc = ensure(reinterpret_cast<void**>(&st->d_fbuf), &st->fbuf_bytes,
-                       nunit_out * F.fork_npos * 3 * sizeof(double))) != RTX_OK)
-        return rc;
+      const size_t fbuf_need = std::max<size_t>(1, bcap) * F.fork_npos * 3 * sizeof(double);
+      if (st->fbuf_bytes > 2 * fbuf_need + (size_t(64) << 20)) {  // a smaller pool than the first render's: give it back
+        (void)hipFree(st->d_fbuf);
+        st->d_fbuf = nullptr;
+        st->fbuf_bytes = 0;
+      }
+      if ((rc = ensure(reinterpret_cast<void**>(&st->d_fbuf), &st->fbuf_bytes, fbuf_need)) != RTX_OK) return rc;
       if ((rc = ensure(reinterpret_cast<void**>(&st->d_fmask), &st->fmask_bytes, nunit_out * sizeof(unsigned int))) !=
           RTX_OK)
         return rc;
+      if ((rc = ensure(reinterpret_cast<void**>(&st->d_bidx), &st->bidx_bytes, nunit_out * sizeof(int))) != RTX_OK)
+        return rc;
+      if (!st->d_bstat) HIP_TRY(hipMalloc(&st->d_bstat, 4 * sizeof(unsigned int)));
+      if (!st->h_bstat) HIP_TRY(hipHostMalloc(&st->h_bstat, 4 * sizeof(unsigned int)));
+      if (!st->bstat_ev) HIP_TRY(hipEventCreateWithFlags(&st->bstat_ev, hipEventDisableTiming));
+      HIP_TRY(hipMemsetAsync(st->d_bstat, 0, 4 * sizeof(unsigned int), stream));
       F.fbuf = st->d_fbuf;
       F.fmask = st->d_fmask;
+      F.bidx = st->d_bidx;
+      F.bcnt = st->d_bstat;
+      F.bover = st->d_bstat + 1;
+      F.bcap = static_cast<int>(std::min<size_t>(bcap, size_t(INT32_MAX)));
       // fmask[sample] is cleared when the sample is claimed (claim_sample)
       if (hits && level0) HIP_TRY(hipMemsetAsync(d_hits, 0xff, nsamp_out * sizeof(RtxHitRecord), stream));
     }
@@ -3166,8 +3294,8 @@ rtx_status rtx_render(void* scene, const RtxRenderParams* params, uint8_t* rgb8,
         return rc;
       F.wterm = st->d_wterm;
     }
-    if ((rc = ensure(&st->d_lane, &st->lane_bytes, lane_mem_bytes(ns))) != RTX_OK) return rc;
-    const LaneMem A = lane_mem_at(st->d_lane, ns);
+    if ((rc = ensure(&st->d_lane, &st->lane_bytes, lane_mem_bytes(ns, fuse))) != RTX_OK) return rc;
+    const LaneMem A = lane_mem_at(st->d_lane, ns, fuse);
     if ((rc = ensure(reinterpret_cast<void**>(&st->d_pbuf), &st->pbuf_bytes,
                      ns * pend_cap * 13 * sizeof(double))) != RTX_OK)
       return rc;
@@ -3548,6 +3676,14 @@ rtx_status rtx_render(void* scene, const RtxRenderParams* params, uint8_t* rgb8,
     for (int g = 1; g < G; ++g) HIP_TRY(hipStreamWaitEvent(stream, st->wf_join[size_t(g)], 0));
     HIP_TRY(hipEventRecord(e1, stream));
     frame_events.push_back({e0, e1});
+    if (fork_ok && st->bucket_hist.find(bkey) == st->bucket_hist.end() && !st->bstat_pending) {
+      // first render of this frame: its set count, read at the next call
+      HIP_TRY(hipMemcpyAsync(st->h_bstat, st->d_bstat, 2 * sizeof(unsigned int), hipMemcpyDeviceToHost, stream));
+      HIP_TRY(hipEventRecord(st->bstat_ev, stream));
+      st->bstat_pending = true;
+      st->bstat_key = bkey;
+    }
+    st->wf_call++;
     return RTX_OK;
   };
   if (!adaptive) {
