@@ -33,6 +33,11 @@ import time
 # set before any OpenMP runtime (torch's or the oracle's) initialises
 os.environ.setdefault("OMP_PROC_BIND", "close")
 os.environ.setdefault("OMP_PLACES", "cores")
+# Consecutive frames overlap on the scene's two frame contexts, each with its
+# slot groups on streams of its own (rtx_render, DESIGN.md "Frame
+# contexts"): with HIP's default of 4 hardware queues per process, the 2 x 3
+# group streams would share queues and serialise.  Read when HIP initialises.
+os.environ.setdefault("GPU_MAX_HW_QUEUES", "16")
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 METRIC = "Mrays/sec + frame ms, trimesh2.ray 1920×1080 depth-5 4×AA; 1/2/4/8 MI355X"
@@ -404,6 +409,23 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     kms, nlaunch = dev.kernel_time()
+    # one frame alone (the frame before it finished, no overlap): the
+    # latency of a frame, beside the throughput of back-to-back frames
+    lat = []
+    for _ in range(3):
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        t1 = time.perf_counter()
+        step()
+        torch.cuda.synchronize()
+        lat.append((time.perf_counter() - t1) * 1e3)
+    frame_latency_ms = sorted(lat)[1]
+    dev.kernel_time()  # (not part of the roofline's frames)
+    if world > 1:
+        t = torch.tensor([frame_latency_ms], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        frame_latency_ms = float(t.item())
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -508,6 +530,12 @@ def main():
             # rays counted as the reference traces them vs rays the GPU traced
             # (dark-light shadow rays are counted, not traced: DESIGN.md §2)
             "rays_traced_per_frame": traced_rays,
+            # frames are rendered back to back: frame k + 1 starts on the
+            # other frame context while frame k finishes; ms_per_step is the
+            # throughput, frame_latency_ms one frame rendered alone (render
+            # + gather, max over ranks)
+            "frame_latency_ms": round(frame_latency_ms, 3),
+            "frame_contexts": 2,
             "mrays_traced_per_s": round(traced_rays * args.steps / elapsed / 1e6, 3),
             "build": {"build_id": build_id(), "lib_sha256": lib_hash},
         }

@@ -2497,21 +2497,15 @@ thread_local std::string g_err;
     }                                                                            \
   } while (0)
 
-struct SceneState {
-  int device = 0;
-  DevScene S;
-  DevScene S_launch;
-  std::vector<void*> allocs;
-  RtxSceneDesc desc;           // shallow copy (pointers valid only during create)
-  RtxCamera cam;
-  std::vector<RtxLight> lights;
-  int stack_cap = 0;
-  int n_cu = 256;
+// Everything one frame writes on the device, with the streams its slot
+// groups run on.  A scene holds two: consecutive frames rendered into device
+// buffers without hit records or counters (bench.py's loop, bin/ray --gpus)
+// alternate between them, so frame k + 1's first, throughput-bound
+// iterations run while frame k's last, latency-bound ones finish (DESIGN.md
+// "Frame contexts"); every other render uses context 0 in caller-stream
+// order, as before.
+struct FrameCtx {
   FrameParams* d_frame = nullptr;
-  unsigned long long* d_work = nullptr;
-  unsigned long long* d_stats = nullptr;
-  double* d_picks = nullptr;
-  int picks_res = -1;
   double* d_offv = nullptr;     // DoF eye offsets
   size_t offv_bytes = 0;
   double* d_sbuf = nullptr;     // per-sample colours (HBM), grown on demand
@@ -2537,8 +2531,7 @@ struct SceneState {
   DevScene* d_scene = nullptr;         // device copy of S_launch (shadow early-out)
   unsigned int* d_acnt = nullptr;      // adaptive AA: regions to subdivide, emit cursor
   // pooled bucket sets (FrameParams.bidx): per unit its set index; pool
-  // counters [taken, refused]; the sets each frame (key: its parameters and
-  // its place in the render) took on its last render, read back once
+  // counters [taken, refused]; a first-time frame's count, read back later
   int* d_bidx = nullptr;
   size_t bidx_bytes = 0;
   unsigned int* d_bstat = nullptr;
@@ -2546,13 +2539,35 @@ struct SceneState {
   hipEvent_t bstat_ev = nullptr;
   bool bstat_pending = false;
   uint64_t bstat_key = 0;
-  std::map<uint64_t, uint32_t> bucket_hist;
   int wf_call = 0;  // run_wavefront calls of the current rtx_render
   // adaptive AA: one buffer per level (values, first-quarter index, mask,
   // regions), grown on demand and reused by later frames (no hipMalloc /
   // hipFree, which synchronises the device, per level per frame)
   std::vector<void*> d_level;
   std::vector<size_t> level_bytes;
+  hipEvent_t free_ev = nullptr;  // recorded on the caller's stream after the frame's last kernel
+  bool used = false;
+};
+
+struct SceneState {
+  int device = 0;
+  DevScene S;
+  DevScene S_launch;
+  std::vector<void*> allocs;
+  RtxSceneDesc desc;           // shallow copy (pointers valid only during create)
+  RtxCamera cam;
+  std::vector<RtxLight> lights;
+  int stack_cap = 0;
+  int n_cu = 256;
+  unsigned long long* d_work = nullptr;
+  unsigned long long* d_stats = nullptr;
+  double* d_picks = nullptr;
+  int picks_res = -1;
+  FrameCtx cx[2];
+  unsigned int next_cx = 0;
+  // the bucket sets each frame (key: its parameters and its place in the
+  // render) took on its last render
+  std::map<uint64_t, uint32_t> bucket_hist;
   int64_t last_work[RTX_STATS_N] = {};  // raw counters of the last counting render (rtx_last_work)
   std::vector<hipEvent_t> ev_pool;
   size_t ev_used = 0;
@@ -2777,7 +2792,8 @@ rtx_status rtx_scene_create(int device, const RtxSceneDesc* d, void** out) {
   }
   st->cam = d->camera;
   st->lights.assign(d->lights, d->lights + d->n_lights);
-  if (hipMalloc(&st->d_frame, sizeof(FrameParams)) != hipSuccess ||
+  if (hipMalloc(&st->cx[0].d_frame, sizeof(FrameParams)) != hipSuccess ||
+      hipMalloc(&st->cx[1].d_frame, sizeof(FrameParams)) != hipSuccess ||
       hipMalloc(&st->d_work, sizeof(unsigned long long)) != hipSuccess ||
       hipMalloc(&st->d_stats, RTX_STATS_N * sizeof(unsigned long long)) != hipSuccess) {
     g_err = "rtx_scene_create: hipMalloc failed";
@@ -2793,32 +2809,35 @@ rtx_status rtx_scene_destroy(void* scene) {
   SceneState* st = static_cast<SceneState*>(scene);
   (void)hipSetDevice(st->device);
   for (void* p : st->allocs) (void)hipFree(p);
-  if (st->d_frame) (void)hipFree(st->d_frame);
   if (st->d_work) (void)hipFree(st->d_work);
   if (st->d_stats) (void)hipFree(st->d_stats);
-  if (st->d_acnt) (void)hipFree(st->d_acnt);
-  if (st->d_bidx) (void)hipFree(st->d_bidx);
-  if (st->d_bstat) (void)hipFree(st->d_bstat);
-  if (st->h_bstat) (void)hipHostFree(st->h_bstat);
-  if (st->bstat_ev) (void)hipEventDestroy(st->bstat_ev);
-  for (void* p : st->d_level)
-    if (p) (void)hipFree(p);
   if (st->d_picks) (void)hipFree(st->d_picks);
-  if (st->d_offv) (void)hipFree(st->d_offv);
-  if (st->d_sbuf) (void)hipFree(st->d_sbuf);
-  if (st->d_pbuf) (void)hipFree(st->d_pbuf);
-  if (st->d_fbuf) (void)hipFree(st->d_fbuf);
-  if (st->d_fmask) (void)hipFree(st->d_fmask);
-  if (st->d_wterm) (void)hipFree(st->d_wterm);
-  if (st->d_wf) (void)hipFree(st->d_wf);
-  if (st->d_lane) (void)hipFree(st->d_lane);
-  for (auto e : st->wf_join) (void)hipEventDestroy(e);
-  for (auto e : st->wf_check) (void)hipEventDestroy(e);
-  if (st->wf_fork) (void)hipEventDestroy(st->wf_fork);
-  for (auto q : st->wf_streams) (void)hipStreamDestroy(q);
-  if (st->d_counters) (void)hipFree(st->d_counters);
-  if (st->h_counters) (void)hipHostFree(st->h_counters);
-  if (st->d_scene) (void)hipFree(st->d_scene);
+  for (FrameCtx& X : st->cx) {
+    if (X.d_frame) (void)hipFree(X.d_frame);
+    if (X.d_acnt) (void)hipFree(X.d_acnt);
+    if (X.d_bidx) (void)hipFree(X.d_bidx);
+    if (X.d_bstat) (void)hipFree(X.d_bstat);
+    if (X.h_bstat) (void)hipHostFree(X.h_bstat);
+    if (X.bstat_ev) (void)hipEventDestroy(X.bstat_ev);
+    for (void* p : X.d_level)
+      if (p) (void)hipFree(p);
+    if (X.d_offv) (void)hipFree(X.d_offv);
+    if (X.d_sbuf) (void)hipFree(X.d_sbuf);
+    if (X.d_pbuf) (void)hipFree(X.d_pbuf);
+    if (X.d_fbuf) (void)hipFree(X.d_fbuf);
+    if (X.d_fmask) (void)hipFree(X.d_fmask);
+    if (X.d_wterm) (void)hipFree(X.d_wterm);
+    if (X.d_wf) (void)hipFree(X.d_wf);
+    if (X.d_lane) (void)hipFree(X.d_lane);
+    for (auto e : X.wf_join) (void)hipEventDestroy(e);
+    for (auto e : X.wf_check) (void)hipEventDestroy(e);
+    if (X.wf_fork) (void)hipEventDestroy(X.wf_fork);
+    for (auto q : X.wf_streams) (void)hipStreamDestroy(q);
+    if (X.d_counters) (void)hipFree(X.d_counters);
+    if (X.h_counters) (void)hipHostFree(X.h_counters);
+    if (X.d_scene) (void)hipFree(X.d_scene);
+    if (X.free_ev) (void)hipEventDestroy(X.free_ev);
+  }
   for (auto e : st->ev_pool) (void)hipEventDestroy(e);
   for (auto e : st->ev_start) (void)hipEventDestroy(e);
   for (auto e : st->ev_stop) (void)hipEventDestroy(e);
@@ -2940,21 +2959,52 @@ rtx_status rtx_render(void* scene, const RtxRenderParams* params, uint8_t* rgb8,
   SceneState* st = static_cast<SceneState*>(scene);
   HIP_TRY(hipSetDevice(st->device));
   hipStream_t stream = static_cast<hipStream_t>(stream_v);
+  // Frame context (DESIGN.md "Frame contexts"): a render into device buffers
+  // with no hit records, counters or adaptive levels alternates between the
+  // scene's two contexts and runs on the context's own streams — after the
+  // context's previous frame only, so it can overlap the frame before it —
+  // and joins the caller's stream for its final reduce.  Every other render
+  // uses context 0 on the caller's stream, after whatever was queued there
+  // (RTX_PIPELINE=0: always that).
+  const char* mk_env0 = getenv("RTX_MEGAKERNEL");
+  const char* pipe_env = getenv("RTX_PIPELINE");
+  const bool pipelined = !(pipe_env && atoi(pipe_env) == 0) && device_ptrs && !hits && !stats &&
+                         params->aa_mode != RTX_AA_ADAPTIVE && !(mk_env0 && atoi(mk_env0) != 0);
+  FrameCtx* X = pipelined ? &st->cx[(st->next_cx++) & 1u] : &st->cx[0];
+  if (!X->free_ev) HIP_TRY(hipEventCreateWithFlags(&X->free_ev, hipEventDisableTiming));
+  if (X->wf_streams.empty()) {
+    hipStream_t s0;
+    HIP_TRY(hipStreamCreateWithFlags(&s0, hipStreamNonBlocking));
+    X->wf_streams.push_back(s0);
+    hipEvent_t ev;
+    HIP_TRY(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+    X->wf_join.push_back(ev);
+    HIP_TRY(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+    X->wf_check.push_back(ev);
+  }
+  hipStream_t ws = stream;  // the frame's work stream (slot group 0)
+  if (pipelined) {
+    ws = X->wf_streams[0];
+    if (X->used) HIP_TRY(hipStreamWaitEvent(ws, X->free_ev, 0));
+  } else {
+    for (FrameCtx& C : st->cx)  // (a pipelined frame may still run on the other context)
+      if (C.used) HIP_TRY(hipStreamWaitEvent(stream, C.free_ev, 0));
+  }
   FrameParams F;
   std::vector<double> offv;
   rtx_status rc = build_frame(st, params, F, offv);
   if (rc != RTX_OK) return rc;
   if (!offv.empty()) {
     const size_t need = offv.size() * sizeof(double);
-    if (need > st->offv_bytes) {
-      if (st->d_offv) (void)hipFree(st->d_offv);
-      st->d_offv = nullptr;
-      st->offv_bytes = 0;
-      HIP_TRY(hipMalloc(&st->d_offv, need));
-      st->offv_bytes = need;
+    if (need > X->offv_bytes) {
+      if (X->d_offv) (void)hipFree(X->d_offv);
+      X->d_offv = nullptr;
+      X->offv_bytes = 0;
+      HIP_TRY(hipMalloc(&X->d_offv, need));
+      X->offv_bytes = need;
     }
-    HIP_TRY(hipMemcpyAsync(st->d_offv, offv.data(), need, hipMemcpyHostToDevice, stream));
-    F.offv = st->d_offv;
+    HIP_TRY(hipMemcpyAsync(X->d_offv, offv.data(), need, hipMemcpyHostToDevice, ws));
+    F.offv = X->d_offv;
   }
   // area-light pick tables depend on ss_res
   st->S_launch = st->S;
@@ -2993,12 +3043,12 @@ rtx_status rtx_render(void* scene, const RtxRenderParams* params, uint8_t* rgb8,
     }
   } tmp;
   if (!device_ptrs) {
-    if (rgb8) { HIP_TRY(hipMalloc(&d_rgb8, npix * 3)); tmp.push_back(d_rgb8); HIP_TRY(hipMemsetAsync(d_rgb8, 0, npix * 3, stream)); }
-    if (rgb_f64) { HIP_TRY(hipMalloc(&d_rgbf, npix * 3 * sizeof(double))); tmp.push_back(d_rgbf); HIP_TRY(hipMemsetAsync(d_rgbf, 0, npix * 3 * sizeof(double), stream)); }
+    if (rgb8) { HIP_TRY(hipMalloc(&d_rgb8, npix * 3)); tmp.push_back(d_rgb8); HIP_TRY(hipMemsetAsync(d_rgb8, 0, npix * 3, ws)); }
+    if (rgb_f64) { HIP_TRY(hipMalloc(&d_rgbf, npix * 3 * sizeof(double))); tmp.push_back(d_rgbf); HIP_TRY(hipMemsetAsync(d_rgbf, 0, npix * 3 * sizeof(double), ws)); }
     if (hits) {
       HIP_TRY(hipMalloc(&d_hits, npix * F.spp * sizeof(RtxHitRecord)));
       tmp.push_back(d_hits);
-      HIP_TRY(hipMemsetAsync(d_hits, 0xff, npix * F.spp * sizeof(RtxHitRecord), stream));
+      HIP_TRY(hipMemsetAsync(d_hits, 0xff, npix * F.spp * sizeof(RtxHitRecord), ws));
     }
   }
   const bool adaptive = params->aa_mode == RTX_AA_ADAPTIVE;
@@ -3015,23 +3065,23 @@ rtx_status rtx_render(void* scene, const RtxRenderParams* params, uint8_t* rgb8,
     F.cam_split = 1;
     F.n_samples *= F.ncam;
   }
-  if (F.cam_split && hits) HIP_TRY(hipMemsetAsync(d_hits, 0xff, npix * F.spp * sizeof(RtxHitRecord), stream));
+  if (F.cam_split && hits) HIP_TRY(hipMemsetAsync(d_hits, 0xff, npix * F.spp * sizeof(RtxHitRecord), ws));
   if (!(adaptive && megakernel)) {
     const size_t need = size_t(npix) * F.spp * (F.cam_split ? F.ncam : 1) * 3 * sizeof(double);
-    if (need > st->sbuf_bytes) {
-      if (st->d_sbuf) (void)hipFree(st->d_sbuf);
-      st->d_sbuf = nullptr;
-      st->sbuf_bytes = 0;
-      HIP_TRY(hipMalloc(&st->d_sbuf, need));
-      st->sbuf_bytes = need;
+    if (need > X->sbuf_bytes) {
+      if (X->d_sbuf) (void)hipFree(X->d_sbuf);
+      X->d_sbuf = nullptr;
+      X->sbuf_bytes = 0;
+      HIP_TRY(hipMalloc(&X->d_sbuf, need));
+      X->sbuf_bytes = need;
     }
   }
-  HIP_TRY(hipMemsetAsync(st->d_work, 0, sizeof(unsigned long long), stream));
+  HIP_TRY(hipMemsetAsync(st->d_work, 0, sizeof(unsigned long long), ws));
   // device copy of the scene record: functions called out of line read it
   // through this pointer (a kernel-argument copy has no address)
-  if (!st->d_scene) HIP_TRY(hipMalloc(&st->d_scene, sizeof(DevScene)));
-  HIP_TRY(hipMemcpyAsync(st->d_scene, &st->S_launch, sizeof(DevScene), hipMemcpyHostToDevice, stream));
-  if (stats) HIP_TRY(hipMemsetAsync(st->d_stats, 0, RTX_STATS_N * sizeof(unsigned long long), stream));
+  if (!X->d_scene) HIP_TRY(hipMalloc(&X->d_scene, sizeof(DevScene)));
+  HIP_TRY(hipMemcpyAsync(X->d_scene, &st->S_launch, sizeof(DevScene), hipMemcpyHostToDevice, ws));
+  if (stats) HIP_TRY(hipMemsetAsync(st->d_stats, 0, RTX_STATS_N * sizeof(unsigned long long), ws));
   const int pend_cap = (params->depth > 0 ? params->depth : 0) + 2;
   auto get_event = [&](hipEvent_t* e) -> rtx_status {
     if (!st->ev_pool.empty()) {
@@ -3052,9 +3102,9 @@ rtx_status rtx_render(void* scene, const RtxRenderParams* params, uint8_t* rgb8,
     }
     return RTX_OK;
   };
-  double* sb = adaptive && megakernel ? nullptr : st->d_sbuf;
+  double* sb = adaptive && megakernel ? nullptr : X->d_sbuf;
   std::vector<std::pair<hipEvent_t, hipEvent_t>> frame_events;
-  st->wf_call = 0;
+  X->wf_call = 0;
 
   if (megakernel) {
     const int cslots = adaptive ? (F.spp > 64 ? F.spp : 64) : 0;
@@ -3090,28 +3140,28 @@ rtx_status rtx_render(void* scene, const RtxRenderParams* params, uint8_t* rgb8,
       if (c > QCHUNK) c = QCHUNK;
       F.qchunk = static_cast<int>(c);
     }
-    HIP_TRY(hipMemcpyAsync(st->d_frame, &F, sizeof(FrameParams), hipMemcpyHostToDevice, stream));
-    if ((rc = ensure(reinterpret_cast<void**>(&st->d_pbuf), &st->pbuf_bytes,
+    HIP_TRY(hipMemcpyAsync(X->d_frame, &F, sizeof(FrameParams), hipMemcpyHostToDevice, ws));
+    if ((rc = ensure(reinterpret_cast<void**>(&X->d_pbuf), &X->pbuf_bytes,
                      size_t(grid) * WG * pend_cap * 13 * sizeof(double))) != RTX_OK)
       return rc;
-    if ((rc = ensure(&st->d_lane, &st->lane_bytes, lane_mem_bytes(size_t(grid) * WG))) != RTX_OK) return rc;
-    const LaneMem lm = lane_mem_at(st->d_lane, size_t(grid) * WG);
+    if ((rc = ensure(&X->d_lane, &X->lane_bytes, lane_mem_bytes(size_t(grid) * WG))) != RTX_OK) return rc;
+    const LaneMem lm = lane_mem_at(X->d_lane, size_t(grid) * WG);
     hipEvent_t e0, e1;
     if ((rc = get_event(&e0)) != RTX_OK || (rc = get_event(&e1)) != RTX_OK) return rc;
-    HIP_TRY(hipEventRecord(e0, stream));
+    HIP_TRY(hipEventRecord(e0, ws));
     dispatch2(stats, adaptive, [&](auto st_, auto ad_) {
       constexpr bool ST_ = decltype(st_)::value, AD_ = decltype(ad_)::value;
       if (media)
-        hipLaunchKernelGGL((render_kernel<ST_, AD_, true>), dim3(grid), dim3(WG), lds, stream, st->S_launch,
-                           st->d_scene, st->d_frame, st->d_work, sb, d_hits, d_rgb8, d_rgbf, st->d_stats, st->stack_cap,
-                           st->d_pbuf, pend_cap, lm);
+        hipLaunchKernelGGL((render_kernel<ST_, AD_, true>), dim3(grid), dim3(WG), lds, ws, st->S_launch,
+                           X->d_scene, X->d_frame, st->d_work, sb, d_hits, d_rgb8, d_rgbf, st->d_stats, st->stack_cap,
+                           X->d_pbuf, pend_cap, lm);
       else
-        hipLaunchKernelGGL((render_kernel<ST_, AD_, false>), dim3(grid), dim3(WG), lds, stream, st->S_launch,
-                           st->d_scene, st->d_frame, st->d_work, sb, d_hits, d_rgb8, d_rgbf, st->d_stats, st->stack_cap,
-                           st->d_pbuf, pend_cap, lm);
+        hipLaunchKernelGGL((render_kernel<ST_, AD_, false>), dim3(grid), dim3(WG), lds, ws, st->S_launch,
+                           X->d_scene, X->d_frame, st->d_work, sb, d_hits, d_rgb8, d_rgbf, st->d_stats, st->stack_cap,
+                           X->d_pbuf, pend_cap, lm);
     });
     HIP_TRY(hipGetLastError());
-    HIP_TRY(hipEventRecord(e1, stream));
+    HIP_TRY(hipEventRecord(e1, ws));
     frame_events.push_back({e0, e1});
   }
   // One run of the wavefront machine over F's work units (F.n_samples), whose
@@ -3121,7 +3171,7 @@ rtx_status rtx_render(void* scene, const RtxRenderParams* params, uint8_t* rgb8,
   auto run_wavefront = [&](FrameParams& F, int64_t nout, bool level0) -> rtx_status {
     // ---------------- wavefront path
     // NSLOT path slots split into G groups, each iterating advance -> trace
-    // (closest) -> trace (next) on its own stream, so one group's launch
+    // (closest) -> trace (next) on its own ws, so one group's launch
     // tails overlap the other groups' work.
     int64_t nslot64 = static_cast<int64_t>(st->n_cu) * 49152;  // 12.6 M on 256 CUs (tools/gpu_exp*.sh sweeps)
     const char* ns_env = getenv("RTX_SLOTS");
@@ -3172,17 +3222,17 @@ rtx_status rtx_render(void* scene, const RtxRenderParams* params, uint8_t* rgb8,
         for (size_t k = 0; k < n; ++k) bkey = (bkey ^ c[k]) * 1099511628211ull;
       };
       mix(&F.P, sizeof(F.P));
-      const int64_t ks[6] = {F.n_samples, nout, level0 ? 1 : 0, st->wf_call, int64_t(npos_b), int64_t(nunit_out)};
+      const int64_t ks[6] = {F.n_samples, nout, level0 ? 1 : 0, X->wf_call, int64_t(npos_b), int64_t(nunit_out)};
       mix(ks, sizeof(ks));
-      if (st->bstat_pending) {  // the last first-time frame's count (long done by now)
-        HIP_TRY(hipEventSynchronize(st->bstat_ev));
-        if (st->h_bstat[1] == 0u) {
-          st->bucket_hist[st->bstat_key] = st->h_bstat[0];
+      if (X->bstat_pending) {  // the last first-time frame's count (long done by now)
+        HIP_TRY(hipEventSynchronize(X->bstat_ev));
+        if (X->h_bstat[1] == 0u) {
+          st->bucket_hist[X->bstat_key] = X->h_bstat[0];
         } else {
-          fprintf(stderr, "rtx_render: bucket pool refused a set (%u taken); frame pool reset\n", st->h_bstat[0]);
-          st->bucket_hist.erase(st->bstat_key);
+          fprintf(stderr, "rtx_render: bucket pool refused a set (%u taken); frame pool reset\n", X->h_bstat[0]);
+          st->bucket_hist.erase(X->bstat_key);
         }
-        st->bstat_pending = false;
+        X->bstat_pending = false;
       }
       const auto it = st->bucket_hist.find(bkey);
       if (it != st->bucket_hist.end()) bcap = std::min<size_t>(nunit_out, size_t(it->second) + 64);
@@ -3193,7 +3243,7 @@ rtx_status rtx_render(void* scene, const RtxRenderParams* params, uint8_t* rgb8,
       size_t freeb = 0, totb = 0;
       HIP_TRY(hipMemGetInfo(&freeb, &totb));
       const size_t held =
-          st->lane_bytes + st->pbuf_bytes + st->wf_bytes + st->fbuf_bytes + st->fmask_bytes + st->wterm_bytes;
+          X->lane_bytes + X->pbuf_bytes + X->wf_bytes + X->fbuf_bytes + X->fmask_bytes + X->wterm_bytes;
       const size_t sbuf_need = size_t(npix) * F.spp * 3 * sizeof(double);
       const size_t avail = freeb + held > sbuf_need ? (freeb + held - sbuf_need) / 10 * 8 : 0;
       const size_t npos = (size_t(1) << (fork_depth + 1)) - 2;
@@ -3251,29 +3301,29 @@ rtx_status rtx_render(void* scene, const RtxRenderParams* params, uint8_t* rgb8,
     if (fork_ok) {
       const size_t nsamp_out = size_t(nout) * F.spp;
       const size_t fbuf_need = std::max<size_t>(1, bcap) * F.fork_npos * 3 * sizeof(double);
-      if (st->fbuf_bytes > 2 * fbuf_need + (size_t(64) << 20)) {  // a smaller pool than the first render's: give it back
-        (void)hipFree(st->d_fbuf);
-        st->d_fbuf = nullptr;
-        st->fbuf_bytes = 0;
+      if (X->fbuf_bytes > 2 * fbuf_need + (size_t(64) << 20)) {  // a smaller pool than the first render's: give it back
+        (void)hipFree(X->d_fbuf);
+        X->d_fbuf = nullptr;
+        X->fbuf_bytes = 0;
       }
-      if ((rc = ensure(reinterpret_cast<void**>(&st->d_fbuf), &st->fbuf_bytes, fbuf_need)) != RTX_OK) return rc;
-      if ((rc = ensure(reinterpret_cast<void**>(&st->d_fmask), &st->fmask_bytes, nunit_out * sizeof(unsigned int))) !=
+      if ((rc = ensure(reinterpret_cast<void**>(&X->d_fbuf), &X->fbuf_bytes, fbuf_need)) != RTX_OK) return rc;
+      if ((rc = ensure(reinterpret_cast<void**>(&X->d_fmask), &X->fmask_bytes, nunit_out * sizeof(unsigned int))) !=
           RTX_OK)
         return rc;
-      if ((rc = ensure(reinterpret_cast<void**>(&st->d_bidx), &st->bidx_bytes, nunit_out * sizeof(int))) != RTX_OK)
+      if ((rc = ensure(reinterpret_cast<void**>(&X->d_bidx), &X->bidx_bytes, nunit_out * sizeof(int))) != RTX_OK)
         return rc;
-      if (!st->d_bstat) HIP_TRY(hipMalloc(&st->d_bstat, 4 * sizeof(unsigned int)));
-      if (!st->h_bstat) HIP_TRY(hipHostMalloc(&st->h_bstat, 4 * sizeof(unsigned int)));
-      if (!st->bstat_ev) HIP_TRY(hipEventCreateWithFlags(&st->bstat_ev, hipEventDisableTiming));
-      HIP_TRY(hipMemsetAsync(st->d_bstat, 0, 4 * sizeof(unsigned int), stream));
-      F.fbuf = st->d_fbuf;
-      F.fmask = st->d_fmask;
-      F.bidx = st->d_bidx;
-      F.bcnt = st->d_bstat;
-      F.bover = st->d_bstat + 1;
+      if (!X->d_bstat) HIP_TRY(hipMalloc(&X->d_bstat, 4 * sizeof(unsigned int)));
+      if (!X->h_bstat) HIP_TRY(hipHostMalloc(&X->h_bstat, 4 * sizeof(unsigned int)));
+      if (!X->bstat_ev) HIP_TRY(hipEventCreateWithFlags(&X->bstat_ev, hipEventDisableTiming));
+      HIP_TRY(hipMemsetAsync(X->d_bstat, 0, 4 * sizeof(unsigned int), ws));
+      F.fbuf = X->d_fbuf;
+      F.fmask = X->d_fmask;
+      F.bidx = X->d_bidx;
+      F.bcnt = X->d_bstat;
+      F.bover = X->d_bstat + 1;
       F.bcap = static_cast<int>(std::min<size_t>(bcap, size_t(INT32_MAX)));
       // fmask[sample] is cleared when the sample is claimed (claim_sample)
-      if (hits && level0) HIP_TRY(hipMemsetAsync(d_hits, 0xff, nsamp_out * sizeof(RtxHitRecord), stream));
+      if (hits && level0) HIP_TRY(hipMemsetAsync(d_hits, 0xff, nsamp_out * sizeof(RtxHitRecord), ws));
     }
     const size_t ns = static_cast<size_t>(nslot64);
     const size_t gs = static_cast<size_t>(gslots);
@@ -3284,40 +3334,40 @@ rtx_status rtx_render(void* scene, const RtxRenderParams* params, uint8_t* rgb8,
     const size_t bytes_qc = al(gs * sizeof(int)) + al(gs * QL_D * sizeof(double)) + al(gs * 2 * sizeof(int));
     const size_t nd = fuse ? QF_D : QL_D, ni = fuse ? QF_I : 2;
     const size_t bytes_qn = al(capn * sizeof(int)) + al(capn * nd * sizeof(double)) + al(capn * ni * sizeof(int));
-    if ((rc = ensure(&st->d_wf, &st->wf_bytes, size_t(G) * (bytes_qc + bytes_qn + 2 * al(gs * sizeof(int))))) != RTX_OK)
+    if ((rc = ensure(&X->d_wf, &X->wf_bytes, size_t(G) * (bytes_qc + bytes_qn + 2 * al(gs * sizeof(int))))) != RTX_OK)
       return rc;
     F.fuse = fuse ? 1 : 0;
     F.wterm = nullptr;
     if (fuse && nl > 0) {
-      if ((rc = ensure(reinterpret_cast<void**>(&st->d_wterm), &st->wterm_bytes, nl * ns * 3 * sizeof(double))) !=
+      if ((rc = ensure(reinterpret_cast<void**>(&X->d_wterm), &X->wterm_bytes, nl * ns * 3 * sizeof(double))) !=
           RTX_OK)
         return rc;
-      F.wterm = st->d_wterm;
+      F.wterm = X->d_wterm;
     }
-    if ((rc = ensure(&st->d_lane, &st->lane_bytes, lane_mem_bytes(ns, fuse))) != RTX_OK) return rc;
-    const LaneMem A = lane_mem_at(st->d_lane, ns, fuse);
-    if ((rc = ensure(reinterpret_cast<void**>(&st->d_pbuf), &st->pbuf_bytes,
+    if ((rc = ensure(&X->d_lane, &X->lane_bytes, lane_mem_bytes(ns, fuse))) != RTX_OK) return rc;
+    const LaneMem A = lane_mem_at(X->d_lane, ns, fuse);
+    if ((rc = ensure(reinterpret_cast<void**>(&X->d_pbuf), &X->pbuf_bytes,
                      ns * pend_cap * 13 * sizeof(double))) != RTX_OK)
       return rc;
-    if (!st->d_counters) HIP_TRY(hipMalloc(&st->d_counters, 16 * CNT_PER_GROUP * sizeof(unsigned int)));
-    if (!st->h_counters) HIP_TRY(hipHostMalloc(&st->h_counters, 16 * CNT_PER_GROUP * sizeof(unsigned int)));
-    // group 0 runs on the caller's stream, groups 1.. on their own streams
+    if (!X->d_counters) HIP_TRY(hipMalloc(&X->d_counters, 16 * CNT_PER_GROUP * sizeof(unsigned int)));
+    if (!X->h_counters) HIP_TRY(hipHostMalloc(&X->h_counters, 16 * CNT_PER_GROUP * sizeof(unsigned int)));
+    // group 0 runs on the caller's ws, groups 1.. on their own streams
     // (GPU_MAX_HW_QUEUES is 4 by default: more streams than queues would
     // serialize groups behind each other)
-    while (static_cast<int>(st->wf_streams.size()) < G) {
+    while (static_cast<int>(X->wf_streams.size()) < G) {
       hipStream_t s2;
       HIP_TRY(hipStreamCreateWithFlags(&s2, hipStreamNonBlocking));
-      st->wf_streams.push_back(s2);
+      X->wf_streams.push_back(s2);
       hipEvent_t ev;
       HIP_TRY(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
-      st->wf_join.push_back(ev);
+      X->wf_join.push_back(ev);
       HIP_TRY(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
-      st->wf_check.push_back(ev);
+      X->wf_check.push_back(ev);
     }
-    if (!st->wf_fork) HIP_TRY(hipEventCreateWithFlags(&st->wf_fork, hipEventDisableTiming));
+    if (!X->wf_fork) HIP_TRY(hipEventCreateWithFlags(&X->wf_fork, hipEventDisableTiming));
     std::vector<QList> ql(size_t(G) * 2);
     {
-      char* base = static_cast<char*>(st->d_wf);
+      char* base = static_cast<char*>(X->d_wf);
       for (size_t m = 0; m < ql.size(); ++m) {
         const size_t cap = (m & 1) ? capn : gs, dn = (m & 1) ? nd : QL_D;
         ql[m].slot = reinterpret_cast<int*>(base);
@@ -3329,7 +3379,7 @@ rtx_status rtx_render(void* scene, const RtxRenderParams* params, uint8_t* rgb8,
     }
     std::vector<int*> live(size_t(G) * 2);  // [g * 2 + 0]: list A, [g * 2 + 1]: list B
     {
-      char* base = static_cast<char*>(st->d_wf) + size_t(G) * (bytes_qc + bytes_qn);
+      char* base = static_cast<char*>(X->d_wf) + size_t(G) * (bytes_qc + bytes_qn);
       for (size_t k = 0; k < live.size(); ++k) {
         live[k] = reinterpret_cast<int*>(base);
         base += al(gs * sizeof(int));
@@ -3385,11 +3435,11 @@ rtx_status rtx_render(void* scene, const RtxRenderParams* params, uint8_t* rgb8,
       }
       cam_n[size_t(g)] = static_cast<int>(c);
     }
-    HIP_TRY(hipMemcpyAsync(st->d_frame, &F, sizeof(FrameParams), hipMemcpyHostToDevice, stream));
+    HIP_TRY(hipMemcpyAsync(X->d_frame, &F, sizeof(FrameParams), hipMemcpyHostToDevice, ws));
     // every slot starts ST_IDLE, kdone = 0, outside a discoverMat walk, no
     // deferred colour: set by the group's first advance_kernel, which visits
     // all of its slots (every other field is written before it is read)
-    HIP_TRY(hipMemsetAsync(st->d_counters, 0, 16 * CNT_PER_GROUP * sizeof(unsigned int), stream));
+    HIP_TRY(hipMemsetAsync(X->d_counters, 0, 16 * CNT_PER_GROUP * sizeof(unsigned int), ws));
     const size_t lds_stacks = size_t(st->stack_cap) * 64 * sizeof(int) * WAVES_PER_WG;
 #ifdef RTX_LDS_STAGE
     const size_t lds = lds_stacks + size_t((S.n_srec <= RTX_LDS_SREC ? S.n_srec : 0) + S.n_mhot) * sizeof(DevNode4);
@@ -3457,16 +3507,16 @@ rtx_status rtx_render(void* scene, const RtxRenderParams* params, uint8_t* rgb8,
     }
     hipEvent_t e0, e1;
     if ((rc = get_event(&e0)) != RTX_OK || (rc = get_event(&e1)) != RTX_OK) return rc;
-    HIP_TRY(hipEventRecord(e0, stream));
-    HIP_TRY(hipEventRecord(st->wf_fork, stream));
-    for (int g = 1; g < G; ++g) HIP_TRY(hipStreamWaitEvent(st->wf_streams[size_t(g)], st->wf_fork, 0));
+    HIP_TRY(hipEventRecord(e0, ws));
+    HIP_TRY(hipEventRecord(X->wf_fork, ws));
+    for (int g = 1; g < G; ++g) HIP_TRY(hipStreamWaitEvent(X->wf_streams[size_t(g)], X->wf_fork, 0));
     std::vector<int> done(size_t(G), 0), pending_check(size_t(G), -1);
     int ndone = 0;
     for (int it = 0; ndone < G; ++it) {
       for (int g = 0; g < G; ++g) {
         if (done[size_t(g)]) continue;
-        hipStream_t sg = g == 0 ? stream : st->wf_streams[size_t(g)];
-        unsigned int* cnt = st->d_counters + CNT_PER_GROUP * g;
+        hipStream_t sg = g == 0 ? ws : X->wf_streams[size_t(g)];
+        unsigned int* cnt = X->d_counters + CNT_PER_GROUP * g;
         const QList& q0 = ql[size_t(g) * 2];
         const QList& q1 = ql[size_t(g) * 2 + 1];
         // (after a claiming first launch, iteration 1 visits every slot by
@@ -3481,24 +3531,24 @@ rtx_status rtx_render(void* scene, const RtxRenderParams* params, uint8_t* rgb8,
           const int64_t grid = std::max<int64_t>(1, (lb + WG - 1) / WG);
           if (fuse) {
             if (stats)
-              hipLaunchKernelGGL((tail_fused_kernel<true>), dim3(grid), dim3(WG), lds, sg, S, st->d_scene, st->d_frame,
-                                 A, sb, d_hits, st->d_pbuf, pend_cap, cnt, live_in, in_cnt, st->stack_cap, st->d_stats,
+              hipLaunchKernelGGL((tail_fused_kernel<true>), dim3(grid), dim3(WG), lds, sg, S, X->d_scene, X->d_frame,
+                                 A, sb, d_hits, X->d_pbuf, pend_cap, cnt, live_in, in_cnt, st->stack_cap, st->d_stats,
                                  ql[size_t(g) * 2 + 1], static_cast<int>(g * gslots));
             else
-              hipLaunchKernelGGL((tail_fused_kernel<false>), dim3(grid), dim3(WG), lds, sg, S, st->d_scene, st->d_frame,
-                                 A, sb, d_hits, st->d_pbuf, pend_cap, cnt, live_in, in_cnt, st->stack_cap, st->d_stats,
+              hipLaunchKernelGGL((tail_fused_kernel<false>), dim3(grid), dim3(WG), lds, sg, S, X->d_scene, X->d_frame,
+                                 A, sb, d_hits, X->d_pbuf, pend_cap, cnt, live_in, in_cnt, st->stack_cap, st->d_stats,
                                  ql[size_t(g) * 2 + 1], static_cast<int>(g * gslots));
           } else {
             dispatch2(stats, media, [&](auto st_, auto md_) {
               hipLaunchKernelGGL((tail_kernel<decltype(st_)::value, decltype(md_)::value>), dim3(grid), dim3(WG), lds,
-                                 sg, S, st->d_scene, st->d_frame, A, sb, d_hits, st->d_pbuf, pend_cap, cnt, live_in,
+                                 sg, S, X->d_scene, X->d_frame, A, sb, d_hits, X->d_pbuf, pend_cap, cnt, live_in,
                                  in_cnt, st->stack_cap, st->d_stats);
             });
           }
           HIP_TRY(hipGetLastError());
           done[size_t(g)] = 1;
           ++ndone;
-          HIP_TRY(hipEventRecord(st->wf_join[size_t(g)], sg));
+          HIP_TRY(hipEventRecord(X->wf_join[size_t(g)], sg));
           continue;
         }
         // ping-pong live-slot lists: even iterations append to A, read B
@@ -3527,7 +3577,7 @@ rtx_status rtx_render(void* scene, const RtxRenderParams* params, uint8_t* rgb8,
         } else if (fuse) {
           dispatch2(stats, fork, [&](auto st_, auto fk_) {
             hipLaunchKernelGGL((advance_fused_kernel<decltype(st_)::value, decltype(fk_)::value>), dim3(agrid),
-                               dim3(WG), 0, sg, S, st->d_scene, st->d_frame, A, sb, d_hits, st->d_pbuf, pend_cap, q0,
+                               dim3(WG), 0, sg, S, X->d_scene, X->d_frame, A, sb, d_hits, X->d_pbuf, pend_cap, q0,
                                q1, cnt, st->d_stats, static_cast<int>(g * gslots), live_in, live_out, first, in_cnt,
                                out_cnt);
           });
@@ -3535,7 +3585,7 @@ rtx_status rtx_render(void* scene, const RtxRenderParams* params, uint8_t* rgb8,
           dispatch3(stats, media, fork, [&](auto st_, auto md_, auto fk_) {
             hipLaunchKernelGGL((advance_kernel<decltype(st_)::value, decltype(md_)::value, decltype(fk_)::value>),
                                dim3(agrid), dim3(WG), 0, sg,
-                               S, st->d_scene, st->d_frame, A, sb, d_hits, st->d_pbuf, pend_cap, q0, q1, cnt,
+                               S, X->d_scene, X->d_frame, A, sb, d_hits, X->d_pbuf, pend_cap, q0, q1, cnt,
                                st->d_stats, static_cast<int>(g * gslots), live_in, live_out, first, in_cnt, out_cnt);
           });
         }
@@ -3546,9 +3596,9 @@ rtx_status rtx_render(void* scene, const RtxRenderParams* params, uint8_t* rgb8,
         std::memset(&sa, 0, sizeof(sa));
         sa.leaf_k = it == 0 ? leaf_k : leaf_k_late;
         if (fuse) {
-          sa.Fp = st->d_frame;
+          sa.Fp = X->d_frame;
           sa.hits = d_hits;
-          sa.pbuf = st->d_pbuf;
+          sa.pbuf = X->d_pbuf;
           sa.pend_cap = pend_cap;
           sa.qn = q1;
           sa.slot_off = static_cast<int>(g * gslots);
@@ -3571,10 +3621,10 @@ rtx_status rtx_render(void* scene, const RtxRenderParams* params, uint8_t* rgb8,
             }
             if (cam_it)
               hipLaunchKernelGGL((trace_kernel<ST_, Q_CLOSEST, true, FK_, true>), dim3(tg), dim3(WG), lds, sg, S,
-                                 st->d_scene, q0, cnt, A, st->stack_cap, st->d_stats, st->d_wterm, sa, -1);
+                                 X->d_scene, q0, cnt, A, st->stack_cap, st->d_stats, X->d_wterm, sa, -1);
             else
               hipLaunchKernelGGL((trace_kernel<ST_, Q_CLOSEST, true, FK_>), dim3(tg), dim3(WG), lds, sg, S,
-                                 st->d_scene, q0, cnt, A, st->stack_cap, st->d_stats, st->d_wterm, sa, -1);
+                                 X->d_scene, q0, cnt, A, st->stack_cap, st->d_stats, X->d_wterm, sa, -1);
             if (dbg_level >= 2) {
               unsigned int hc[CNT_PER_GROUP];
               unsigned long long hs[4] = {0, 0, 0, 0}, hw[4] = {0, 0, 0, 0};
@@ -3599,8 +3649,8 @@ rtx_status rtx_render(void* scene, const RtxRenderParams* params, uint8_t* rgb8,
               (void)(hipEventCreate(&d1));
               (void)(hipEventRecord(d0, sg));
             }
-            hipLaunchKernelGGL((trace_kernel<ST_, Q_NEXT, true>), dim3(tgn), dim3(WG), lds, sg, S, st->d_scene, q1,
-                               cnt, A, st->stack_cap, st->d_stats, st->d_wterm, sa, clr_next);
+            hipLaunchKernelGGL((trace_kernel<ST_, Q_NEXT, true>), dim3(tgn), dim3(WG), lds, sg, S, X->d_scene, q1,
+                               cnt, A, st->stack_cap, st->d_stats, X->d_wterm, sa, clr_next);
             if (dbg_level >= 2) {
               float ms = 0.f;
               unsigned long long hw[4] = {0, 0, 0, 0}, hs2[4] = {0, 0, 0, 0};
@@ -3618,22 +3668,22 @@ rtx_status rtx_render(void* scene, const RtxRenderParams* params, uint8_t* rgb8,
               (void)(hipEventDestroy(d1));
             }
           } else if (!FK_) {
-            hipLaunchKernelGGL((trace_kernel<ST_, Q_CLOSEST>), dim3(tg), dim3(WG), lds, sg, S, st->d_scene, q0, cnt, A,
+            hipLaunchKernelGGL((trace_kernel<ST_, Q_CLOSEST>), dim3(tg), dim3(WG), lds, sg, S, X->d_scene, q0, cnt, A,
                                st->stack_cap, st->d_stats, nullptr, sa, -1);
-            hipLaunchKernelGGL((trace_kernel<ST_, Q_NEXT>), dim3(tg), dim3(WG), lds, sg, S, st->d_scene, q1, cnt, A,
+            hipLaunchKernelGGL((trace_kernel<ST_, Q_NEXT>), dim3(tg), dim3(WG), lds, sg, S, X->d_scene, q1, cnt, A,
                                st->stack_cap, st->d_stats, nullptr, sa, clr_next);
           }
         });
         if (!fuse && fork) {  // the sequential machine's trace kernels do not depend on forking
           if (stats) {
-            hipLaunchKernelGGL((trace_kernel<true, Q_CLOSEST>), dim3(tg), dim3(WG), lds, sg, S, st->d_scene, q0, cnt,
+            hipLaunchKernelGGL((trace_kernel<true, Q_CLOSEST>), dim3(tg), dim3(WG), lds, sg, S, X->d_scene, q0, cnt,
                                A, st->stack_cap, st->d_stats, nullptr, sa, -1);
-            hipLaunchKernelGGL((trace_kernel<true, Q_NEXT>), dim3(tg), dim3(WG), lds, sg, S, st->d_scene, q1, cnt, A,
+            hipLaunchKernelGGL((trace_kernel<true, Q_NEXT>), dim3(tg), dim3(WG), lds, sg, S, X->d_scene, q1, cnt, A,
                                st->stack_cap, st->d_stats, nullptr, sa, clr_next);
           } else {
-            hipLaunchKernelGGL((trace_kernel<false, Q_CLOSEST>), dim3(tg), dim3(WG), lds, sg, S, st->d_scene, q0, cnt,
+            hipLaunchKernelGGL((trace_kernel<false, Q_CLOSEST>), dim3(tg), dim3(WG), lds, sg, S, X->d_scene, q0, cnt,
                                A, st->stack_cap, st->d_stats, nullptr, sa, -1);
-            hipLaunchKernelGGL((trace_kernel<false, Q_NEXT>), dim3(tg), dim3(WG), lds, sg, S, st->d_scene, q1, cnt, A,
+            hipLaunchKernelGGL((trace_kernel<false, Q_NEXT>), dim3(tg), dim3(WG), lds, sg, S, X->d_scene, q1, cnt, A,
                                st->stack_cap, st->d_stats, nullptr, sa, clr_next);
           }
         }
@@ -3643,8 +3693,8 @@ rtx_status rtx_render(void* scene, const RtxRenderParams* params, uint8_t* rgb8,
           // enqueued one round earlier (the GPU keeps ~check_every
           // iterations of this group queued meanwhile)
           if (pending_check[size_t(g)] >= 0) {
-            HIP_TRY(hipEventSynchronize(st->wf_check[size_t(g)]));
-            const unsigned int* hc = st->h_counters + CNT_PER_GROUP * g;
+            HIP_TRY(hipEventSynchronize(X->wf_check[size_t(g)]));
+            const unsigned int* hc = X->h_counters + CNT_PER_GROUP * g;
             const unsigned int alive = hc[(pending_check[size_t(g)] & 1) ? CNT_ALIVE_B : CNT_ALIVE_A];
             live_bound[size_t(g)] = alive;
             // forks add live slots: bound by the fork slots still free
@@ -3658,13 +3708,13 @@ rtx_status rtx_render(void* scene, const RtxRenderParams* params, uint8_t* rgb8,
             if (alive == 0) {
               done[size_t(g)] = 1;
               ++ndone;
-              HIP_TRY(hipEventRecord(st->wf_join[size_t(g)], sg));
+              HIP_TRY(hipEventRecord(X->wf_join[size_t(g)], sg));
               continue;
             }
           }
-          HIP_TRY(hipMemcpyAsync(st->h_counters + CNT_PER_GROUP * g, cnt, CNT_PER_GROUP * sizeof(unsigned int),
+          HIP_TRY(hipMemcpyAsync(X->h_counters + CNT_PER_GROUP * g, cnt, CNT_PER_GROUP * sizeof(unsigned int),
                                  hipMemcpyDeviceToHost, sg));
-          HIP_TRY(hipEventRecord(st->wf_check[size_t(g)], sg));
+          HIP_TRY(hipEventRecord(X->wf_check[size_t(g)], sg));
           pending_check[size_t(g)] = it;
         }
       }
@@ -3673,24 +3723,28 @@ rtx_status rtx_render(void* scene, const RtxRenderParams* params, uint8_t* rgb8,
         return RTX_ERR_INVALID;
       }
     }
-    for (int g = 1; g < G; ++g) HIP_TRY(hipStreamWaitEvent(stream, st->wf_join[size_t(g)], 0));
-    HIP_TRY(hipEventRecord(e1, stream));
+    for (int g = 1; g < G; ++g) HIP_TRY(hipStreamWaitEvent(ws, X->wf_join[size_t(g)], 0));
+    HIP_TRY(hipEventRecord(e1, ws));
     frame_events.push_back({e0, e1});
-    if (fork_ok && st->bucket_hist.find(bkey) == st->bucket_hist.end() && !st->bstat_pending) {
+    if (fork_ok && st->bucket_hist.find(bkey) == st->bucket_hist.end() && !X->bstat_pending) {
       // first render of this frame: its set count, read at the next call
-      HIP_TRY(hipMemcpyAsync(st->h_bstat, st->d_bstat, 2 * sizeof(unsigned int), hipMemcpyDeviceToHost, stream));
-      HIP_TRY(hipEventRecord(st->bstat_ev, stream));
-      st->bstat_pending = true;
-      st->bstat_key = bkey;
+      HIP_TRY(hipMemcpyAsync(X->h_bstat, X->d_bstat, 2 * sizeof(unsigned int), hipMemcpyDeviceToHost, ws));
+      HIP_TRY(hipEventRecord(X->bstat_ev, ws));
+      X->bstat_pending = true;
+      X->bstat_key = bkey;
     }
-    st->wf_call++;
+    X->wf_call++;
     return RTX_OK;
   };
   if (!adaptive) {
     if (!megakernel && (rc = run_wavefront(F, npix, true)) != RTX_OK) return rc;
+    if (ws != stream) {  // the caller's stream waits for the frame (its group-0 stream, joined by the others)
+      HIP_TRY(hipEventRecord(X->wf_join[0], ws));
+      HIP_TRY(hipStreamWaitEvent(stream, X->wf_join[0], 0));
+    }
     const int64_t ppb = WG / F.spp;
     const int64_t rblocks = (npix + ppb - 1) / ppb;
-    hipLaunchKernelGGL(reduce_kernel, dim3(rblocks), dim3(WG), 0, stream, st->d_frame, sb, d_rgb8, d_rgbf, npix);
+    hipLaunchKernelGGL(reduce_kernel, dim3(rblocks), dim3(WG), 0, stream, X->d_frame, sb, d_rgb8, d_rgbf, npix);
     HIP_TRY(hipGetLastError());
   } else if (!megakernel) {
     // adaptive AA, level by level (adapt_*_kernel): level 0's regions are the
@@ -3704,12 +3758,12 @@ rtx_status rtx_render(void* scene, const RtxRenderParams* params, uint8_t* rgb8,
       auto al = [](size_t x) { return (x + 255) & ~size_t(255); };
       const size_t bv = al(size_t(n) * sizeof(dvec3)), bi = al(size_t(n) * sizeof(int));
       const size_t br = regs ? al(size_t(n) * sizeof(ARegion)) : 0;
-      if (st->d_level.size() <= nlevel) {
-        st->d_level.push_back(nullptr);
-        st->level_bytes.push_back(0);
+      if (X->d_level.size() <= nlevel) {
+        X->d_level.push_back(nullptr);
+        X->level_bytes.push_back(0);
       }
-      if ((rc = ensure(&st->d_level[nlevel], &st->level_bytes[nlevel], bv + 2 * bi + br + 256)) != RTX_OK) return rc;
-      char* b = static_cast<char*>(st->d_level[nlevel++]);
+      if ((rc = ensure(&X->d_level[nlevel], &X->level_bytes[nlevel], bv + 2 * bi + br + 256)) != RTX_OK) return rc;
+      char* b = static_cast<char*>(X->d_level[nlevel++]);
       lv.val = reinterpret_cast<dvec3*>(b);
       lv.first = reinterpret_cast<int*>(b + bv);
       lv.mask = reinterpret_cast<int*>(b + bv + bi);
@@ -3719,23 +3773,23 @@ rtx_status rtx_render(void* scene, const RtxRenderParams* params, uint8_t* rgb8,
     };
     std::vector<ALevel> levels(1);
     if ((rc = level_alloc(npix, false, levels[0])) != RTX_OK) return rc;
-    if (!st->d_acnt) HIP_TRY(hipMalloc(&st->d_acnt, 2 * sizeof(unsigned int)));
+    if (!X->d_acnt) HIP_TRY(hipMalloc(&X->d_acnt, 2 * sizeof(unsigned int)));
     unsigned int hcnt[2] = {0u, 0u};
-    HIP_TRY(hipMemsetAsync(st->d_acnt, 0, 2 * sizeof(unsigned int), stream));
-    hipLaunchKernelGGL(adapt_stats_kernel, dim3((npix + WG - 1) / WG), dim3(WG), 0, stream, st->d_frame, sb,
-                       levels[0], int64_t(0), int64_t(npix), st->d_acnt);
+    HIP_TRY(hipMemsetAsync(X->d_acnt, 0, 2 * sizeof(unsigned int), ws));
+    hipLaunchKernelGGL(adapt_stats_kernel, dim3((npix + WG - 1) / WG), dim3(WG), 0, ws, X->d_frame, sb,
+                       levels[0], int64_t(0), int64_t(npix), X->d_acnt);
     HIP_TRY(hipGetLastError());
-    HIP_TRY(hipMemcpyAsync(hcnt, st->d_acnt, sizeof(hcnt), hipMemcpyDeviceToHost, stream));
-    HIP_TRY(hipStreamSynchronize(stream));
+    HIP_TRY(hipMemcpyAsync(hcnt, X->d_acnt, sizeof(hcnt), hipMemcpyDeviceToHost, ws));
+    HIP_TRY(hipStreamSynchronize(ws));
     // (the recursion ends once a region is under eps: ~14 levels at most)
     while (hcnt[0] > 0 && levels.size() < 64) {
       const int64_t n = hcnt[0];
       ALevel nx;
       if ((rc = level_alloc(n, true, nx)) != RTX_OK) return rc;
-      HIP_TRY(hipMemsetAsync(st->d_acnt, 0, 2 * sizeof(unsigned int), stream));
+      HIP_TRY(hipMemsetAsync(X->d_acnt, 0, 2 * sizeof(unsigned int), ws));
       const ALevel& up = levels.back();
-      hipLaunchKernelGGL(adapt_emit_kernel, dim3((up.n + WG - 1) / WG), dim3(WG), 0, stream, st->d_frame, up,
-                         const_cast<ARegion*>(nx.reg), st->d_acnt + 1);
+      hipLaunchKernelGGL(adapt_emit_kernel, dim3((up.n + WG - 1) / WG), dim3(WG), 0, ws, X->d_frame, up,
+                         const_cast<ARegion*>(nx.reg), X->d_acnt + 1);
       HIP_TRY(hipGetLastError());
       levels.push_back(nx);
       for (int64_t c0 = 0; c0 < n; c0 += npix) {
@@ -3745,15 +3799,15 @@ rtx_status rtx_render(void* scene, const RtxRenderParams* params, uint8_t* rgb8,
         FL.n_items = nc;
         FL.n_samples = nc * FL.spp * (FL.cam_split ? FL.ncam : 1);
         if ((rc = run_wavefront(FL, nc, false)) != RTX_OK) return rc;
-        hipLaunchKernelGGL(adapt_stats_kernel, dim3((nc + WG - 1) / WG), dim3(WG), 0, stream, st->d_frame, sb, nx, c0,
-                           nc, st->d_acnt);
+        hipLaunchKernelGGL(adapt_stats_kernel, dim3((nc + WG - 1) / WG), dim3(WG), 0, ws, X->d_frame, sb, nx, c0,
+                           nc, X->d_acnt);
         HIP_TRY(hipGetLastError());
         // (run_wavefront copies FL to the device before its first launch;
         // FL must outlive that copy)
-        HIP_TRY(hipStreamSynchronize(stream));
+        HIP_TRY(hipStreamSynchronize(ws));
       }
-      HIP_TRY(hipMemcpyAsync(hcnt, st->d_acnt, sizeof(hcnt), hipMemcpyDeviceToHost, stream));
-      HIP_TRY(hipStreamSynchronize(stream));
+      HIP_TRY(hipMemcpyAsync(hcnt, X->d_acnt, sizeof(hcnt), hipMemcpyDeviceToHost, ws));
+      HIP_TRY(hipStreamSynchronize(ws));
     }
     if (hcnt[0] > 0) {
       g_err = "rtx_render: adaptive AA recursion deeper than 64 levels";
@@ -3761,26 +3815,30 @@ rtx_status rtx_render(void* scene, const RtxRenderParams* params, uint8_t* rgb8,
     }
     for (size_t L = levels.size(); L-- > 0;) {
       ALevel below = L + 1 < levels.size() ? levels[L + 1] : ALevel{nullptr, nullptr, nullptr, nullptr, 0};
-      hipLaunchKernelGGL(adapt_combine_kernel, dim3((levels[L].n + WG - 1) / WG), dim3(WG), 0, stream, st->d_frame,
+      hipLaunchKernelGGL(adapt_combine_kernel, dim3((levels[L].n + WG - 1) / WG), dim3(WG), 0, ws, X->d_frame,
                          levels[L], below, d_rgb8, d_rgbf);
       HIP_TRY(hipGetLastError());
     }
-    HIP_TRY(hipStreamSynchronize(stream));  // the level buffers are freed on return
+    HIP_TRY(hipStreamSynchronize(ws));  // the level buffers are freed on return
   }
   for (auto& pr : frame_events) {
     st->ev_start.push_back(pr.first);
     st->ev_stop.push_back(pr.second);
   }
+  // the context is free again once the caller's stream has passed the frame
+  // (its reduce on the caller's stream; ws == stream for the other renders)
+  HIP_TRY(hipEventRecord(X->free_ev, stream));
+  X->used = true;
   if (!device_ptrs) {
-    if (rgb8) HIP_TRY(hipMemcpyAsync(rgb8, d_rgb8, npix * 3, hipMemcpyDeviceToHost, stream));
-    if (rgb_f64) HIP_TRY(hipMemcpyAsync(rgb_f64, d_rgbf, npix * 3 * sizeof(double), hipMemcpyDeviceToHost, stream));
-    if (hits) HIP_TRY(hipMemcpyAsync(hits, d_hits, npix * F.spp * sizeof(RtxHitRecord), hipMemcpyDeviceToHost, stream));
-    HIP_TRY(hipStreamSynchronize(stream));
+    if (rgb8) HIP_TRY(hipMemcpyAsync(rgb8, d_rgb8, npix * 3, hipMemcpyDeviceToHost, ws));
+    if (rgb_f64) HIP_TRY(hipMemcpyAsync(rgb_f64, d_rgbf, npix * 3 * sizeof(double), hipMemcpyDeviceToHost, ws));
+    if (hits) HIP_TRY(hipMemcpyAsync(hits, d_hits, npix * F.spp * sizeof(RtxHitRecord), hipMemcpyDeviceToHost, ws));
+    HIP_TRY(hipStreamSynchronize(ws));
   }
   if (stats) {
     unsigned long long c[RTX_STATS_N];
-    HIP_TRY(hipMemcpyAsync(c, st->d_stats, sizeof(c), hipMemcpyDeviceToHost, stream));
-    HIP_TRY(hipStreamSynchronize(stream));
+    HIP_TRY(hipMemcpyAsync(c, st->d_stats, sizeof(c), hipMemcpyDeviceToHost, ws));
+    HIP_TRY(hipStreamSynchronize(ws));
     {
       const char* dbg = getenv("RTX_DEBUG");
       if (dbg && atoi(dbg) != 0)

@@ -145,6 +145,44 @@ def test_repeat_deterministic(pkg):
     assert np.array_equal(a["rgb"], b["rgb"])
 
 
+@pytest.mark.parametrize("scene,flags,tile,nshards", [
+    ("trimesh2_glass.ray", "-w 96 -r 5 -O r -A 2", 0, 1),
+    ("trimesh2.ray", "-w 128 -r 5 -O r -A 4", 32, 3),
+    ("trimesh2.ray", "-w 64 -r 5 -O d -A 2.5 -B 4 -C 0.05", 0, 1),
+])
+def test_pipelined_frames_identical(pkg, scene, flags, tile, nshards):
+    """Renders into device buffers alternate between the scene's two frame
+    contexts and overlap each other (rtx_render: frame contexts).  Eight such
+    frames queued back to back — each shard twice, into separate buffers,
+    on one stream, one synchronisation at the end — must each equal the
+    stream-ordered host-mode render of the same shard byte for byte (and a
+    host-mode render queued behind them must still see a consistent
+    context)."""
+    import torch
+
+    path = scene_path(scene)
+    opts = pkg.RenderOptions.from_cli(flags.split())
+    host = pkg.HostScene(path)
+    dev = pkg.DeviceScene(host, 0)
+    h = host.height_for(opts.width)
+    packed = nshards > 1
+    want = [dev.render(opts, want_f64=False, tile=tile, shard=r, nshards=nshards, packed=packed)["rgb8"].reshape(-1)
+            for r in range(nshards)]
+    stream = torch.cuda.current_stream().cuda_stream
+    outs = []
+    for k in range(8):
+        r = k % nshards
+        n = pkg.shard_pixels(opts, h, tile, r, nshards, packed)
+        o = torch.zeros(n * 3, dtype=torch.uint8, device="cuda")
+        dev.render_device(opts, o.data_ptr(), 0, stream, tile=tile, shard=r, nshards=nshards, packed=packed)
+        outs.append((r, o))
+    again = dev.render(opts, want_f64=False, tile=tile, shard=0, nshards=nshards, packed=packed)["rgb8"].reshape(-1)
+    torch.cuda.synchronize()
+    for k, (r, o) in enumerate(outs):
+        assert np.array_equal(o.cpu().numpy(), want[r]), f"pipelined frame {k} (shard {r}) differs"
+    assert np.array_equal(again, want[0])
+
+
 @pytest.mark.parametrize("slots", ["20000", "40000", "1000000"])
 def test_buckets_independent_of_fork_slots(pkg, slots):
     """Ray-tree buckets make the image independent of which sub-trees won a

@@ -15,6 +15,8 @@ usage: python tools/bench_configs.py [C1 C2 ...]  (on the GPU box)
 """
 import json
 import os
+
+os.environ.setdefault("GPU_MAX_HW_QUEUES", "16")  # frame contexts: 2 x 3 group streams (bench.py)
 import subprocess
 import sys
 import time

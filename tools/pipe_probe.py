@@ -7,6 +7,8 @@ slowest rank's per-frame time with and without the overlap.
 usage (GPU box): python tools/pipe_probe.py [--scene S] [--flags F] [--frames K] [N ...]"""
 import json
 import os
+
+os.environ.setdefault("GPU_MAX_HW_QUEUES", "16")  # frame contexts: 2 x 3 group streams (bench.py)
 import sys
 import time
 

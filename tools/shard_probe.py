@@ -1,6 +1,7 @@
 #!/usr/bin/env python3
 """Per-rank frame time of the tile-sharded headline frame, measured on ONE
-GPU: rank r of N renders tiles t % N == r (what bench.py --gpus N runs on
+GPU (back-to-back frames, which overlap on the scene's two frame contexts,
+and one frame alone): rank r of N renders tiles t % N == r (what bench.py --gpus N runs on
 each GPU).  The slowest shard's time bounds the N-GPU frame (plus the RCCL
 gather of a few MB).  Prints one JSON line per N.
 usage (GPU box): python tools/shard_probe.py [--scene NAME.ray] [--flags "-w 1920 ..."] [--rank R] [N ...]
@@ -8,6 +9,8 @@ usage (GPU box): python tools/shard_probe.py [--scene NAME.ray] [--flags "-w 192
 (dragon.ray, C5's scene, is generated when missing: tools/gen_scenes.py --dragon)"""
 import json
 import os
+
+os.environ.setdefault("GPU_MAX_HW_QUEUES", "16")  # frame contexts: 2 x 3 group streams (bench.py)
 import subprocess
 import sys
 import time
@@ -44,7 +47,7 @@ def main():
     stream = torch.cuda.current_stream().cuda_stream
     free0 = torch.cuda.mem_get_info()[0]
     for n in ns:
-        times = []
+        times, lat = [], []
         for r in range(n):
             if only_rank is not None and n > 1 and r != only_rank:
                 continue
@@ -54,14 +57,22 @@ def main():
             dev.render_device(opts, out.data_ptr(), 0, stream, tile=tile, shard=r, nshards=n, packed=n > 1)
             torch.cuda.synchronize()
             t0 = time.perf_counter()
-            for _ in range(3):
+            for _ in range(3):  # back to back (consecutive frames overlap: frame contexts)
                 dev.render_device(opts, out.data_ptr(), 0, stream, tile=tile, shard=r, nshards=n, packed=n > 1)
             torch.cuda.synchronize()
             times.append((time.perf_counter() - t0) / 3 * 1e3)
+            one = []
+            for _ in range(3):  # one frame alone
+                t0 = time.perf_counter()
+                dev.render_device(opts, out.data_ptr(), 0, stream, tile=tile, shard=r, nshards=n, packed=n > 1)
+                torch.cuda.synchronize()
+                one.append((time.perf_counter() - t0) * 1e3)
+            lat.append(sorted(one)[1])
         # HBM the library holds beyond the scene (frame buffers grown so far)
         held = (free0 - torch.cuda.mem_get_info()[0]) / 2**30
         print(json.dumps({"scene": scene, "flags": flags, "n": n, "shard_ms": [round(t, 2) for t in times],
-                          "max_ms": round(max(times), 2), "frame_buffers_gb": round(held, 2)}),
+                          "max_ms": round(max(times), 2), "latency_ms": [round(t, 2) for t in lat],
+                          "max_latency_ms": round(max(lat), 2), "frame_buffers_gb": round(held, 2)}),
               flush=True)
 
 
