@@ -153,13 +153,20 @@ def test_repeat_deterministic(pkg):
 def test_pipelined_frames_identical(pkg, scene, flags, tile, nshards):
     """Renders into device buffers alternate between the scene's two frame
     contexts and overlap each other (rtx_render: frame contexts).  Eight such
-    frames queued back to back — each shard twice, into separate buffers,
-    on one stream, one synchronisation at the end — must each equal the
-    stream-ordered host-mode render of the same shard byte for byte (and a
-    host-mode render queued behind them must still see a consistent
-    context)."""
-    import torch
+    frames queued back to back — each shard more than once, into separate
+    buffers, on one stream, one synchronisation at the end — must each equal
+    the stream-ordered host-mode render of the same shard byte for byte (and
+    a host-mode render queued behind them must still see a consistent
+    context).  Device memory through the library's own HIP runtime (ctypes),
+    not torch's: the two runtimes in one process must not race to init."""
+    import ctypes as C
 
+    hip = C.CDLL("libamdhip64.so.7")
+    hip.hipMalloc.argtypes = [C.POINTER(C.c_void_p), C.c_size_t]
+    hip.hipFree.argtypes = [C.c_void_p]
+    hip.hipMemcpy.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int]
+    hip.hipStreamCreate.argtypes = [C.POINTER(C.c_void_p)]
+    hip.hipStreamDestroy.argtypes = [C.c_void_p]
     path = scene_path(scene)
     opts = pkg.RenderOptions.from_cli(flags.split())
     host = pkg.HostScene(path)
@@ -168,19 +175,28 @@ def test_pipelined_frames_identical(pkg, scene, flags, tile, nshards):
     packed = nshards > 1
     want = [dev.render(opts, want_f64=False, tile=tile, shard=r, nshards=nshards, packed=packed)["rgb8"].reshape(-1)
             for r in range(nshards)]
-    stream = torch.cuda.current_stream().cuda_stream
+    stream = C.c_void_p()
+    assert hip.hipStreamCreate(C.byref(stream)) == 0
     outs = []
-    for k in range(8):
-        r = k % nshards
-        n = pkg.shard_pixels(opts, h, tile, r, nshards, packed)
-        o = torch.zeros(n * 3, dtype=torch.uint8, device="cuda")
-        dev.render_device(opts, o.data_ptr(), 0, stream, tile=tile, shard=r, nshards=nshards, packed=packed)
-        outs.append((r, o))
-    again = dev.render(opts, want_f64=False, tile=tile, shard=0, nshards=nshards, packed=packed)["rgb8"].reshape(-1)
-    torch.cuda.synchronize()
-    for k, (r, o) in enumerate(outs):
-        assert np.array_equal(o.cpu().numpy(), want[r]), f"pipelined frame {k} (shard {r}) differs"
-    assert np.array_equal(again, want[0])
+    try:
+        for k in range(8):
+            r = k % nshards
+            n = pkg.shard_pixels(opts, h, tile, r, nshards, packed) * 3
+            buf = C.c_void_p()
+            assert hip.hipMalloc(C.byref(buf), n) == 0
+            outs.append((r, buf, n))
+            dev.render_device(opts, buf.value, 0, stream.value, tile=tile, shard=r, nshards=nshards, packed=packed)
+        again = dev.render(opts, want_f64=False, tile=tile, shard=0, nshards=nshards, packed=packed)
+        assert hip.hipDeviceSynchronize() == 0
+        for k, (r, buf, n) in enumerate(outs):
+            got = np.zeros(n, np.uint8)
+            assert hip.hipMemcpy(got.ctypes.data, buf, n, 2) == 0  # hipMemcpyDeviceToHost
+            assert np.array_equal(got, want[r]), f"pipelined frame {k} (shard {r}) differs"
+        assert np.array_equal(again["rgb8"].reshape(-1), want[0])
+    finally:
+        for _, buf, _ in outs:
+            hip.hipFree(buf)
+        hip.hipStreamDestroy(stream)
 
 
 @pytest.mark.parametrize("slots", ["20000", "40000", "1000000"])
