@@ -3224,16 +3224,17 @@ rtx_status rtx_render(void* scene, const RtxRenderParams* params, uint8_t* rgb8,
       mix(&F.P, sizeof(F.P));
       const int64_t ks[6] = {F.n_samples, nout, level0 ? 1 : 0, X->wf_call, int64_t(npos_b), int64_t(nunit_out)};
       mix(ks, sizeof(ks));
-      if (X->bstat_pending) {  // the last first-time frame's count (long done by now)
-        HIP_TRY(hipEventSynchronize(X->bstat_ev));
-        if (X->h_bstat[1] == 0u) {
-          st->bucket_hist[X->bstat_key] = X->h_bstat[0];
-        } else {
-          fprintf(stderr, "rtx_render: bucket pool refused a set (%u taken); frame pool reset\n", X->h_bstat[0]);
-          st->bucket_hist.erase(X->bstat_key);
+      for (FrameCtx& C : st->cx)  // the first-time frames' counts (either context's; long done by now)
+        if (C.bstat_pending) {
+          HIP_TRY(hipEventSynchronize(C.bstat_ev));
+          if (C.h_bstat[1] == 0u) {
+            st->bucket_hist[C.bstat_key] = C.h_bstat[0];
+          } else {
+            fprintf(stderr, "rtx_render: bucket pool refused a set (%u taken); frame pool reset\n", C.h_bstat[0]);
+            st->bucket_hist.erase(C.bstat_key);
+          }
+          C.bstat_pending = false;
         }
-        X->bstat_pending = false;
-      }
       const auto it = st->bucket_hist.find(bkey);
       if (it != st->bucket_hist.end()) bcap = std::min<size_t>(nunit_out, size_t(it->second) + 64);
     }

@@ -54,13 +54,14 @@ def main():
             tile = 32 if n > 1 else 0
             npix = pkg.shard_pixels(opts, h, tile, r, n, n > 1)
             out = torch.zeros(npix * 3, dtype=torch.uint8, device="cuda")
-            dev.render_device(opts, out.data_ptr(), 0, stream, tile=tile, shard=r, nshards=n, packed=n > 1)
-            torch.cuda.synchronize()
+            for _ in range(4):  # warm both frame contexts (buffers, bucket-pool sizes)
+                dev.render_device(opts, out.data_ptr(), 0, stream, tile=tile, shard=r, nshards=n, packed=n > 1)
+                torch.cuda.synchronize()
             t0 = time.perf_counter()
-            for _ in range(3):  # back to back (consecutive frames overlap: frame contexts)
+            for _ in range(6):  # back to back (consecutive frames overlap: frame contexts)
                 dev.render_device(opts, out.data_ptr(), 0, stream, tile=tile, shard=r, nshards=n, packed=n > 1)
             torch.cuda.synchronize()
-            times.append((time.perf_counter() - t0) / 3 * 1e3)
+            times.append((time.perf_counter() - t0) / 6 * 1e3)
             one = []
             for _ in range(3):  # one frame alone
                 t0 = time.perf_counter()
