@@ -36,8 +36,12 @@ os.environ.setdefault("OMP_PLACES", "cores")
 # Consecutive frames overlap on the scene's two frame contexts, each with its
 # slot groups on streams of its own (rtx_render, DESIGN.md "Frame
 # contexts"): with HIP's default of 4 hardware queues per process, the 2 x 3
-# group streams would share queues and serialise.  Read when HIP initialises.
-os.environ.setdefault("GPU_MAX_HW_QUEUES", "16")
+# group streams share queues and frame k + 1 queues behind frame k's tail
+# (kernel trace, profiles/r04i_timeline_q4.txt).  The environment may hold the
+# default explicitly (the GPU box does), so a lower value is raised.  Read
+# when HIP initialises.
+if int(os.environ.get("GPU_MAX_HW_QUEUES", "0") or 0) < 16:
+    os.environ["GPU_MAX_HW_QUEUES"] = "16"
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 METRIC = "Mrays/sec + frame ms, trimesh2.ray 1920×1080 depth-5 4×AA; 1/2/4/8 MI355X"

@@ -3201,12 +3201,19 @@ rtx_status rtx_render(void* scene, const RtxRenderParams* params, uint8_t* rgb8,
                 st->lights.size() <= 8;
     for (const auto& L : st->lights) fuse &= L.type == RTX_LIGHT_POINT || L.type == RTX_LIGHT_DIRECTIONAL;
     const size_t nl = fuse ? st->lights.size() : 0;
+    // pending-stack entries: a ray at entry i has depth <= P.depth - i (the
+    // camera ray is entry 0, a forked sub-tree's root entry 0 with less; a
+    // hit overwrites its own entry with one child and pushes the other), and
+    // only rays of depth > 0 push, so the fused machine never writes past
+    // entry P.depth - 1: P.depth entries (the sequential machine keeps
+    // depth + 2 for its media walks)
+    const int pcap = fuse ? std::max(1, params->depth) : pend_cap;
     // query records: closest (slot, 9 doubles, 2 ints); next: one per slot,
     // or one per light and slot with fused walks (slot, QF_D doubles, 3 ints)
     const size_t rec_c = sizeof(int) + QL_D * sizeof(double) + 2 * sizeof(int);
     const size_t rec_n = fuse ? sizeof(int) + QF_D * sizeof(double) + QF_I * sizeof(int) : rec_c;
     const size_t nrec_n = fuse ? std::max<size_t>(1, nl) : 1;
-    const size_t per_slot = lane_mem_bytes(1, fuse) - 512 + size_t(pend_cap) * 13 * sizeof(double) + rec_c +
+    const size_t per_slot = lane_mem_bytes(1, fuse) - 512 + size_t(pcap) * 13 * sizeof(double) + rec_c +
                             nrec_n * rec_n + 2 * sizeof(int) + nl * 3 * sizeof(double);
     // the bucket-set pool: as many sets as this frame took on its last
     // render (deterministic: one per unit whose root has a node child), the
@@ -3348,7 +3355,7 @@ rtx_status rtx_render(void* scene, const RtxRenderParams* params, uint8_t* rgb8,
     if ((rc = ensure(&X->d_lane, &X->lane_bytes, lane_mem_bytes(ns, fuse))) != RTX_OK) return rc;
     const LaneMem A = lane_mem_at(X->d_lane, ns, fuse);
     if ((rc = ensure(reinterpret_cast<void**>(&X->d_pbuf), &X->pbuf_bytes,
-                     ns * pend_cap * 13 * sizeof(double))) != RTX_OK)
+                     ns * pcap * 13 * sizeof(double))) != RTX_OK)
       return rc;
     if (!X->d_counters) HIP_TRY(hipMalloc(&X->d_counters, 16 * CNT_PER_GROUP * sizeof(unsigned int)));
     if (!X->h_counters) HIP_TRY(hipHostMalloc(&X->h_counters, 16 * CNT_PER_GROUP * sizeof(unsigned int)));
@@ -3533,16 +3540,16 @@ rtx_status rtx_render(void* scene, const RtxRenderParams* params, uint8_t* rgb8,
           if (fuse) {
             if (stats)
               hipLaunchKernelGGL((tail_fused_kernel<true>), dim3(grid), dim3(WG), lds, sg, S, X->d_scene, X->d_frame,
-                                 A, sb, d_hits, X->d_pbuf, pend_cap, cnt, live_in, in_cnt, st->stack_cap, st->d_stats,
+                                 A, sb, d_hits, X->d_pbuf, pcap, cnt, live_in, in_cnt, st->stack_cap, st->d_stats,
                                  ql[size_t(g) * 2 + 1], static_cast<int>(g * gslots));
             else
               hipLaunchKernelGGL((tail_fused_kernel<false>), dim3(grid), dim3(WG), lds, sg, S, X->d_scene, X->d_frame,
-                                 A, sb, d_hits, X->d_pbuf, pend_cap, cnt, live_in, in_cnt, st->stack_cap, st->d_stats,
+                                 A, sb, d_hits, X->d_pbuf, pcap, cnt, live_in, in_cnt, st->stack_cap, st->d_stats,
                                  ql[size_t(g) * 2 + 1], static_cast<int>(g * gslots));
           } else {
             dispatch2(stats, media, [&](auto st_, auto md_) {
               hipLaunchKernelGGL((tail_kernel<decltype(st_)::value, decltype(md_)::value>), dim3(grid), dim3(WG), lds,
-                                 sg, S, X->d_scene, X->d_frame, A, sb, d_hits, X->d_pbuf, pend_cap, cnt, live_in,
+                                 sg, S, X->d_scene, X->d_frame, A, sb, d_hits, X->d_pbuf, pcap, cnt, live_in,
                                  in_cnt, st->stack_cap, st->d_stats);
             });
           }
@@ -3578,7 +3585,7 @@ rtx_status rtx_render(void* scene, const RtxRenderParams* params, uint8_t* rgb8,
         } else if (fuse) {
           dispatch2(stats, fork, [&](auto st_, auto fk_) {
             hipLaunchKernelGGL((advance_fused_kernel<decltype(st_)::value, decltype(fk_)::value>), dim3(agrid),
-                               dim3(WG), 0, sg, S, X->d_scene, X->d_frame, A, sb, d_hits, X->d_pbuf, pend_cap, q0,
+                               dim3(WG), 0, sg, S, X->d_scene, X->d_frame, A, sb, d_hits, X->d_pbuf, pcap, q0,
                                q1, cnt, st->d_stats, static_cast<int>(g * gslots), live_in, live_out, first, in_cnt,
                                out_cnt);
           });
@@ -3586,7 +3593,7 @@ rtx_status rtx_render(void* scene, const RtxRenderParams* params, uint8_t* rgb8,
           dispatch3(stats, media, fork, [&](auto st_, auto md_, auto fk_) {
             hipLaunchKernelGGL((advance_kernel<decltype(st_)::value, decltype(md_)::value, decltype(fk_)::value>),
                                dim3(agrid), dim3(WG), 0, sg,
-                               S, X->d_scene, X->d_frame, A, sb, d_hits, X->d_pbuf, pend_cap, q0, q1, cnt,
+                               S, X->d_scene, X->d_frame, A, sb, d_hits, X->d_pbuf, pcap, q0, q1, cnt,
                                st->d_stats, static_cast<int>(g * gslots), live_in, live_out, first, in_cnt, out_cnt);
           });
         }
@@ -3600,7 +3607,7 @@ rtx_status rtx_render(void* scene, const RtxRenderParams* params, uint8_t* rgb8,
           sa.Fp = X->d_frame;
           sa.hits = d_hits;
           sa.pbuf = X->d_pbuf;
-          sa.pend_cap = pend_cap;
+          sa.pend_cap = pcap;
           sa.qn = q1;
           sa.slot_off = static_cast<int>(g * gslots);
           sa.live_out = live_out;

@@ -16,7 +16,10 @@ usage: python tools/bench_configs.py [C1 C2 ...]  (on the GPU box)
 import json
 import os
 
-os.environ.setdefault("GPU_MAX_HW_QUEUES", "16")  # frame contexts: 2 x 3 group streams (bench.py)
+# frame contexts: 2 x 3 slot-group streams want their own hardware queues; the
+# environment may hold HIP's default of 4 (the GPU box does), so raise it
+if int(os.environ.get("GPU_MAX_HW_QUEUES", "0") or 0) < 16:
+    os.environ["GPU_MAX_HW_QUEUES"] = "16"
 import subprocess
 import sys
 import time

@@ -8,7 +8,10 @@ usage (GPU box): python tools/pipe_probe.py [--scene S] [--flags F] [--frames K]
 import json
 import os
 
-os.environ.setdefault("GPU_MAX_HW_QUEUES", "16")  # frame contexts: 2 x 3 group streams (bench.py)
+# frame contexts: 2 x 3 slot-group streams want their own hardware queues; the
+# environment may hold HIP's default of 4 (the GPU box does), so raise it
+if int(os.environ.get("GPU_MAX_HW_QUEUES", "0") or 0) < 16:
+    os.environ["GPU_MAX_HW_QUEUES"] = "16"
 import sys
 import time
 

@@ -5,12 +5,16 @@ and one frame alone): rank r of N renders tiles t % N == r (what bench.py --gpus
 each GPU).  The slowest shard's time bounds the N-GPU frame (plus the RCCL
 gather of a few MB).  Prints one JSON line per N.
 usage (GPU box): python tools/shard_probe.py [--scene NAME.ray] [--flags "-w 1920 ..."] [--rank R] [N ...]
-(--rank R: only rank R of each N > 1, e.g. for a kernel trace of one shard)
+(--rank R: only rank R of each N > 1, e.g. for a kernel trace of one shard;
+ --own-stream: a created stream, not the default one)
 (dragon.ray, C5's scene, is generated when missing: tools/gen_scenes.py --dragon)"""
 import json
 import os
 
-os.environ.setdefault("GPU_MAX_HW_QUEUES", "16")  # frame contexts: 2 x 3 group streams (bench.py)
+# frame contexts: 2 x 3 slot-group streams want their own hardware queues; the
+# environment may hold HIP's default of 4 (the GPU box does), so raise it
+if int(os.environ.get("GPU_MAX_HW_QUEUES", "0") or 0) < 16:
+    os.environ["GPU_MAX_HW_QUEUES"] = "16"
 import subprocess
 import sys
 import time
@@ -28,7 +32,12 @@ def main():
     flags = "-w 1920 -r 5 -O r -A 4"
     scene = "trimesh2.ray"
     only_rank = None
-    while args and args[0] in ("--flags", "--scene", "--rank"):
+    own_stream = False
+    while args and args[0] in ("--flags", "--scene", "--rank", "--own-stream"):
+        if args[0] == "--own-stream":  # render on a created stream instead of torch's default (null) stream
+            own_stream = True
+            args = args[1:]
+            continue
         if args[0] == "--flags":
             flags = args[1]
         elif args[0] == "--rank":
@@ -44,7 +53,8 @@ def main():
     host = pkg.HostScene(os.path.join(ROOT, "scenes", scene))
     dev = pkg.DeviceScene(host, 0)
     h = host.height_for(opts.width)
-    stream = torch.cuda.current_stream().cuda_stream
+    ts = torch.cuda.Stream() if own_stream else torch.cuda.current_stream()
+    stream = ts.cuda_stream
     free0 = torch.cuda.mem_get_info()[0]
     for n in ns:
         times, lat = [], []
