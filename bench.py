@@ -398,6 +398,13 @@ def main():
             send[: rgb8.numel()].copy_(rgb8)
             dist.gather(send, gather_list, dst=0)
 
+    # settle (untimed, before the W warmups): a frame's first render on each
+    # frame context sizes its buffers for the default slot pool, and the
+    # renders after it resize them once to the frame's fork history (a
+    # hipMalloc / hipFree that waits for the device) — 3 frames cover both
+    # contexts
+    for _ in range(3):
+        step()
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()

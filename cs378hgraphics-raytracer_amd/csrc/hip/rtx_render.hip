@@ -2535,10 +2535,11 @@ struct FrameCtx {
   int* d_bidx = nullptr;
   size_t bidx_bytes = 0;
   unsigned int* d_bstat = nullptr;
-  unsigned int* h_bstat = nullptr;  // pinned
+  unsigned int* h_bstat = nullptr;  // pinned: [taken, refused, -, -, fork requests of group g at 4 + g]
   hipEvent_t bstat_ev = nullptr;
   bool bstat_pending = false;
   uint64_t bstat_key = 0;
+  int bstat_groups = 0;  // groups whose fork counts were read back (0: the frame did not fork)
   int wf_call = 0;  // run_wavefront calls of the current rtx_render
   // adaptive AA: one buffer per level (values, first-quarter index, mask,
   // regions), grown on demand and reused by later frames (no hipMalloc /
@@ -2565,9 +2566,14 @@ struct SceneState {
   int picks_res = -1;
   FrameCtx cx[2];
   unsigned int next_cx = 0;
-  // the bucket sets each frame (key: its parameters and its place in the
-  // render) took on its last render
-  std::map<uint64_t, uint32_t> bucket_hist;
+  // what each frame (key: its parameters and its place in the render) took
+  // on its first render: bucket sets, and the most fork requests of one
+  // slot group (-1: unknown, the frame did not fork)
+  struct FrameHist {
+    uint32_t sets;
+    int64_t forks;
+  };
+  std::map<uint64_t, FrameHist> bucket_hist;
   int64_t last_work[RTX_STATS_N] = {};  // raw counters of the last counting render (rtx_last_work)
   std::vector<hipEvent_t> ev_pool;
   size_t ev_used = 0;
@@ -2966,10 +2972,25 @@ rtx_status rtx_render(void* scene, const RtxRenderParams* params, uint8_t* rgb8,
   // and joins the caller's stream for its final reduce.  Every other render
   // uses context 0 on the caller's stream, after whatever was queued there
   // (RTX_PIPELINE=0: always that).
+  FrameParams F;
+  std::vector<double> offv;
+  rtx_status rc = build_frame(st, params, F, offv);
+  if (rc != RTX_OK) return rc;
+  // Only frames of at most RTX_PIPELINE_SAMPLES work units (samples x DoF
+  // camera rays; default 20 M: the shards of a multi-GPU frame) overlap: a
+  // whole headline frame's last iterations are a small share of it (32.6 /
+  // 33.2 ms against 33.5 / 32.9 without on two boxes, at twice the frame
+  // buffers), a 4-way shard's are not (8.8 vs 10.0 ms; profiles/r04k_*).
+  // RTX_PIPELINE=0: never.
   const char* mk_env0 = getenv("RTX_MEGAKERNEL");
   const char* pipe_env = getenv("RTX_PIPELINE");
+  int64_t pipe_max = 20000000;
+  if (const char* e = getenv("RTX_PIPELINE_SAMPLES")) pipe_max = atoll(e);
+  int64_t npix0 = 0;
+  rtx_shard_pixels(params, &npix0);
   const bool pipelined = !(pipe_env && atoi(pipe_env) == 0) && device_ptrs && !hits && !stats &&
-                         params->aa_mode != RTX_AA_ADAPTIVE && !(mk_env0 && atoi(mk_env0) != 0);
+                         params->aa_mode != RTX_AA_ADAPTIVE && !(mk_env0 && atoi(mk_env0) != 0) &&
+                         npix0 * int64_t(F.spp) * int64_t(F.ncam) <= pipe_max;
   FrameCtx* X = pipelined ? &st->cx[(st->next_cx++) & 1u] : &st->cx[0];
   if (!X->free_ev) HIP_TRY(hipEventCreateWithFlags(&X->free_ev, hipEventDisableTiming));
   if (X->wf_streams.empty()) {
@@ -2990,10 +3011,6 @@ rtx_status rtx_render(void* scene, const RtxRenderParams* params, uint8_t* rgb8,
     for (FrameCtx& C : st->cx)  // (a pipelined frame may still run on the other context)
       if (C.used) HIP_TRY(hipStreamWaitEvent(stream, C.free_ev, 0));
   }
-  FrameParams F;
-  std::vector<double> offv;
-  rtx_status rc = build_frame(st, params, F, offv);
-  if (rc != RTX_OK) return rc;
   if (!offv.empty()) {
     const size_t need = offv.size() * sizeof(double);
     if (need > X->offv_bytes) {
@@ -3210,7 +3227,9 @@ rtx_status rtx_render(void* scene, const RtxRenderParams* params, uint8_t* rgb8,
     const int pcap = fuse ? std::max(1, params->depth) : pend_cap;
     // query records: closest (slot, 9 doubles, 2 ints); next: one per slot,
     // or one per light and slot with fused walks (slot, QF_D doubles, 3 ints)
-    const size_t rec_c = sizeof(int) + QL_D * sizeof(double) + 2 * sizeof(int);
+    // (fused closest records hold the ray only: 6 doubles, no ints)
+    const size_t qc_d = fuse ? 6 : QL_D, qc_i = fuse ? 0 : 2;
+    const size_t rec_c = sizeof(int) + qc_d * sizeof(double) + qc_i * sizeof(int);
     const size_t rec_n = fuse ? sizeof(int) + QF_D * sizeof(double) + QF_I * sizeof(int) : rec_c;
     const size_t nrec_n = fuse ? std::max<size_t>(1, nl) : 1;
     const size_t per_slot = lane_mem_bytes(1, fuse) - 512 + size_t(pcap) * 13 * sizeof(double) + rec_c +
@@ -3222,6 +3241,12 @@ rtx_status rtx_render(void* scene, const RtxRenderParams* params, uint8_t* rgb8,
     // depends on the pool.
     const size_t npos_b = (size_t(1) << (fork_depth + 1)) - 2;  // (as npos below)
     size_t bcap = nunit_out;
+    // fork slots per group the frame needs: its largest per-group count of
+    // fork requests on its first render (every node child asks for a fork
+    // slot whether or not it gets one, so the count does not depend on the
+    // spare slots; with at least that many spares every request is granted
+    // as on the first render).  -1: unknown, half a slot per sample.
+    int64_t fspare = -1;
     uint64_t bkey = 1469598103934665603ull;
     {
       auto mix = [&](const void* p, size_t n) {
@@ -3235,7 +3260,9 @@ rtx_status rtx_render(void* scene, const RtxRenderParams* params, uint8_t* rgb8,
         if (C.bstat_pending) {
           HIP_TRY(hipEventSynchronize(C.bstat_ev));
           if (C.h_bstat[1] == 0u) {
-            st->bucket_hist[C.bstat_key] = C.h_bstat[0];
+            int64_t fm = C.bstat_groups > 0 ? 0 : -1;
+            for (int g = 0; g < C.bstat_groups; ++g) fm = std::max<int64_t>(fm, C.h_bstat[4 + g]);
+            st->bucket_hist[C.bstat_key] = {C.h_bstat[0], fm};
           } else {
             fprintf(stderr, "rtx_render: bucket pool refused a set (%u taken); frame pool reset\n", C.h_bstat[0]);
             st->bucket_hist.erase(C.bstat_key);
@@ -3243,7 +3270,12 @@ rtx_status rtx_render(void* scene, const RtxRenderParams* params, uint8_t* rgb8,
           C.bstat_pending = false;
         }
       const auto it = st->bucket_hist.find(bkey);
-      if (it != st->bucket_hist.end()) bcap = std::min<size_t>(nunit_out, size_t(it->second) + 64);
+      if (it != st->bucket_hist.end()) {
+        bcap = std::min<size_t>(nunit_out, size_t(it->second.sets) + 64);
+        // (never more than the half slot per sample of the default pool)
+        if (it->second.forks >= 0)
+          fspare = std::min<int64_t>(it->second.forks, (F.n_samples + G - 1) / G / 2);
+      }
     }
     {
       // memory budget: what the device has free plus the frame buffers this
@@ -3277,7 +3309,8 @@ rtx_status rtx_render(void* scene, const RtxRenderParams* params, uint8_t* rgb8,
       if (fork_ok && !(ns_env && atoll(ns_env) > 0)) {
         // one slot per sample plus half as many fork slots (headline frame:
         // 50 M slots, 89 -> 84 ms; 2-way shard 58 -> 50 ms)
-        const int64_t want = std::min<int64_t>(cap, F.n_samples + F.n_samples / 2 + int64_t(G) * 2 * WG);
+        const int64_t spare_all = fspare >= 0 ? int64_t(G) * (fspare + WG) : F.n_samples / 2;
+        const int64_t want = std::min<int64_t>(cap, F.n_samples + spare_all + int64_t(G) * 2 * WG);
         if (want > nslot64) nslot64 = want;
       }
       if (nslot64 > cap && !(ns_env && atoll(ns_env) > 0)) nslot64 = std::max<int64_t>(cap, int64_t(G) * 4 * WG);
@@ -3286,7 +3319,10 @@ rtx_status rtx_render(void* scene, const RtxRenderParams* params, uint8_t* rgb8,
     // give every sample a slot of its own plus half as many spares
     const bool fork = fork_ok && nslot64 >= int64_t(G) * 8 * WG;
     int64_t gsamp = (F.n_samples + G - 1) / G;  // sample slots per group
-    const int64_t gcap = fork && F.n_samples * 4 > nslot64 * 3 ? nslot64 * 2 / 3 : nslot64;
+    // (a pool sized from the fork history holds every sample and the spares
+    // its forks need: no third set aside)
+    const bool spare_fit = fspare >= 0 && nslot64 >= F.n_samples + int64_t(G) * (fspare + WG);
+    const int64_t gcap = fork && F.n_samples * 4 > nslot64 * 3 && !spare_fit ? nslot64 * 2 / 3 : nslot64;
     if (gsamp > (gcap + G - 1) / G) gsamp = (gcap + G - 1) / G;
     gsamp = (gsamp + 63) / 64 * 64;  // whole 64-unit runs (slot_unit)
     int64_t gspare = 0;
@@ -3321,7 +3357,7 @@ rtx_status rtx_render(void* scene, const RtxRenderParams* params, uint8_t* rgb8,
       if ((rc = ensure(reinterpret_cast<void**>(&X->d_bidx), &X->bidx_bytes, nunit_out * sizeof(int))) != RTX_OK)
         return rc;
       if (!X->d_bstat) HIP_TRY(hipMalloc(&X->d_bstat, 4 * sizeof(unsigned int)));
-      if (!X->h_bstat) HIP_TRY(hipHostMalloc(&X->h_bstat, 4 * sizeof(unsigned int)));
+      if (!X->h_bstat) HIP_TRY(hipHostMalloc(&X->h_bstat, (4 + 16) * sizeof(unsigned int)));
       if (!X->bstat_ev) HIP_TRY(hipEventCreateWithFlags(&X->bstat_ev, hipEventDisableTiming));
       HIP_TRY(hipMemsetAsync(X->d_bstat, 0, 4 * sizeof(unsigned int), ws));
       F.fbuf = X->d_fbuf;
@@ -3339,22 +3375,35 @@ rtx_status rtx_render(void* scene, const RtxRenderParams* params, uint8_t* rgb8,
     // per group: the closest and the next query list, then two live-slot
     // lists (ping-pong)
     const size_t capn = gs * nrec_n;
-    const size_t bytes_qc = al(gs * sizeof(int)) + al(gs * QL_D * sizeof(double)) + al(gs * 2 * sizeof(int));
+    const size_t bytes_qc = al(gs * sizeof(int)) + al(gs * qc_d * sizeof(double)) + al(gs * qc_i * sizeof(int));
     const size_t nd = fuse ? QF_D : QL_D, ni = fuse ? QF_I : 2;
     const size_t bytes_qn = al(capn * sizeof(int)) + al(capn * nd * sizeof(double)) + al(capn * ni * sizeof(int));
-    if ((rc = ensure(&X->d_wf, &X->wf_bytes, size_t(G) * (bytes_qc + bytes_qn + 2 * al(gs * sizeof(int))))) != RTX_OK)
+    // the slot buffers follow the pool: a first render sizes them for the
+    // default pool, later renders of the frame for its fork history, and a
+    // buffer much larger than this frame needs is given back (once; hipFree
+    // waits for the device) — only on a render's first pass, so an
+    // adaptive frame's level chunks never free what its first pass uses
+    auto fit = [&](void** ptr, size_t* have, size_t need) -> rtx_status {
+      if (X->wf_call == 0 && *have > need + need / 8 + (size_t(64) << 20)) {
+        (void)hipFree(*ptr);
+        *ptr = nullptr;
+        *have = 0;
+      }
+      return ensure(ptr, have, need);
+    };
+    if ((rc = fit(&X->d_wf, &X->wf_bytes, size_t(G) * (bytes_qc + bytes_qn + 2 * al(gs * sizeof(int))))) != RTX_OK)
       return rc;
     F.fuse = fuse ? 1 : 0;
     F.wterm = nullptr;
     if (fuse && nl > 0) {
-      if ((rc = ensure(reinterpret_cast<void**>(&X->d_wterm), &X->wterm_bytes, nl * ns * 3 * sizeof(double))) !=
+      if ((rc = fit(reinterpret_cast<void**>(&X->d_wterm), &X->wterm_bytes, nl * ns * 3 * sizeof(double))) !=
           RTX_OK)
         return rc;
       F.wterm = X->d_wterm;
     }
-    if ((rc = ensure(&X->d_lane, &X->lane_bytes, lane_mem_bytes(ns, fuse))) != RTX_OK) return rc;
+    if ((rc = fit(&X->d_lane, &X->lane_bytes, lane_mem_bytes(ns, fuse))) != RTX_OK) return rc;
     const LaneMem A = lane_mem_at(X->d_lane, ns, fuse);
-    if ((rc = ensure(reinterpret_cast<void**>(&X->d_pbuf), &X->pbuf_bytes,
+    if ((rc = fit(reinterpret_cast<void**>(&X->d_pbuf), &X->pbuf_bytes,
                      ns * pcap * 13 * sizeof(double))) != RTX_OK)
       return rc;
     if (!X->d_counters) HIP_TRY(hipMalloc(&X->d_counters, 16 * CNT_PER_GROUP * sizeof(unsigned int)));
@@ -3377,7 +3426,7 @@ rtx_status rtx_render(void* scene, const RtxRenderParams* params, uint8_t* rgb8,
     {
       char* base = static_cast<char*>(X->d_wf);
       for (size_t m = 0; m < ql.size(); ++m) {
-        const size_t cap = (m & 1) ? capn : gs, dn = (m & 1) ? nd : QL_D;
+        const size_t cap = (m & 1) ? capn : gs, dn = (m & 1) ? nd : qc_d;
         ql[m].slot = reinterpret_cast<int*>(base);
         ql[m].d = reinterpret_cast<double*>(base + al(cap * sizeof(int)));
         ql[m].iv = reinterpret_cast<int*>(base + al(cap * sizeof(int)) + al(cap * dn * sizeof(double)));
@@ -3737,6 +3786,11 @@ rtx_status rtx_render(void* scene, const RtxRenderParams* params, uint8_t* rgb8,
     if (fork_ok && st->bucket_hist.find(bkey) == st->bucket_hist.end() && !X->bstat_pending) {
       // first render of this frame: its set count, read at the next call
       HIP_TRY(hipMemcpyAsync(X->h_bstat, X->d_bstat, 2 * sizeof(unsigned int), hipMemcpyDeviceToHost, ws));
+      // (the fork counters are final: the other groups joined ws above)
+      X->bstat_groups = fork ? G : 0;
+      for (int g = 0; g < X->bstat_groups; ++g)
+        HIP_TRY(hipMemcpyAsync(X->h_bstat + 4 + g, X->d_counters + CNT_PER_GROUP * g + CNT_FORK, sizeof(unsigned int),
+                               hipMemcpyDeviceToHost, ws));
       HIP_TRY(hipEventRecord(X->bstat_ev, ws));
       X->bstat_pending = true;
       X->bstat_key = bkey;
