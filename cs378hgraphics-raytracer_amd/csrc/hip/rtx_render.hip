@@ -2299,6 +2299,12 @@ __device__ __forceinline__ bool slot_pixel(const FrameParams& F, int64_t o, int&
 
 // Per-pixel ordered reduction of the sample buffer (RayTracer.cpp:288-298:
 // col += tracePixel(...) in si-major order, col /= s*s; setPixel truncates).
+// zeros into output slot o (packed padding)
+__device__ __forceinline__ void pad_slot(int64_t o, uint8_t* __restrict__ rgb8, double* __restrict__ rgbf) {
+  if (rgb8) rgb8[o * 3 + 0] = rgb8[o * 3 + 1] = rgb8[o * 3 + 2] = 0;
+  if (rgbf) rgbf[o * 3 + 0] = rgbf[o * 3 + 1] = rgbf[o * 3 + 2] = 0.0;
+}
+
 __global__ void __launch_bounds__(WG) reduce_kernel(const FrameParams* __restrict__ Fp, const double* __restrict__ sbuf,
                                                      uint8_t* __restrict__ rgb8, double* __restrict__ rgbf,
                                                      int64_t npix_slots) {
@@ -2315,7 +2321,8 @@ __global__ void __launch_bounds__(WG) reduce_kernel(const FrameParams* __restric
   const int pl = t / spp, q = t - pl * spp;
   const int64_t o = static_cast<int64_t>(blockIdx.x) * ppb + pl;
   int i, j;
-  const bool own = pl < ppb && o < npix_slots && slot_pixel(F, o, i, j);
+  const bool in_slots = pl < ppb && o < npix_slots;
+  const bool own = in_slots && slot_pixel(F, o, i, j);
   if (own) {
     const dvec3 v = sample_value(F, sbuf, o * spp + q);
     sv[t * 3 + 0] = v.x;
@@ -2323,7 +2330,14 @@ __global__ void __launch_bounds__(WG) reduce_kernel(const FrameParams* __restric
     sv[t * 3 + 2] = v.z;
   }
   __syncthreads();
-  if (!own || q != 0) return;
+  if (!in_slots || q != 0) return;
+  if (!own) {
+    // a packed shard's slot past the image border (a partial tile): zeros,
+    // as a host-mode render leaves it, not whatever the caller's buffer held
+    // (a sharded full frame's other tiles are not ours to write)
+    if (F.P.packed && F.P.tile > 0) pad_slot(o, rgb8, rgbf);
+    return;
+  }
   dvec3 acc = mk3(0.0, 0.0, 0.0);
   for (int k = 0; k < spp; ++k) acc += mk3(sv[(t + k) * 3 + 0], sv[(t + k) * 3 + 1], sv[(t + k) * 3 + 2]);
   if (F.P.aa_mode != RTX_AA_NONE) acc = acc / double(F.s * F.s);
@@ -2458,7 +2472,10 @@ __global__ void __launch_bounds__(WG) adapt_combine_kernel(const FrameParams* __
   if (r >= lv.n) return;
   if (!lv.reg) {
     int i, j;
-    if (!slot_pixel(F, r, i, j)) return;
+    if (!slot_pixel(F, r, i, j)) {
+      if (F.P.packed && F.P.tile > 0) pad_slot(r, rgb8, rgbf);  // (as reduce_kernel)
+      return;
+    }
   }
   dvec3 v = lv.val[r];
   if (lv.first[r] != -1) {  // mu = 0; mu += subval (2 x 2, RayTracer.cpp:352-360); mu *= 1/4
@@ -2566,6 +2583,21 @@ struct SceneState {
   int picks_res = -1;
   FrameCtx cx[2];
   unsigned int next_cx = 0;
+  // Pinned staging for the frame's host-to-device copies (frame record,
+  // scene record, DoF offsets).  A hipMemcpyAsync from pageable memory may
+  // read the host buffer only when its stream reaches the copy — after the
+  // caller's locals are gone, or rewritten by the next frame's render, when
+  // the stream waits for an earlier frame (a pipelined frame waits for its
+  // context's previous one).  Entries are reused round-robin; an entry's
+  // event says its last copy has run.
+  struct Stage {
+    void* h = nullptr;
+    size_t cap = 0;
+    hipEvent_t ev = nullptr;
+    bool used = false;
+  };
+  Stage stage[16];
+  unsigned int next_stage = 0;
   // what each frame (key: its parameters and its place in the render) took
   // on its first render: bucket sets, and the most fork requests of one
   // slot group (-1: unknown, the frame did not fork)
@@ -2814,6 +2846,7 @@ rtx_status rtx_scene_destroy(void* scene) {
   if (!scene) return RTX_OK;
   SceneState* st = static_cast<SceneState*>(scene);
   (void)hipSetDevice(st->device);
+  (void)hipDeviceSynchronize();  // (pipelined frames may still be in flight)
   for (void* p : st->allocs) (void)hipFree(p);
   if (st->d_work) (void)hipFree(st->d_work);
   if (st->d_stats) (void)hipFree(st->d_stats);
@@ -2844,10 +2877,35 @@ rtx_status rtx_scene_destroy(void* scene) {
     if (X.d_scene) (void)hipFree(X.d_scene);
     if (X.free_ev) (void)hipEventDestroy(X.free_ev);
   }
+  for (SceneState::Stage& E : st->stage) {
+    if (E.ev) (void)hipEventSynchronize(E.ev);
+    if (E.h) (void)hipHostFree(E.h);
+    if (E.ev) (void)hipEventDestroy(E.ev);
+  }
   for (auto e : st->ev_pool) (void)hipEventDestroy(e);
   for (auto e : st->ev_start) (void)hipEventDestroy(e);
   for (auto e : st->ev_stop) (void)hipEventDestroy(e);
   delete st;
+  return RTX_OK;
+}
+
+// dst <- bytes at src on `stream`, through the next pinned staging entry (the
+// source may change or go away as soon as this returns)
+static rtx_status stage_copy(SceneState* st, void* dst, const void* src, size_t bytes, hipStream_t stream) {
+  SceneState::Stage& E = st->stage[st->next_stage++ % 16u];
+  if (E.used) HIP_TRY(hipEventSynchronize(E.ev));
+  if (bytes > E.cap) {
+    if (E.h) (void)hipHostFree(E.h);
+    E.h = nullptr;
+    E.cap = 0;
+    HIP_TRY(hipHostMalloc(&E.h, bytes));
+    E.cap = bytes;
+  }
+  if (!E.ev) HIP_TRY(hipEventCreateWithFlags(&E.ev, hipEventDisableTiming));
+  std::memcpy(E.h, src, bytes);
+  HIP_TRY(hipMemcpyAsync(dst, E.h, bytes, hipMemcpyHostToDevice, stream));
+  HIP_TRY(hipEventRecord(E.ev, stream));
+  E.used = true;
   return RTX_OK;
 }
 
@@ -3003,6 +3061,13 @@ rtx_status rtx_render(void* scene, const RtxRenderParams* params, uint8_t* rgb8,
     HIP_TRY(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
     X->wf_check.push_back(ev);
   }
+  // a buffer of this context may still be read by its previous frame (a
+  // pipelined render returns before its frame ends): wait for that frame
+  // before giving one back
+  auto ctx_free = [&](void* p) {
+    if (X->used) (void)hipEventSynchronize(X->free_ev);
+    (void)hipFree(p);
+  };
   hipStream_t ws = stream;  // the frame's work stream (slot group 0)
   if (pipelined) {
     ws = X->wf_streams[0];
@@ -3014,13 +3079,13 @@ rtx_status rtx_render(void* scene, const RtxRenderParams* params, uint8_t* rgb8,
   if (!offv.empty()) {
     const size_t need = offv.size() * sizeof(double);
     if (need > X->offv_bytes) {
-      if (X->d_offv) (void)hipFree(X->d_offv);
+      if (X->d_offv) ctx_free(X->d_offv);
       X->d_offv = nullptr;
       X->offv_bytes = 0;
       HIP_TRY(hipMalloc(&X->d_offv, need));
       X->offv_bytes = need;
     }
-    HIP_TRY(hipMemcpyAsync(X->d_offv, offv.data(), need, hipMemcpyHostToDevice, ws));
+    if ((rc = stage_copy(st, X->d_offv, offv.data(), need, ws)) != RTX_OK) return rc;
     F.offv = X->d_offv;
   }
   // area-light pick tables depend on ss_res
@@ -3086,7 +3151,7 @@ rtx_status rtx_render(void* scene, const RtxRenderParams* params, uint8_t* rgb8,
   if (!(adaptive && megakernel)) {
     const size_t need = size_t(npix) * F.spp * (F.cam_split ? F.ncam : 1) * 3 * sizeof(double);
     if (need > X->sbuf_bytes) {
-      if (X->d_sbuf) (void)hipFree(X->d_sbuf);
+      if (X->d_sbuf) ctx_free(X->d_sbuf);
       X->d_sbuf = nullptr;
       X->sbuf_bytes = 0;
       HIP_TRY(hipMalloc(&X->d_sbuf, need));
@@ -3097,7 +3162,7 @@ rtx_status rtx_render(void* scene, const RtxRenderParams* params, uint8_t* rgb8,
   // device copy of the scene record: functions called out of line read it
   // through this pointer (a kernel-argument copy has no address)
   if (!X->d_scene) HIP_TRY(hipMalloc(&X->d_scene, sizeof(DevScene)));
-  HIP_TRY(hipMemcpyAsync(X->d_scene, &st->S_launch, sizeof(DevScene), hipMemcpyHostToDevice, ws));
+  if ((rc = stage_copy(st, X->d_scene, &st->S_launch, sizeof(DevScene), ws)) != RTX_OK) return rc;
   if (stats) HIP_TRY(hipMemsetAsync(st->d_stats, 0, RTX_STATS_N * sizeof(unsigned long long), ws));
   const int pend_cap = (params->depth > 0 ? params->depth : 0) + 2;
   auto get_event = [&](hipEvent_t* e) -> rtx_status {
@@ -3111,7 +3176,7 @@ rtx_status rtx_render(void* scene, const RtxRenderParams* params, uint8_t* rgb8,
   };
   auto ensure = [&](void** ptr, size_t* have, size_t need) -> rtx_status {
     if (need > *have) {
-      if (*ptr) (void)hipFree(*ptr);
+      if (*ptr) ctx_free(*ptr);
       *ptr = nullptr;
       *have = 0;
       HIP_TRY(hipMalloc(ptr, need));
@@ -3157,7 +3222,7 @@ rtx_status rtx_render(void* scene, const RtxRenderParams* params, uint8_t* rgb8,
       if (c > QCHUNK) c = QCHUNK;
       F.qchunk = static_cast<int>(c);
     }
-    HIP_TRY(hipMemcpyAsync(X->d_frame, &F, sizeof(FrameParams), hipMemcpyHostToDevice, ws));
+    if ((rc = stage_copy(st, X->d_frame, &F, sizeof(FrameParams), ws)) != RTX_OK) return rc;
     if ((rc = ensure(reinterpret_cast<void**>(&X->d_pbuf), &X->pbuf_bytes,
                      size_t(grid) * WG * pend_cap * 13 * sizeof(double))) != RTX_OK)
       return rc;
@@ -3346,7 +3411,7 @@ rtx_status rtx_render(void* scene, const RtxRenderParams* params, uint8_t* rgb8,
       const size_t nsamp_out = size_t(nout) * F.spp;
       const size_t fbuf_need = std::max<size_t>(1, bcap) * F.fork_npos * 3 * sizeof(double);
       if (X->fbuf_bytes > 2 * fbuf_need + (size_t(64) << 20)) {  // a smaller pool than the first render's: give it back
-        (void)hipFree(X->d_fbuf);
+        ctx_free(X->d_fbuf);
         X->d_fbuf = nullptr;
         X->fbuf_bytes = 0;
       }
@@ -3385,7 +3450,7 @@ rtx_status rtx_render(void* scene, const RtxRenderParams* params, uint8_t* rgb8,
     // adaptive frame's level chunks never free what its first pass uses
     auto fit = [&](void** ptr, size_t* have, size_t need) -> rtx_status {
       if (X->wf_call == 0 && *have > need + need / 8 + (size_t(64) << 20)) {
-        (void)hipFree(*ptr);
+        ctx_free(*ptr);
         *ptr = nullptr;
         *have = 0;
       }
@@ -3492,7 +3557,7 @@ rtx_status rtx_render(void* scene, const RtxRenderParams* params, uint8_t* rgb8,
       }
       cam_n[size_t(g)] = static_cast<int>(c);
     }
-    HIP_TRY(hipMemcpyAsync(X->d_frame, &F, sizeof(FrameParams), hipMemcpyHostToDevice, ws));
+    if ((rc = stage_copy(st, X->d_frame, &F, sizeof(FrameParams), ws)) != RTX_OK) return rc;
     // every slot starts ST_IDLE, kdone = 0, outside a discoverMat walk, no
     // deferred colour: set by the group's first advance_kernel, which visits
     // all of its slots (every other field is written before it is read)

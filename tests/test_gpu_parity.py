@@ -191,7 +191,8 @@ def test_pipelined_frames_identical(pkg, scene, flags, tile, nshards):
         for k, (r, buf, n) in enumerate(outs):
             got = np.zeros(n, np.uint8)
             assert hip.hipMemcpy(got.ctypes.data, buf, n, 2) == 0  # hipMemcpyDeviceToHost
-            assert np.array_equal(got, want[r]), f"pipelined frame {k} (shard {r}) differs"
+            bad = np.nonzero(got != want[r])[0]
+            assert len(bad) == 0, f"pipelined frame {k} (shard {r}): {len(bad)} of {n} bytes differ, first at {bad[:6]}"
         assert np.array_equal(again["rgb8"].reshape(-1), want[0])
     finally:
         for _, buf, _ in outs:

@@ -37,7 +37,7 @@ for step in "$@"; do
       timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_$TAG -o run \
         -- python3 bench.py --no-cpu --steps 3 --warmup 1 > gpurun_out/prof_$TAG.log 2>&1 \
         || { tail -5 gpurun_out/prof_$TAG.log; exit 1; }
-      python3 tools/kstats.py gpurun_out/prof_$TAG/run_kernel_stats.csv 4 | tail -6 ;;
+      python3 tools/kstats.py gpurun_out/prof_$TAG/run_kernel_stats.csv 10 | tail -6 ;;
     pmc)
       export TMPDIR=/tmp
       bash tools/profile_traffic.sh $TAG > gpurun_out/traffic_$TAG.log 2>&1 || { tail -5 gpurun_out/traffic_$TAG.log; exit 1; }
@@ -46,7 +46,7 @@ for step in "$@"; do
         2> gpurun_out/bench2_$TAG.err || { tail -5 gpurun_out/bench2_$TAG.err; exit 1; }
       tail -1 gpurun_out/bench2_$TAG.json | cut -c1-300
       if [ -f gpurun_out/prof_$TAG/run_kernel_stats.csv ]; then
-        python3 tools/kernel_roofline.py gpurun_out/bench2_$TAG.json gpurun_out/prof_$TAG/run_kernel_stats.csv 4 \
+        python3 tools/kernel_roofline.py gpurun_out/bench2_$TAG.json gpurun_out/prof_$TAG/run_kernel_stats.csv 10 \
           profiles/traffic_$TAG.json > gpurun_out/kernel_roofline_$TAG.json || exit 1
       fi ;;
     shards)
