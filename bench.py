@@ -31,6 +31,9 @@ import time
 
 # The CPU leg's OpenMP threads stay on their cores (one per core, packed):
 # set before any OpenMP runtime (torch's or the oracle's) initialises
+# (the affinity mask as the job got it: once an OpenMP runtime binds the
+# initial thread to its first place, sched_getaffinity reports that place)
+_AFFINITY0 = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
 os.environ.setdefault("OMP_PROC_BIND", "close")
 os.environ.setdefault("OMP_PLACES", "cores")
 # Consecutive frames overlap on the scene's two frame contexts, each with its
@@ -108,7 +111,7 @@ def host_cpu():
     except OSError:
         pass
     ncpu = os.cpu_count() or 1
-    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else ncpu
+    aff = _AFFINITY0
     quota = None
     try:
         q, per = open("/sys/fs/cgroup/cpu.max").read().split()
