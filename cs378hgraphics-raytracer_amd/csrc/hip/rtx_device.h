@@ -356,16 +356,17 @@ RT_HD bool box_cons32v(float lox, float loy, float loz, float hix, float hiy, fl
   const float t1z = (loz - r.olo[2]) * r.inv[2], t2z = (hiz - r.ohi[2]) * r.inv[2];
   const float tmin = fmaxf(fmaxf(fminf(t1x, t2x), fminf(t1y, t2y)), fminf(t1z, t2z));
   const float tmax = fminf(fminf(fmaxf(t1x, t2x), fmaxf(t1y, t2y)), fmaxf(t1z, t2z));
-  // (err is finite; an infinite bound stays infinite, a miss stays a miss)
+  // (err is finite; an infinite bound stays infinite)
   a = tmin - (r.err + fabsf(tmin) * 0x1p-21f);
   b = tmax + (r.err + fabsf(tmax) * 0x1p-21f);
-  // inf - inf (an inside-test axis): the infinite bound itself — entry at
-  // +inf or exit at -inf, a miss either way
-  if (!(a == a)) a = tmin;
-  if (!(b == b)) b = tmax;
+  // tmin is finite or +inf and tmax finite or -inf (a ray has a nonzero
+  // direction axis, whose slab is finite); the infinities come from
+  // inside-test axes that miss, and give a = NaN (inf - inf) or b = NaN.
+  // The ordered compares below are false on NaN: a miss, as it must be, with
+  // no fix-up of a and b (a and b are used only on a hit).
   // (no 1e-8 cut on the exit, as the double slab had none here; leaf_ok
   // applies the reference's)
-  return !(a > b) && !(b < 0.0f);
+  return a <= b && b >= 0.0f;
 }
 
 RT_HD bool box_cons32(const DevNode4& nd, int k, const RayF& r, float& a, float& b) {

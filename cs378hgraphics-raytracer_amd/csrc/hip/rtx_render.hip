@@ -2583,6 +2583,7 @@ struct SceneState {
   int picks_res = -1;
   FrameCtx cx[2];
   unsigned int next_cx = 0;
+  bool any_recur = true;  // some material reflects or refracts (no: no ray tree, no buckets)
   // Pinned staging for the frame's host-to-device copies (frame record,
   // scene record, DoF offsets).  A hipMemcpyAsync from pageable memory may
   // read the host buffer only when its stream reaches the copy — after the
@@ -2830,6 +2831,10 @@ rtx_status rtx_scene_create(int device, const RtxSceneDesc* d, void** out) {
   }
   st->cam = d->camera;
   st->lights.assign(d->lights, d->lights + d->n_lights);
+  // can any hit spawn a reflection or refraction ray?  (per-vertex materials
+  // never recurse: their flags are 0, hit_flags)
+  st->any_recur = false;
+  for (int m = 0; m < d->n_materials; ++m) st->any_recur |= (d->materials[m].flags & RTX_MF_RECUR) != 0;
   if (hipMalloc(&st->cx[0].d_frame, sizeof(FrameParams)) != hipSuccess ||
       hipMalloc(&st->cx[1].d_frame, sizeof(FrameParams)) != hipSuccess ||
       hipMalloc(&st->d_work, sizeof(unsigned long long)) != hipSuccess ||
@@ -3174,8 +3179,10 @@ rtx_status rtx_render(void* scene, const RtxRenderParams* params, uint8_t* rgb8,
     HIP_TRY(hipEventCreate(e));
     return RTX_OK;
   };
+  static const bool dbg_alloc = getenv("RTX_DEBUG_ALLOC") && atoi(getenv("RTX_DEBUG_ALLOC")) != 0;
   auto ensure = [&](void** ptr, size_t* have, size_t need) -> rtx_status {
     if (need > *have) {
+      if (dbg_alloc) fprintf(stderr, "rtx alloc ctx %d: %zu -> %zu B (call %d)\n", int(X - st->cx), *have, need, X->wf_call);
       if (*ptr) ctx_free(*ptr);
       *ptr = nullptr;
       *have = 0;
@@ -3273,7 +3280,11 @@ rtx_status rtx_render(void* scene, const RtxRenderParams* params, uint8_t* rgb8,
     const char* fd_env = getenv("RTX_FORK_DEPTH");
     if (fd_env && atoi(fd_env) > 0) fork_depth = std::min(4, atoi(fd_env));
     // (DoF: with the camera-ray split each camera ray owns its buckets)
-    bool fork_ok = !(fork_env && atoi(fork_env) == 0) && !F.P.anaglyph && (!params->dof || F.cam_split);
+    // (a scene whose materials never reflect or refract has no ray trees to
+    // fork: the C5 dragon, whose 8 x 8 adaptive shards took 48 GB of
+    // buckets for nothing)
+    bool fork_ok = !(fork_env && atoi(fork_env) == 0) && !F.P.anaglyph && (!params->dof || F.cam_split) &&
+                   st->any_recur && params->depth > 0;
     const size_t nunit_out = size_t(nout) * F.spp * (F.cam_split ? F.ncam : 1);  // bucket owners
     // fused shadow walks (rtx_fused.h): every light a point or directional
     // light, no overlapping media, no adaptive termination (RTX_FUSE=0: the
@@ -3410,7 +3421,9 @@ rtx_status rtx_render(void* scene, const RtxRenderParams* params, uint8_t* rgb8,
     if (fork_ok) {
       const size_t nsamp_out = size_t(nout) * F.spp;
       const size_t fbuf_need = std::max<size_t>(1, bcap) * F.fork_npos * 3 * sizeof(double);
-      if (X->fbuf_bytes > 2 * fbuf_need + (size_t(64) << 20)) {  // a smaller pool than the first render's: give it back
+      // a smaller pool than the first render's: give it back (not on adaptive
+      // frames, whose level chunks take smaller pools than their first pass)
+      if (!adaptive && X->fbuf_bytes > 2 * fbuf_need + (size_t(64) << 20)) {
         ctx_free(X->d_fbuf);
         X->d_fbuf = nullptr;
         X->fbuf_bytes = 0;
@@ -3446,10 +3459,10 @@ rtx_status rtx_render(void* scene, const RtxRenderParams* params, uint8_t* rgb8,
     // the slot buffers follow the pool: a first render sizes them for the
     // default pool, later renders of the frame for its fork history, and a
     // buffer much larger than this frame needs is given back (once; hipFree
-    // waits for the device) — only on a render's first pass, so an
-    // adaptive frame's level chunks never free what its first pass uses
+    // waits for the device) — on a render's first pass and not on adaptive
+    // frames, whose level chunks would resize them back and forth
     auto fit = [&](void** ptr, size_t* have, size_t need) -> rtx_status {
-      if (X->wf_call == 0 && *have > need + need / 8 + (size_t(64) << 20)) {
+      if (X->wf_call == 0 && !adaptive && *have > need + need / 8 + (size_t(64) << 20)) {
         ctx_free(*ptr);
         *ptr = nullptr;
         *have = 0;

@@ -137,7 +137,7 @@ RT_HD bool visit4(const DevNode4& nd, const RayF& rf, const double hi, const dou
                   int& rk) {
     if (STATS && k < nrec) C.nodes++;
     float ta, tb;
-    const bool hit = box_cons32v(lox, loy, loz, hix, hiy, hiz, rf, ta, tb) && !(ta > hf) && !(tb < lf);
+    const bool hit = box_cons32v(lox, loy, loz, hix, hiy, hiz, rf, ta, tb) && ta <= hf && tb >= lf;
     if (k < nrec && hit) {
       ak = ta;
       rk = child;
