@@ -227,6 +227,15 @@ def _free_port():
     return port
 
 
+def _rehearsal():
+    """RTX_BENCH_REHEARSAL=1: every rank on device 0 and the gather over gloo
+    through host memory — the N-rank path (launch, shards, gather, timing
+    over ranks, the JSON line) exercised on a one-GPU box, where RCCL cannot
+    put two ranks on one device.  Its numbers are not an N-GPU measurement
+    (the ranks share one GPU) and its line says so."""
+    return os.environ.get("RTX_BENCH_REHEARSAL", "0") == "1"
+
+
 def launch_ranks(n, argv, probe=False, grace_s=10.0):
     """`bench.py --gpus N` without an external launcher: start N rank
     processes of this script (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* set,
@@ -238,7 +247,7 @@ def launch_ranks(n, argv, probe=False, grace_s=10.0):
     product driver's failure path (csrc/host/multi_gpu.cpp)."""
     import signal
 
-    if not probe:
+    if not probe and not _rehearsal():
         import torch
 
         ndev = torch.cuda.device_count()
@@ -357,16 +366,23 @@ def main():
     pkg_dir = os.path.join(ROOT, "cs378hgraphics-raytracer_amd")
     if rank == 0 or world == 1:
         ensure_built(pkg_dir)
-    if not os.path.exists(args.scene):
-        if rank == 0:
-            subprocess.run([sys.executable, os.path.join(ROOT, "tools", "gen_scenes.py")], check=True,
-                           stdout=subprocess.DEVNULL)
     import torch
     import torch.distributed as dist
 
+    rehearsal = _rehearsal() and world > 1
+    if rehearsal:
+        local_rank = 0
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        if rehearsal:
+            dist.init_process_group("gloo", rank=rank, world_size=world)
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
     torch.cuda.set_device(local_rank)
+    # (under an external launcher the scenes may not exist yet: rank 0 makes
+    # them, the others wait at the barrier; launch_ranks made them already)
+    if not os.path.exists(args.scene) and rank == 0:
+        subprocess.run([sys.executable, os.path.join(ROOT, "tools", "gen_scenes.py")], check=True,
+                       stdout=subprocess.DEVNULL)
     if world > 1:
         dist.barrier()
     pkg = load_package()
@@ -374,6 +390,7 @@ def main():
     host = pkg.HostScene(args.scene)
     height = host.height_for(opts.width)
     dev = pkg.DeviceScene(host, local_rank)
+    cdev = "cpu" if rehearsal else "cuda"  # where the collectives' tensors live (gloo: host memory)
     tile = args.tile if world > 1 else 0
     packed = world > 1
     npix = pkg.shard_pixels(opts, height, tile, rank, world, packed)
@@ -386,14 +403,14 @@ def main():
     gather_list = None
     if world > 1 and rank == 0:
         gather_list = [torch.zeros(pkg.shard_pixels(opts, height, tile, r, world, True) * 3, dtype=torch.uint8,
-                                   device="cuda") for r in range(world)]
+                                   device=cdev) for r in range(world)]
         # dist.gather needs equal sizes: pad to the largest shard
         mx = max(g.numel() for g in gather_list)
-        gather_list = [torch.zeros(mx, dtype=torch.uint8, device="cuda") for _ in range(world)]
+        gather_list = [torch.zeros(mx, dtype=torch.uint8, device=cdev) for _ in range(world)]
     if world > 1:
-        mx = torch.tensor([rgb8.numel()], device="cuda")
+        mx = torch.tensor([rgb8.numel()], device=cdev)
         dist.all_reduce(mx, op=dist.ReduceOp.MAX)
-        send = torch.zeros(int(mx.item()), dtype=torch.uint8, device="cuda")
+        send = torch.zeros(int(mx.item()), dtype=torch.uint8, device=cdev)
 
     def step():
         dev.render_device(opts, rgb8.data_ptr(), 0, stream, tile=tile, shard=rank, nshards=world, packed=packed)
@@ -437,21 +454,21 @@ def main():
     frame_latency_ms = sorted(lat)[1]
     dev.kernel_time()  # (not part of the roofline's frames)
     if world > 1:
-        t = torch.tensor([frame_latency_ms], dtype=torch.float64, device="cuda")
+        t = torch.tensor([frame_latency_ms], dtype=torch.float64, device=cdev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         frame_latency_ms = float(t.item())
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        t = torch.tensor([elapsed], dtype=torch.float64, device=cdev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-        tot = torch.tensor([st["rays"]], dtype=torch.int64, device="cuda")
+        tot = torch.tensor([st["rays"]], dtype=torch.int64, device=cdev)
         dist.all_reduce(tot)
         frame_rays = int(tot.item())
     else:
         frame_rays = st["rays"]
     shadow_skipped = st["shadow_rays"] - st["shadow_traced"]
     if world > 1:
-        t = torch.tensor([shadow_skipped], dtype=torch.int64, device="cuda")
+        t = torch.tensor([shadow_skipped], dtype=torch.int64, device=cdev)
         dist.all_reduce(t)
         shadow_skipped = int(t.item())
     traced_rays = frame_rays - shadow_skipped
@@ -515,7 +532,9 @@ def main():
             "data": "synthetic (procedural trimesh2 stand-in scene, tools/gen_scenes.py seed 2; reference scene absent)",
             "config": {"workload": f"trimesh2 {opts.width}x{height} {args.flags}", "scene": os.path.basename(args.scene),
                        "triangles": host.info.n_faces, "rays_per_frame": frame_rays, "tile": tile or None,
-                       "parallelism": f"tile-shard x{world} + RCCL gather" if world > 1 else "single GPU"},
+                       "parallelism": ((f"REHEARSAL: {world} ranks sharing one GPU, gloo gather through host memory"
+                                        " (not an N-GPU measurement)") if rehearsal else
+                                       f"tile-shard x{world} + RCCL gather" if world > 1 else "single GPU")},
             "roofline": {"bound": bound, "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                          # measured: PMC HBM bytes of a frame / the frame's GPU time / peak
