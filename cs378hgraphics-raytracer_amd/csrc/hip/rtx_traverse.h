@@ -100,7 +100,7 @@ RT_HD bool visit4(const DevNode4& nd, const RayF& rf, const double hi, const dou
                   const int lane, int& sp, int& ref, Counters& C) {
   const float NOHIT = __builtin_inff();
   // prune bounds widened to floats (hi up, lo down): pruning stays safe
-  const float hf = f_up(hi), lf = f_down(lo);
+  const float hf = f_up_wide(hi), lf = f_down_wide(lo);
   float a0 = NOHIT, a1 = NOHIT, a2 = NOHIT, a3 = NOHIT;
   int r0 = 0, r1 = 0, r2 = 0, r3 = 0;
 #ifdef RTX_PACKED_RECORDS

@@ -142,6 +142,15 @@ int rec_test_host(int32_t n, const double* P, const double* D, const double* box
   return 0;
 }
 
+// The record walk's prune bounds (f_up_wide / f_down_wide) for n doubles.
+int prune_bounds_host(int32_t n, const double* x, float* up, float* dn) {
+  for (int32_t k = 0; k < n; ++k) {
+    up[k] = f_up_wide(x[k]);
+    dn[k] = f_down_wide(x[k]);
+  }
+  return 0;
+}
+
 // Per-ray traversal cost of closest queries (record entries, object tests,
 // face tests): which rays make the long queries (tools/ray_cost_probe.py).
 int trav_host_cost(const RtxSceneDesc* d, int32_t n, const double* P, const double* D, int64_t* nodes,

@@ -130,3 +130,33 @@ def test_tiny_direction_components(pkg):
     for k in range(n):
         assert exact_hit(P[k], D[k], B[k, :3], B[k, 3:]), k
         assert ok[k] == 1, f"case {k}: exact hit rejected (d={D[k]!r}, box={B[k]!r})"
+
+
+def test_prune_bounds_widen(pkg):
+    """The record walk prunes a record entry whose float slab starts past the
+    query's best t (or ends before its lower bound) against float copies of
+    those bounds (visit4: f_up_wide / f_down_wide, rtx_device.h).  They must
+    never be tighter than the doubles — up >= x >= dn exactly — over the
+    whole double range: float-range edges, denormals, zeros, infinities."""
+    L = _harness(pkg)
+    L.prune_bounds_host.argtypes = [C.c_int32, C.c_void_p, C.c_void_p, C.c_void_p]
+    rng = np.random.default_rng(11)
+    mant = rng.random(200000) + 1.0
+    expo = rng.integers(-160, 140, 200000).astype(np.float64)
+    x = np.concatenate([
+        mant * np.exp2(expo) * np.where(rng.random(200000) < 0.5, -1.0, 1.0),
+        rng.normal(size=20000) * 100.0,
+        np.nextafter(np.float32(rng.normal(size=2000)).astype(np.float64), np.inf),  # just past a float
+        np.nextafter(np.float32(rng.normal(size=2000)).astype(np.float64), -np.inf),
+        np.array([0.0, -0.0, 1e-320, -1e-320, 1e-45, -1e-45, 1.2e-38, -1.2e-38, 3.4028234e38, -3.4028234e38,
+                  3.5e38, -3.5e38, 1e308, -1e308, np.inf, -np.inf, 1e-5, 0.1, 1.0, 4096.0]),
+    ])
+    up = np.zeros(x.size, np.float32)
+    dn = np.zeros(x.size, np.float32)
+    assert L.prune_bounds_host(x.size, x.ctypes.data, up.ctypes.data, dn.ctypes.data) == 0
+    assert np.all(up.astype(np.float64) >= x), x[up.astype(np.float64) < x][:5]
+    assert np.all(dn.astype(np.float64) <= x), x[dn.astype(np.float64) > x][:5]
+    # and not much wider than the tightest floats (a few ulps) where finite
+    fin = np.isfinite(up) & (np.abs(x) > 1e-30) & (np.abs(x) < 1e38)
+    rel = (up[fin].astype(np.float64) - x[fin]) / np.abs(x[fin])
+    assert rel.max() < 2.0 ** -20
