@@ -200,6 +200,42 @@ def test_pipelined_frames_identical(pkg, scene, flags, tile, nshards):
         hip.hipStreamDestroy(stream)
 
 
+@pytest.mark.parametrize("flags", ["-w 80 -r 5 -O r -A 2", "-w 80 -r 3 -O a -A 4"], ids=["regular", "adaptive"])
+def test_packed_padding_zeroed(pkg, flags):
+    """A packed shard's slots past the image border (the partial tiles of an
+    80 x 45 frame) are written as zeros by the device-buffer render too —
+    not left as whatever the caller's buffer held — so a device render of a
+    shard equals the host-mode render byte for byte (reduce_kernel,
+    adapt_combine_kernel)."""
+    import ctypes as C
+
+    hip = C.CDLL("libamdhip64.so.7")
+    hip.hipMalloc.argtypes = [C.POINTER(C.c_void_p), C.c_size_t]
+    hip.hipFree.argtypes = [C.c_void_p]
+    hip.hipMemset.argtypes = [C.c_void_p, C.c_int, C.c_size_t]
+    hip.hipMemcpy.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int]
+    host = pkg.HostScene(scene_path("spheres_overlap.ray"))
+    dev = pkg.DeviceScene(host, 0)
+    opts = pkg.RenderOptions.from_cli(flags.split())
+    h = host.height_for(opts.width)
+    nsh = 3
+    for r in range(nsh):
+        want = dev.render(opts, want_f64=False, tile=32, shard=r, nshards=nsh, packed=True)["rgb8"].reshape(-1)
+        n = pkg.shard_pixels(opts, h, 32, r, nsh, True) * 3
+        assert n > opts.width * h * 3 // nsh  # the shard holds padding
+        buf = C.c_void_p()
+        assert hip.hipMalloc(C.byref(buf), n) == 0
+        try:
+            assert hip.hipMemset(buf, 0xAB, n) == 0
+            dev.render_device(opts, buf.value, 0, 0, tile=32, shard=r, nshards=nsh, packed=True)
+            assert hip.hipDeviceSynchronize() == 0
+            got = np.zeros(n, np.uint8)
+            assert hip.hipMemcpy(got.ctypes.data, buf, n, 2) == 0
+        finally:
+            hip.hipFree(buf)
+        assert np.array_equal(got, want), f"shard {r}: {int((got != want).sum())} bytes differ"
+
+
 @pytest.mark.parametrize("slots", ["20000", "40000", "1000000"])
 def test_buckets_independent_of_fork_slots(pkg, slots):
     """Ray-tree buckets make the image independent of which sub-trees won a
