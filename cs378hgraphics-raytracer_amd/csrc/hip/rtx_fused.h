@@ -360,6 +360,7 @@ struct ShadeArgs {
                    // ray of the group's slot k (cam_first_claim), k < cam_n
   int leaf_k;      // object / leaf units wait while >= leaf_k lanes are at a
                    // record (trace_kernel; 65: never)
+  const int* free_ids;  // the group's free fork slots (advance_fused_kernel pushes them)
 };
 
 // Camera ray k of the sample at (sx, sy), eye pass `pass` (trace(),
@@ -569,7 +570,7 @@ __global__ void __launch_bounds__(WG, RTX_FUSED_ADV_WAVES)
                          double* __restrict__ sbuf, RtxHitRecord* __restrict__ hits, double* __restrict__ pbuf,
                          int pend_cap, QList q0, QList q1, unsigned int* __restrict__ counters,
                          unsigned long long* __restrict__ stats, int slot_off, const int* __restrict__ live_in,
-                         int* __restrict__ live_out, int first, int in_cnt, int out_cnt) {
+                         int* __restrict__ live_out, int first, int in_cnt, int out_cnt, int* __restrict__ free_ids) {
   const FrameParams& F = *Fp;
   const int tid = blockIdx.x * WG + threadIdx.x;
   // first: 1 every slot of the group, initialised here; 2 every slot (the
@@ -582,6 +583,8 @@ __global__ void __launch_bounds__(WG, RTX_FUSED_ADV_WAVES)
   LaneRef L(lm, static_cast<size_t>(slot));
   if (first == 1) lane_init(L);
   int qm = Q_NONE;
+  // a fork slot (past the group's sample slots) running a sub-tree
+  const bool was_fork = FORK && valid && slot - slot_off >= F.wf_gsamp && L.st() != ST_IDLE;
   if (valid && (L.st() != ST_IDLE || slot_unit(F, slot, L.kdone()) >= 0)) {
     flush_terms(L, F);
     L.qmode() = Q_NONE;
@@ -619,6 +622,19 @@ __global__ void __launch_bounds__(WG, RTX_FUSED_ADV_WAVES)
     if (lane == 0) base = atomicAdd(&counters[out_cnt], static_cast<unsigned int>(__popcll(alive)));
     base = __shfl(base, 0);
     if (live) live_out[base + lane_prefix(alive)] = slot;
+  }
+  if (FORK && free_ids) {
+    // a fork slot whose sub-tree ended here goes on the group's free list
+    // (fork_claim in the closest-hit launch reuses it: the spare slots then
+    // serve more forks than there are spares)
+    const bool freed = was_fork && L.st() == ST_IDLE;
+    const unsigned long long fm = __ballot(freed);
+    if (fm) {
+      unsigned int base = 0;
+      if (lane == 0) base = atomicAdd(&counters[CNT_FREE], static_cast<unsigned int>(__popcll(fm)));
+      base = __shfl(base, 0);
+      if (freed) free_ids[base + lane_prefix(fm)] = slot;
+    }
   }
   if (STATS) {
     stats_add(C, stats, lane);
