@@ -3589,6 +3589,11 @@ rtx_status rtx_render(void* scene, const RtxRenderParams* params, uint8_t* rgb8,
     // slots than units, iteration 5 comes long before the units are all
     // claimed, and the switch waits for the live count instead)
     if (int64_t(F.wf_nslot) < F.n_samples && !ti_env) tail_iter = 0;
+    // (nor when the frame's history shows more fork requests than spares:
+    // its sub-trees then also run on their parents' stacks, one ray per
+    // iteration, and much is left at iteration 5 — R1, the glass frame:
+    // 394 -> 253 ms with the switch by live count only, profiles/r04w_*)
+    if (fspare >= 0 && !spares_enough && !ti_env) tail_iter = 0;
     F.qchunk = 64;
     // First iteration without an advance launch (fused frames): the closest-
     // hit launch claims each sample slot's first sample and queries its first
