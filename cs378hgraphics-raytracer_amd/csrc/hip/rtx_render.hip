@@ -3348,6 +3348,9 @@ rtx_status rtx_render(void* scene, const RtxRenderParams* params, uint8_t* rgb8,
     const size_t npos_b = (size_t(1) << (fork_depth + 1)) - 2;  // (as npos below)
     size_t bcap = nunit_out;
     bool spares_enough = false;  // the spares cover every fork request (no free list needed)
+    // spare slots per sample slot at most, in percent (RTX_SPARE, default 50)
+    int64_t spare_pct = 50;
+    if (const char* e = getenv("RTX_SPARE")) spare_pct = std::max<int64_t>(1, std::min<int64_t>(400, atoll(e)));
     // fork slots per group the frame needs: its largest per-group count of
     // fork requests on its first render (every node child asks for a fork
     // slot whether or not it gets one, so the count does not depend on the
@@ -3381,7 +3384,7 @@ rtx_status rtx_render(void* scene, const RtxRenderParams* params, uint8_t* rgb8,
         bcap = std::min<size_t>(nunit_out, size_t(it->second.sets) + 64);
         // (never more than the half slot per sample of the default pool)
         if (it->second.forks >= 0) {
-          fspare = std::min<int64_t>(it->second.forks, (F.n_samples + G - 1) / G / 2);
+          fspare = std::min<int64_t>(it->second.forks, (F.n_samples + G - 1) / G * spare_pct / 100);
           spares_enough = fspare == it->second.forks;
         }
       }
@@ -3418,7 +3421,7 @@ rtx_status rtx_render(void* scene, const RtxRenderParams* params, uint8_t* rgb8,
       if (fork_ok && !(ns_env && atoll(ns_env) > 0)) {
         // one slot per sample plus half as many fork slots (headline frame:
         // 50 M slots, 89 -> 84 ms; 2-way shard 58 -> 50 ms)
-        const int64_t spare_all = fspare >= 0 ? int64_t(G) * (fspare + WG) : F.n_samples / 2;
+        const int64_t spare_all = fspare >= 0 ? int64_t(G) * (fspare + WG) : F.n_samples * spare_pct / 100;
         const int64_t want = std::min<int64_t>(cap, F.n_samples + spare_all + int64_t(G) * 2 * WG);
         if (want > nslot64) nslot64 = want;
       }
@@ -3435,7 +3438,7 @@ rtx_status rtx_render(void* scene, const RtxRenderParams* params, uint8_t* rgb8,
     if (gsamp > (gcap + G - 1) / G) gsamp = (gcap + G - 1) / G;
     gsamp = (gsamp + 63) / 64 * 64;  // whole 64-unit runs (slot_unit)
     int64_t gspare = 0;
-    if (fork) gspare = std::min<int64_t>(gsamp / 2 + WG, nslot64 / G - gsamp);
+    if (fork) gspare = std::min<int64_t>(gsamp * spare_pct / 100 + WG, nslot64 / G - gsamp);
     const int64_t per = (gsamp + gspare + WG - 1) / WG;  // workgroups per group
     const int64_t gslots = per * WG;
     if (!fork) gsamp = gslots;
