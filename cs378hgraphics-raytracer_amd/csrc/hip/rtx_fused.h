@@ -327,21 +327,27 @@ __device__ __forceinline__ void shade_hit(LaneRef& LR, const DevScene& S, const 
     bucket_alloc(F, LR.bunit(), (node_refl || node_refr) && ((next_trans && !tir) || (flags & RTX_MF_REFL) || tir));
   // push refraction first so that reflection is traced first (the entry at
   // `top` is this ray's own, read above: it is overwritten)
-  if (next_trans && !tir && LR.top() < pend_cap) {
+  // (a child that neither forks nor fits on the stack can only happen with
+  // the two-entry stacks of rtx_render's low_stack rule: flagged, *bover bit 2)
+  if (next_trans && !tir) {
     const dvec3 tp = rtm::ray_at(rp, rd, bt + RTX_RAY_EPS);
     const dvec3 td = eta * rd + (eta * c - sqrt(radicand)) * normal;
     const dvec3 kf = leaving ? mk3(1.0, 1.0, 1.0) : hit_param(S, R, RTX_P_KT);
-    if (!fused_fork_child<FORK>(LR, fk, pbuf, nlanes, tp, td, W, kf, depth, 2, node_refr))
-      fused_push(LR, pbuf, nlanes, tp, td, W, kf, depth, 2, node_refr ? node_refr : pos);
+    if (!fused_fork_child<FORK>(LR, fk, pbuf, nlanes, tp, td, W, kf, depth, 2, node_refr)) {
+      if (LR.top() < pend_cap) fused_push(LR, pbuf, nlanes, tp, td, W, kf, depth, 2, node_refr ? node_refr : pos);
+      else if (F.bover) atomicOr(F.bover, 4u);
+    }
     if (STATS) C.secondary++;
   }
-  if (((flags & RTX_MF_REFL) || tir) && LR.top() < pend_cap) {
+  if ((flags & RTX_MF_REFL) || tir) {
     const dvec3 rdir = rd + 2 * c * normal;
     const dvec3 rs = rtm::ray_at(rp, rd, bt - RTX_RAY_EPS);
     const dvec3 wr = W * hit_param(S, R, RTX_P_KR);
     const dvec3 kf = leaving ? hit_param(S, R, RTX_P_KT) : mk3(1.0, 1.0, 1.0);
-    if (!fused_fork_child<FORK>(LR, fk, pbuf, nlanes, rs, rdir, wr, kf, depth, 1, node_refl))
-      fused_push(LR, pbuf, nlanes, rs, rdir, wr, kf, depth, 1, node_refl ? node_refl : pos);
+    if (!fused_fork_child<FORK>(LR, fk, pbuf, nlanes, rs, rdir, wr, kf, depth, 1, node_refl)) {
+      if (LR.top() < pend_cap) fused_push(LR, pbuf, nlanes, rs, rdir, wr, kf, depth, 1, node_refl ? node_refl : pos);
+      else if (F.bover) atomicOr(F.bover, 4u);
+    }
     if (STATS) C.secondary++;
   }
 }

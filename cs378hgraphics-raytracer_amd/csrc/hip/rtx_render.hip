@@ -2586,6 +2586,9 @@ struct FrameCtx {
   bool bstat_pending = false;
   uint64_t bstat_key = 0;
   int bstat_groups = 0;  // groups whose fork counts were read back (0: the frame did not fork)
+  hipEvent_t ovf_ev = nullptr;  // the last two-entry-stack frame's *bover, read back into h_bstat[2]
+  bool ovf_pending = false;
+  uint64_t ovf_key = 0;
   int wf_call = 0;  // run_wavefront calls of the current rtx_render
   // adaptive AA: one buffer per level (values, first-quarter index, mask,
   // regions), grown on demand and reused by later frames (no hipMalloc /
@@ -2634,6 +2637,7 @@ struct SceneState {
   struct FrameHist {
     uint32_t sets;
     int64_t forks;
+    bool no_low = false;  // a two-entry pending stack overflowed: full stacks
   };
   std::map<uint64_t, FrameHist> bucket_hist;
   int64_t last_work[RTX_STATS_N] = {};  // raw counters of the last counting render (rtx_last_work)
@@ -2893,6 +2897,7 @@ rtx_status rtx_scene_destroy(void* scene) {
     if (X.d_bstat) (void)hipFree(X.d_bstat);
     if (X.h_bstat) (void)hipHostFree(X.h_bstat);
     if (X.bstat_ev) (void)hipEventDestroy(X.bstat_ev);
+    if (X.ovf_ev) (void)hipEventDestroy(X.ovf_ev);
     for (void* p : X.d_level)
       if (p) (void)hipFree(p);
     if (X.d_offv) (void)hipFree(X.d_offv);
@@ -3372,13 +3377,23 @@ rtx_status rtx_render(void* scene, const RtxRenderParams* params, uint8_t* rgb8,
           if (C.h_bstat[1] == 0u) {
             int64_t fm = C.bstat_groups > 0 ? 0 : -1;
             for (int g = 0; g < C.bstat_groups; ++g) fm = std::max<int64_t>(fm, C.h_bstat[4 + g]);
-            st->bucket_hist[C.bstat_key] = {C.h_bstat[0], fm};
+            st->bucket_hist[C.bstat_key] = {C.h_bstat[0], fm, false};
           } else {
             fprintf(stderr, "rtx_render: bucket pool refused a set (%u taken); frame pool reset\n", C.h_bstat[0]);
             st->bucket_hist.erase(C.bstat_key);
           }
           C.bstat_pending = false;
         }
+      if (X->ovf_pending) {  // this context's last two-entry-stack frame (long done by now)
+        HIP_TRY(hipEventSynchronize(X->ovf_ev));
+        if (X->h_bstat[2] & 4u) {
+          fprintf(stderr,
+                  "rtx_render: a two-entry pending stack overflowed: the frame rendered before this one is "
+                  "wrong; this frame and later ones use full stacks\n");
+          st->bucket_hist[X->ovf_key].no_low = true;
+        }
+        X->ovf_pending = false;
+      }
       const auto it = st->bucket_hist.find(bkey);
       if (it != st->bucket_hist.end()) {
         bcap = std::min<size_t>(nunit_out, size_t(it->second.sets) + 64);
@@ -3492,6 +3507,56 @@ rtx_status rtx_render(void* scene, const RtxRenderParams* params, uint8_t* rgb8,
     const size_t bytes_qc = al(gs * sizeof(int)) + al(gs * qc_d * sizeof(double)) + al(gs * qc_i * sizeof(int));
     const size_t nd = fuse ? QF_D : QL_D, ni = fuse ? QF_I : 2;
     const size_t bytes_qn = al(capn * sizeof(int)) + al(capn * nd * sizeof(double)) + al(capn * ni * sizeof(int));
+    // tail switch: a group whose live slots fall to this many finishes in
+    // tail_kernel (RTX_TAIL; fused walks, headline frame: 64.0 / 62.4 / 62.0
+    // ms at 200k / 400k / 1M; sequential machine: 92.6 / 91.0 / 99.5 ms at
+    // 65k / 200k / 400k)
+    int64_t tail_slots = 1000000;
+    // (a capped pool, fewer slots than units: the same share of a group's
+    // slots as 1 M is of the uncapped headline frame's 16.6 M)
+    if (int64_t(F.wf_nslot) < F.n_samples) tail_slots = std::min<int64_t>(tail_slots, gslots * 6 / 100);
+    const char* tail_env = getenv("RTX_TAIL");
+    if (tail_env) tail_slots = atoll(tail_env);
+    // RTX_TAIL_ITER=k: the tail kernel takes over at batched iteration k
+    // whatever the live count (0: by the live count only).  Default 5: the
+    // full frames have nothing left by then (46.4 vs 46.4 ms headline, 62.7
+    // vs 63.4 C4) while a shard's stragglers finish without 1-2 more
+    // launch pairs bounded by their slowest query (8-way shard 9.7 vs 10.4
+    // ms, C4's 12.1 vs 12.4; iteration 4: full frames 0.5-1.5 ms slower)
+    int tail_iter = 5;
+    const char* ti_env = getenv("RTX_TAIL_ITER");
+    if (ti_env) tail_iter = std::max(0, atoi(ti_env));
+    // (only when every unit has its sample slot from the start: with fewer
+    // slots than units, iteration 5 comes long before the units are all
+    // claimed, and the switch waits for the live count instead)
+    if (int64_t(F.wf_nslot) < F.n_samples && !ti_env) tail_iter = 0;
+    // (nor when the frame's history shows more fork requests than spares:
+    // its sub-trees then also run on their parents' stacks, one ray per
+    // iteration, and much is left at iteration 5 — R1, the glass frame:
+    // 394 -> 253 ms with the switch by live count only, profiles/r04w_*)
+    if (fspare >= 0 && !spares_enough && !ti_env) tail_iter = 0;
+    // Pending stacks of two entries, not P.depth, when every
+    // ray that pushes children forks them all: the frame's history shows every
+    // fork request granted (spares_enough — requests do not depend on the
+    // grants, so a render with at least that many spares grants them all
+    // again), every child is a node (P.depth <= fork depth + 1), and no such
+    // ray reaches the tail kernel, which does not fork (rays with children
+    // are shaded by iteration P.depth - 2; the tail starts at tail_iter, or
+    // by the live count only once a check is read, iteration 7, unless the
+    // group starts under tail_slots).  A slot then holds only its own ray.
+    // A push that would not fit sets bit 2 of *bover, read back after the
+    // frame: the host reports it and the frame's later renders use full
+    // stacks (RTX_LOW_STACK=0: never two entries).
+    bool low_stack = false;
+    {
+      const char* e = getenv("RTX_LOW_STACK");
+      const auto h = st->bucket_hist.find(bkey);
+      low_stack = !(e && atoi(e) == 0) && fuse && fork && spares_enough && spare_fit && !adaptive &&
+                  params->depth <= fork_depth + 1 && gslots > tail_slots &&
+                  (tail_iter == 0 || tail_iter >= params->depth - 1) && h != st->bucket_hist.end() &&
+                  !h->second.no_low;
+    }
+    const int pcap_run = low_stack ? std::min(pcap, 2) : pcap;
     // the slot buffers follow the pool: a first render sizes them for the
     // default pool, later renders of the frame for its fork history, and a
     // buffer much larger than this frame needs is given back (once; hipFree
@@ -3518,7 +3583,7 @@ rtx_status rtx_render(void* scene, const RtxRenderParams* params, uint8_t* rgb8,
     if ((rc = fit(&X->d_lane, &X->lane_bytes, lane_mem_bytes(ns, fuse))) != RTX_OK) return rc;
     const LaneMem A = lane_mem_at(X->d_lane, ns, fuse);
     if ((rc = fit(reinterpret_cast<void**>(&X->d_pbuf), &X->pbuf_bytes,
-                     ns * pcap * 13 * sizeof(double))) != RTX_OK)
+                     ns * pcap_run * 13 * sizeof(double))) != RTX_OK)
       return rc;
     // Fork slots go back on a free list when their sub-trees end, unless the
     // frame's history says the spares cover every request (the headline
@@ -3569,34 +3634,6 @@ rtx_status rtx_render(void* scene, const RtxRenderParams* params, uint8_t* rgb8,
     // upper bound of the live slots an iteration can see (live_bound plus
     // the forks that can still start): sizes the grids
     std::vector<int64_t> grid_bound(size_t(G), gslots);
-    // tail switch: a group whose live slots fall to this many finishes in
-    // tail_kernel (RTX_TAIL; fused walks, headline frame: 64.0 / 62.4 / 62.0
-    // ms at 200k / 400k / 1M; sequential machine: 92.6 / 91.0 / 99.5 ms at
-    // 65k / 200k / 400k)
-    int64_t tail_slots = 1000000;
-    // (a capped pool, fewer slots than units: the same share of a group's
-    // slots as 1 M is of the uncapped headline frame's 16.6 M)
-    if (int64_t(F.wf_nslot) < F.n_samples) tail_slots = std::min<int64_t>(tail_slots, gslots * 6 / 100);
-    const char* tail_env = getenv("RTX_TAIL");
-    if (tail_env) tail_slots = atoll(tail_env);
-    // RTX_TAIL_ITER=k: the tail kernel takes over at batched iteration k
-    // whatever the live count (0: by the live count only).  Default 5: the
-    // full frames have nothing left by then (46.4 vs 46.4 ms headline, 62.7
-    // vs 63.4 C4) while a shard's stragglers finish without 1-2 more
-    // launch pairs bounded by their slowest query (8-way shard 9.7 vs 10.4
-    // ms, C4's 12.1 vs 12.4; iteration 4: full frames 0.5-1.5 ms slower)
-    int tail_iter = 5;
-    const char* ti_env = getenv("RTX_TAIL_ITER");
-    if (ti_env) tail_iter = std::max(0, atoi(ti_env));
-    // (only when every unit has its sample slot from the start: with fewer
-    // slots than units, iteration 5 comes long before the units are all
-    // claimed, and the switch waits for the live count instead)
-    if (int64_t(F.wf_nslot) < F.n_samples && !ti_env) tail_iter = 0;
-    // (nor when the frame's history shows more fork requests than spares:
-    // its sub-trees then also run on their parents' stacks, one ray per
-    // iteration, and much is left at iteration 5 — R1, the glass frame:
-    // 394 -> 253 ms with the switch by live count only, profiles/r04w_*)
-    if (fspare >= 0 && !spares_enough && !ti_env) tail_iter = 0;
     F.qchunk = 64;
     // First iteration without an advance launch (fused frames): the closest-
     // hit launch claims each sample slot's first sample and queries its first
@@ -3715,16 +3752,16 @@ rtx_status rtx_render(void* scene, const RtxRenderParams* params, uint8_t* rgb8,
           if (fuse) {
             if (stats)
               hipLaunchKernelGGL((tail_fused_kernel<true>), dim3(grid), dim3(WG), lds, sg, S, X->d_scene, X->d_frame,
-                                 A, sb, d_hits, X->d_pbuf, pcap, cnt, live_in, in_cnt, st->stack_cap, st->d_stats,
+                                 A, sb, d_hits, X->d_pbuf, pcap_run, cnt, live_in, in_cnt, st->stack_cap, st->d_stats,
                                  ql[size_t(g) * 2 + 1], static_cast<int>(g * gslots));
             else
               hipLaunchKernelGGL((tail_fused_kernel<false>), dim3(grid), dim3(WG), lds, sg, S, X->d_scene, X->d_frame,
-                                 A, sb, d_hits, X->d_pbuf, pcap, cnt, live_in, in_cnt, st->stack_cap, st->d_stats,
+                                 A, sb, d_hits, X->d_pbuf, pcap_run, cnt, live_in, in_cnt, st->stack_cap, st->d_stats,
                                  ql[size_t(g) * 2 + 1], static_cast<int>(g * gslots));
           } else {
             dispatch2(stats, media, [&](auto st_, auto md_) {
               hipLaunchKernelGGL((tail_kernel<decltype(st_)::value, decltype(md_)::value>), dim3(grid), dim3(WG), lds,
-                                 sg, S, X->d_scene, X->d_frame, A, sb, d_hits, X->d_pbuf, pcap, cnt, live_in,
+                                 sg, S, X->d_scene, X->d_frame, A, sb, d_hits, X->d_pbuf, pcap_run, cnt, live_in,
                                  in_cnt, st->stack_cap, st->d_stats);
             });
           }
@@ -3760,7 +3797,7 @@ rtx_status rtx_render(void* scene, const RtxRenderParams* params, uint8_t* rgb8,
         } else if (fuse) {
           dispatch2(stats, fork, [&](auto st_, auto fk_) {
             hipLaunchKernelGGL((advance_fused_kernel<decltype(st_)::value, decltype(fk_)::value>), dim3(agrid),
-                               dim3(WG), 0, sg, S, X->d_scene, X->d_frame, A, sb, d_hits, X->d_pbuf, pcap, q0,
+                               dim3(WG), 0, sg, S, X->d_scene, X->d_frame, A, sb, d_hits, X->d_pbuf, pcap_run, q0,
                                q1, cnt, st->d_stats, static_cast<int>(g * gslots), live_in, live_out, first, in_cnt,
                                out_cnt, recycle ? X->d_free + size_t(g) * gs : nullptr);
           });
@@ -3768,7 +3805,7 @@ rtx_status rtx_render(void* scene, const RtxRenderParams* params, uint8_t* rgb8,
           dispatch3(stats, media, fork, [&](auto st_, auto md_, auto fk_) {
             hipLaunchKernelGGL((advance_kernel<decltype(st_)::value, decltype(md_)::value, decltype(fk_)::value>),
                                dim3(agrid), dim3(WG), 0, sg,
-                               S, X->d_scene, X->d_frame, A, sb, d_hits, X->d_pbuf, pcap, q0, q1, cnt,
+                               S, X->d_scene, X->d_frame, A, sb, d_hits, X->d_pbuf, pcap_run, q0, q1, cnt,
                                st->d_stats, static_cast<int>(g * gslots), live_in, live_out, first, in_cnt, out_cnt);
           });
         }
@@ -3783,7 +3820,7 @@ rtx_status rtx_render(void* scene, const RtxRenderParams* params, uint8_t* rgb8,
           sa.Fp = X->d_frame;
           sa.hits = d_hits;
           sa.pbuf = X->d_pbuf;
-          sa.pend_cap = pcap;
+          sa.pend_cap = pcap_run;
           sa.qn = q1;
           sa.slot_off = static_cast<int>(g * gslots);
           sa.live_out = live_out;
@@ -3912,6 +3949,13 @@ rtx_status rtx_render(void* scene, const RtxRenderParams* params, uint8_t* rgb8,
     for (int g = 1; g < G; ++g) HIP_TRY(hipStreamWaitEvent(ws, X->wf_join[size_t(g)], 0));
     HIP_TRY(hipEventRecord(e1, ws));
     frame_events.push_back({e0, e1});
+    if (low_stack) {  // did a push not fit?  (read at this context's next render)
+      if (!X->ovf_ev) HIP_TRY(hipEventCreateWithFlags(&X->ovf_ev, hipEventDisableTiming));
+      HIP_TRY(hipMemcpyAsync(X->h_bstat + 2, X->d_bstat + 1, sizeof(unsigned int), hipMemcpyDeviceToHost, ws));
+      HIP_TRY(hipEventRecord(X->ovf_ev, ws));
+      X->ovf_pending = true;
+      X->ovf_key = bkey;
+    }
     if (fork_ok && st->bucket_hist.find(bkey) == st->bucket_hist.end() && !X->bstat_pending) {
       // first render of this frame: its set count, read at the next call
       HIP_TRY(hipMemcpyAsync(X->h_bstat, X->d_bstat, 2 * sizeof(unsigned int), hipMemcpyDeviceToHost, ws));
