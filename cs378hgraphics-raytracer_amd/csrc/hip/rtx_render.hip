@@ -3075,14 +3075,16 @@ rtx_status rtx_render(void* scene, const RtxRenderParams* params, uint8_t* rgb8,
   rtx_status rc = build_frame(st, params, F, offv);
   if (rc != RTX_OK) return rc;
   // Only frames of at most RTX_PIPELINE_SAMPLES work units (samples x DoF
-  // camera rays; default 20 M: the shards of a multi-GPU frame) overlap: a
-  // whole headline frame's last iterations are a small share of it (32.6 /
-  // 33.2 ms against 33.5 / 32.9 without on two boxes, at twice the frame
-  // buffers), a 4-way shard's are not (8.8 vs 10.0 ms; profiles/r04k_*).
-  // RTX_PIPELINE=0: never.
+  // camera rays; default 40 M: the headline and C4 frames and the shards of
+  // a multi-GPU frame) overlap.  A whole headline frame's last iterations are
+  // a small share of it: 32.5 vs 33.0 ms on one box, bench 32.4 vs 33.1 ms
+  // (profiles/r04pipe1_*), and the scene then holds two sets of frame
+  // buffers (2 x 31 GiB); a 4-way shard gains 12 % (8.8 vs 10.0 ms,
+  // r04k_*).  Larger frames (the C5 dragon's adaptive levels are not
+  // overlapped anyway) keep one set.  RTX_PIPELINE=0: never.
   const char* mk_env0 = getenv("RTX_MEGAKERNEL");
   const char* pipe_env = getenv("RTX_PIPELINE");
-  int64_t pipe_max = 20000000;
+  int64_t pipe_max = 40000000;
   if (const char* e = getenv("RTX_PIPELINE_SAMPLES")) pipe_max = atoll(e);
   int64_t npix0 = 0;
   rtx_shard_pixels(params, &npix0);
