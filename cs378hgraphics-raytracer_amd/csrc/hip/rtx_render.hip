@@ -3074,23 +3074,26 @@ rtx_status rtx_render(void* scene, const RtxRenderParams* params, uint8_t* rgb8,
   std::vector<double> offv;
   rtx_status rc = build_frame(st, params, F, offv);
   if (rc != RTX_OK) return rc;
-  // Only frames of at most RTX_PIPELINE_SAMPLES work units (samples x DoF
-  // camera rays; default 40 M: the headline and C4 frames and the shards of
-  // a multi-GPU frame) overlap.  A whole headline frame's last iterations are
-  // a small share of it: 32.5 vs 33.0 ms on one box, bench 32.4 vs 33.1 ms
-  // (profiles/r04pipe1_*), and the scene then holds two sets of frame
-  // buffers (2 x 31 GiB); a 4-way shard gains 12 % (8.8 vs 10.0 ms,
-  // r04k_*).  Larger frames (the C5 dragon's adaptive levels are not
-  // overlapped anyway) keep one set.  RTX_PIPELINE=0: never.
+  // Which frames overlap: up to 20 M work units (samples x DoF camera rays:
+  // the shards of a multi-GPU frame; a 4-way shard gains 12 %, 8.8 vs 10.0
+  // ms, profiles/r04k_*), and up to RTX_PIPELINE_SAMPLES (default 40 M: the
+  // headline and C4 frames) when context 0 holds at most 36 GiB of frame
+  // buffers, since the scene then holds two sets: a whole headline frame's
+  // last iterations are a small share of it (32.5 vs 33.0 ms, bench 32.4 vs
+  // 33.1 ms, r04pipe1_*) — not worth R1's 2 x 71 GB.  RTX_PIPELINE=0: never.
   const char* mk_env0 = getenv("RTX_MEGAKERNEL");
   const char* pipe_env = getenv("RTX_PIPELINE");
   int64_t pipe_max = 40000000;
   if (const char* e = getenv("RTX_PIPELINE_SAMPLES")) pipe_max = atoll(e);
   int64_t npix0 = 0;
   rtx_shard_pixels(params, &npix0);
+  const int64_t units0 = npix0 * int64_t(F.spp) * int64_t(F.ncam);
+  const FrameCtx& C0 = st->cx[0];
+  const size_t held0 = C0.lane_bytes + C0.pbuf_bytes + C0.wf_bytes + C0.fbuf_bytes + C0.fmask_bytes +
+                       C0.wterm_bytes + C0.sbuf_bytes + C0.bidx_bytes + C0.free_bytes;
   const bool pipelined = !(pipe_env && atoi(pipe_env) == 0) && device_ptrs && !hits && !stats &&
                          params->aa_mode != RTX_AA_ADAPTIVE && !(mk_env0 && atoi(mk_env0) != 0) &&
-                         npix0 * int64_t(F.spp) * int64_t(F.ncam) <= pipe_max;
+                         (units0 <= 20000000 || (units0 <= pipe_max && held0 > 0 && held0 <= (size_t(36) << 30)));
   FrameCtx* X = pipelined ? &st->cx[(st->next_cx++) & 1u] : &st->cx[0];
   if (!X->free_ev) HIP_TRY(hipEventCreateWithFlags(&X->free_ev, hipEventDisableTiming));
   if (X->wf_streams.empty()) {
