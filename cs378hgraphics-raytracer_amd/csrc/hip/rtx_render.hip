@@ -3358,8 +3358,11 @@ rtx_status rtx_render(void* scene, const RtxRenderParams* params, uint8_t* rgb8,
     const size_t npos_b = (size_t(1) << (fork_depth + 1)) - 2;  // (as npos below)
     size_t bcap = nunit_out;
     bool spares_enough = false;  // the spares cover every fork request (no free list needed)
-    // spare slots per sample slot at most, in percent (RTX_SPARE, default 50)
-    int64_t spare_pct = 50;
+    // spare slots per sample slot at most, in percent (RTX_SPARE): 50 on
+    // whole frames, 100 on frames of at most 20 M units (the shards of a
+    // multi-GPU frame, whose buffers are small: R1's 8-way shard 38.3 ->
+    // 34.0 ms, the headline's and C4's unchanged, profiles/r04sp_*)
+    int64_t spare_pct = F.n_samples <= 20000000 ? 100 : 50;
     if (const char* e = getenv("RTX_SPARE")) spare_pct = std::max<int64_t>(1, std::min<int64_t>(400, atoll(e)));
     // fork slots per group the frame needs: its largest per-group count of
     // fork requests on its first render (every node child asks for a fork
