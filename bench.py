@@ -43,7 +43,11 @@ os.environ.setdefault("OMP_PLACES", "cores")
 # (kernel trace, profiles/r04i_timeline_q4.txt).  The environment may hold the
 # default explicitly (the GPU box does), so a lower value is raised.  Read
 # when HIP initialises.
-if int(os.environ.get("GPU_MAX_HW_QUEUES", "0") or 0) < 16:
+_HWQ_ENV = os.environ.get("GPU_MAX_HW_QUEUES")  # as the job got it (reported in the line)
+if int(_HWQ_ENV or 0) < 16:
+    if _HWQ_ENV:
+        print(f"bench.py: GPU_MAX_HW_QUEUES={_HWQ_ENV} in the environment raised to 16 (the frame contexts' "
+              "six group streams need queues of their own)", file=sys.stderr)
     os.environ["GPU_MAX_HW_QUEUES"] = "16"
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
@@ -54,11 +58,16 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 # (a BVH box test reads one 32-B entry of a 128-B 4-wide float record)
 B_RAY, B_NODE, B_OBJ, B_TRI, B_SHADE = 48 + 72, 32, 224, 96, 176
 # VALU issue ceiling (MI355X_MICROARCH.md: 256 CUs x 4 SIMDs at 2.4 GHz).  A
-# CDNA SIMD is 16 lanes wide, so every non-packed wave64 VALU instruction —
-# FP32, FP64 or integer — occupies it for 4 cycles (78.6 TF FP64 vector =
-# 256 x 4 x 16 lanes x 2.4 GHz x 2): wave-instructions per second
+# CDNA4 SIMD is 32 lanes wide (MI355X_MICROARCH.md "Terms", "Wave
+# scheduling", per-instruction table: v_fma_f32 wave64 2 cycles of
+# throughput), so a wave64 VALU instruction occupies its SIMD for 2 cycles;
+# FP64 runs at half the FP32 rate (78.6 vs 157.3 TFLOP/s vector), 4 cycles.
+# The ceiling is priced in SIMD cycles: 2 per non-FP64 and 4 per FP64
+# wave-instruction (the FP64 share from the PMC classes ADD/MUL/FMA/TRANS_F64).
 N_CU, SIMD_PER_CU, CLOCK_HZ = 256, 4, 2.4e9
-VALU_PEAK = N_CU * SIMD_PER_CU * CLOCK_HZ / 4
+SIMD_CYCLES_PER_S = N_CU * SIMD_PER_CU * CLOCK_HZ
+VALU_CYC, VALU_CYC_F64 = 2, 4
+VALU_PEAK = SIMD_CYCLES_PER_S / VALU_CYC  # non-FP64 wave-instructions per second
 
 
 def kernel_bytes(w):
@@ -176,11 +185,14 @@ def cpu_baseline(pkg, path, opts, height, budget_s=10.0, repeats=3):
             "_band": band, "_threads": threads}
 
 
-def parity_block(pkg, dev, path, opts, height, band, threads):
-    """Parity of the timed frame (untimed, after the CPU leg): the GPU frame
-    with its per-sample hit records against the CPU restatement's, under the
-    north-star bar of tests/parity.py — over the whole frame when the CPU leg
-    rendered it whole, else over the CPU leg's row bands."""
+def parity_block(pkg, dev, path, opts, height, band, threads, timed_rgb8=None):
+    """Parity of the benchmarked frame (untimed, after the CPU leg): the frame
+    rendered again into host buffers with its per-sample hit records, against
+    the CPU restatement's under the north-star bar of tests/parity.py — over
+    the whole frame when the CPU leg rendered it whole, else over the CPU
+    leg's row bands.  timed_rgb8: the last timed frame itself (rendered into
+    HBM on the overlapping frame contexts), compared byte for byte with that
+    host-buffer render over the whole frame."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import numpy as np
@@ -212,8 +224,14 @@ def parity_block(pkg, dev, path, opts, height, band, threads):
     m = measure(gpu["rgb"][sel], gpu["rgb8"][sel], ref_rgb[sel], ref_rgb8[sel], gpu["hits"][sel], ref_hits[sel])
     m["rows"] = "whole frame" if band >= height else [list(x) for x in rows]
     m["tolerance_rgb"] = RGB_TOL
+    ok_timed = True
+    if timed_rgb8 is not None:
+        t8 = timed_rgb8.reshape(gpu["rgb8"].shape)
+        m["timed_frame_rgb8_mismatch"] = int(np.count_nonzero(np.any(t8 != gpu["rgb8"], axis=-1)))
+        m["timed_frame_pixels"] = int(t8.shape[0] * t8.shape[1])
+        ok_timed = m["timed_frame_rgb8_mismatch"] == 0
     m["pass"] = bool(m["max_abs_rgb"] <= RGB_TOL and m["rgb8_mismatch"] == 0 and m["hit_mismatch"] == 0 and
-                     m["t_mismatch"] == 0 and m["nan_mismatch"] == 0)
+                     m["t_mismatch"] == 0 and m["nan_mismatch"] == 0 and ok_timed)
     return m
 
 
@@ -429,6 +447,8 @@ def main():
         step()
     torch.cuda.synchronize()
     dev.kernel_time()
+    dev.frame_status()  # (raises if a frame so far came out wrong: rtx_frame_status)
+    dev.overlap_count()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -448,6 +468,12 @@ def main():
     elapsed = time.perf_counter() - t0
     gpu_ms = ev0.elapsed_time(ev1)
     kms, nlaunch = dev.kernel_time()
+    # every timed frame came out right (a wrong one raises: the line is not
+    # printed), and how many of them ran on the alternating frame contexts
+    frame_check = dev.frame_status()
+    pipelined, renders = dev.overlap_count()
+    # the last timed frame, for the byte comparison in the parity block
+    timed_rgb8 = rgb8.cpu().numpy() if world == 1 else None
     # one frame alone (the frame before it finished, no overlap): the
     # latency of a frame, beside the throughput of back-to-back frames
     lat = []
@@ -465,6 +491,22 @@ def main():
         t = torch.tensor([frame_latency_ms], dtype=torch.float64, device=cdev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         frame_latency_ms = float(t.item())
+    dev.frame_status()  # (the latency frames too)
+    # N > 1: the gathered frame (the last one: every rank rendered its tiles
+    # into HBM on the overlapping frame contexts, rank 0 gathered them) against
+    # rank 0's own host-buffer render of the whole frame, byte for byte
+    gather_check = None
+    if world > 1 and rank == 0:
+        import numpy as np
+
+        full = np.zeros((height, opts.width, 3), np.uint8)
+        for r in range(world):
+            n = pkg.shard_pixels(opts, height, tile, r, world, True) * 3
+            pkg.unpack_tiles(gather_list[r][:n].cpu().numpy(), opts.width, height, tile, r, world, full)
+        ref = dev.render(opts, want_f64=False)["rgb8"].reshape(full.shape)
+        gather_check = {"rgb8_mismatch_pixels": int(np.count_nonzero(np.any(full != ref, axis=-1))),
+                        "pixels": int(height * opts.width),
+                        "against": "rank 0's host-buffer render of the whole frame"}
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=cdev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -520,12 +562,20 @@ def main():
         # the frame's GPU time / the issue peak = the measured share of VALU
         # issue cycles
         valu = totals.get("SQ_INSTS_VALU")
-        frac_valu = round(valu / (avg_kernel_ms * 1e-3) / VALU_PEAK, 4) if valu else None
         f64 = sum(totals.get(k, 0.0) for k in ("SQ_INSTS_VALU_ADD_F64", "SQ_INSTS_VALU_MUL_F64",
                                                  "SQ_INSTS_VALU_FMA_F64", "SQ_INSTS_VALU_TRANS_F64"))
+        valu_cycles = (VALU_CYC * (valu - f64) + VALU_CYC_F64 * f64) if valu else None
+        frac_valu = round(valu_cycles / (avg_kernel_ms * 1e-3) / SIMD_CYCLES_PER_S, 4) if valu else None
         frac_hbm = round(traffic / (avg_kernel_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4) if traffic else None
         # the ceiling the frame is closer to, by the measured fractions
-        bound = "valu" if frac_valu and (frac_hbm is None or frac_valu > frac_hbm) else "hbm"
+        # the roofline priced is HBM's (north star: achieved HBM GB/s against
+        # the gfx950 peak; no MFMA on this path).  What limits the frame is
+        # named beside it from the measured fractions: a ceiling past half its
+        # peak, else dependent-load latency (neither is)
+        bound = "hbm"
+        fr = {"valu": frac_valu or 0.0, "hbm": frac_hbm or 0.0}
+        top = max(fr, key=fr.get)
+        limiter = top if fr[top] >= 0.5 else "latency"
         kernels = st.get("kernels") or {}
         for w in kernels.values():
             w["algorithmic_bytes"] = kernel_bytes(w)
@@ -534,7 +584,7 @@ def main():
             cpu = cpu_baseline(pkg, args.scene, opts, height, args.cpu_budget)
             band, threads = cpu.pop("_band"), cpu.pop("_threads")
             if not args.no_parity:
-                parity = parity_block(pkg, dev, args.scene, opts, height, band, threads)
+                parity = parity_block(pkg, dev, args.scene, opts, height, band, threads, timed_rgb8)
         line = {
             "metric": METRIC, "value": round(value, 3), "unit": "Mrays/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3),
@@ -545,15 +595,17 @@ def main():
                        "parallelism": ((f"REHEARSAL: {world} ranks sharing one GPU, gloo gather through host memory"
                                         " (not an N-GPU measurement)") if rehearsal else
                                        f"tile-shard x{world} + RCCL gather" if world > 1 else "single GPU")},
-            "roofline": {"bound": bound, "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "roofline": {"bound": bound, "limiter": limiter if (frac_valu or frac_hbm) else None, "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                          # measured: PMC HBM bytes of a frame / the frame's GPU time / peak
                          "frac_hbm": frac_hbm,
-                         # measured: VALU wave-instructions of a frame / GPU time / issue
-                         # peak (4 cycles per wave64 instruction on a 16-lane SIMD)
+                         # measured: SIMD cycles the frame's VALU instructions occupy (2 per
+                         # wave64 instruction on a 32-lane SIMD, 4 for FP64) / GPU time /
+                         # SIMD cycles available (256 CUs x 4 SIMDs x 2.4 GHz)
                          "frac_valu": frac_valu,
-                         "valu_insts": valu, "valu_f64_insts": f64 or None,
-                         "valu_peak_per_s": VALU_PEAK,
+                         "valu_insts": valu, "valu_f64_insts": f64 or None, "valu_simd_cycles": valu_cycles,
+                         "valu_cycles_per_inst": {"non_f64": VALU_CYC, "f64": VALU_CYC_F64},
+                         "simd_cycles_per_s": SIMD_CYCLES_PER_S,
                          "traffic_source": traffic_src,
                          "kernel": ("render_kernel<false,false> (megakernel, 1 launch per frame)" if mega else
                                     "frame: advance_kernel + trace_kernel<false,1|2> iterations on 3 streams, "
@@ -580,7 +632,14 @@ def main():
             # throughput, frame_latency_ms one frame rendered alone (render
             # + gather, max over ranks)
             "frame_latency_ms": round(frame_latency_ms, 3),
-            "frame_contexts": 2,
+            # timed frames that ran pipelined on the two frame contexts
+            # (rtx_overlap_count), and the frame check of the timed frames
+            # (rtx_frame_status: first wrong frame, wrong frames)
+            "frame_contexts": 2 if pipelined == renders and renders > 0 else (1 if pipelined == 0 else "mixed"),
+            "pipelined_frames": [pipelined, renders],
+            "frame_check": {"first_bad": frame_check[0], "bad_frames": frame_check[1]},
+            "gather_check": gather_check,
+            "gpu_max_hw_queues": {"effective": os.environ.get("GPU_MAX_HW_QUEUES"), "environment": _HWQ_ENV},
             "mrays_traced_per_s": round(traced_rays * args.steps / elapsed / 1e6, 3),
             "build": {"build_id": build_id(), "lib_sha256": lib_hash},
         }

@@ -27,6 +27,7 @@ BIN_DIR = os.path.join(PKG_DIR, "bin")
 REPO_ROOT = os.path.dirname(PKG_DIR)
 
 RTX_AA_NONE, RTX_AA_SUPERSAMPLE, RTX_AA_ADAPTIVE, RTX_AA_JITTERED = 0, 1, 2, 3
+RTX_OK, RTX_ERR_INVALID, RTX_ERR_HIP, RTX_ERR_NODEVICE, RTX_ERR_CAPACITY, RTX_ERR_FRAME = 0, -1, -2, -3, -4, -5  # include/rtx.h
 
 
 class RtxError(RuntimeError):
@@ -155,13 +156,15 @@ def hip_lib():
         lib.rtx_shard_pixels.argtypes = [C.POINTER(RtxRenderParams), C.POINTER(C.c_int64)]
         lib.rtx_kernel_time.argtypes = [C.c_void_p, C.POINTER(C.c_double), C.POINTER(C.c_int)]
         lib.rtx_last_work.argtypes = [C.c_void_p, C.POINTER(C.c_int64), C.c_int]
+        lib.rtx_frame_status.argtypes = [C.c_void_p, C.POINTER(C.c_int64), C.POINTER(C.c_int64)]
+        lib.rtx_overlap_count.argtypes = [C.c_void_p, C.POINTER(C.c_int64), C.POINTER(C.c_int64)]
         _hip = lib
     return _hip
 
 
 # symbols include/*.h declare (checked by the CPU test suite)
 HIP_SYMBOLS = ["rtx_last_error", "rtx_device_count", "rtx_scene_create", "rtx_scene_destroy", "rtx_render",
-               "rtx_shard_pixels", "rtx_kernel_time", "rtx_last_work"]
+               "rtx_shard_pixels", "rtx_kernel_time", "rtx_last_work", "rtx_frame_status", "rtx_overlap_count"]
 HOST_SYMBOLS = ["rtx_host_last_error", "rtx_host_load", "rtx_host_desc", "rtx_host_info", "rtx_host_free",
                 "rtx_host_cubemap", "rtx_write_image", "rtx_image_height", "rtx_read_image", "rtx_shard_tiles",
                 "rtx_unpack_tiles", "rtx_host_tokens", "rtx_host_raw_records"]
@@ -389,6 +392,24 @@ class DeviceScene:
         n = C.c_int()
         _check(lib.rtx_kernel_time(self._s, C.byref(ms), C.byref(n)), lib, "rtx_kernel_time")
         return ms.value, n.value
+
+    def frame_status(self, raise_on_bad: bool = True):
+        """Outcome of the device-buffer renders issued so far (rtx_frame_status):
+        (first_bad, bad_frames), (-1, 0) when every frame came out right.
+        Raises RtxError on a wrong frame unless raise_on_bad is False."""
+        lib = hip_lib()
+        fb, nb = C.c_int64(), C.c_int64()
+        rc = lib.rtx_frame_status(self._s, C.byref(fb), C.byref(nb))
+        if rc != 0 and (raise_on_bad or rc != RTX_ERR_FRAME):
+            _check(rc, lib, "rtx_frame_status")
+        return fb.value, nb.value
+
+    def overlap_count(self):
+        """(pipelined renders, renders) since the last call (rtx_overlap_count)."""
+        lib = hip_lib()
+        a, b = C.c_int64(), C.c_int64()
+        _check(lib.rtx_overlap_count(self._s, C.byref(a), C.byref(b)), lib, "rtx_overlap_count")
+        return a.value, b.value
 
     def close(self):
         if self._s:

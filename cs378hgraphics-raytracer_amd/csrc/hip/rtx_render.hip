@@ -27,6 +27,7 @@
 #include <cstdio>
 #include <cstring>
 #include <memory>
+#include <set>
 #include <string>
 #include <type_traits>
 #include <map>
@@ -2586,9 +2587,13 @@ struct FrameCtx {
   bool bstat_pending = false;
   uint64_t bstat_key = 0;
   int bstat_groups = 0;  // groups whose fork counts were read back (0: the frame did not fork)
-  hipEvent_t ovf_ev = nullptr;  // the last two-entry-stack frame's *bover, read back into h_bstat[2]
-  bool ovf_pending = false;
-  uint64_t ovf_key = 0;
+  // the last history-sized frame's check: its *bover (bit 1 a bucket set
+  // refused, bit 2 a push that fit neither a fork slot nor the two-entry
+  // stack), read back into h_bstat[2]; chk_keys are the frame's history keys
+  hipEvent_t chk_ev = nullptr;
+  bool chk_pending = false;
+  int64_t chk_seq = -1;
+  std::vector<uint64_t> chk_keys;
   int wf_call = 0;  // run_wavefront calls of the current rtx_render
   // adaptive AA: one buffer per level (values, first-quarter index, mask,
   // regions), grown on demand and reused by later frames (no hipMalloc /
@@ -2637,9 +2642,17 @@ struct SceneState {
   struct FrameHist {
     uint32_t sets;
     int64_t forks;
-    bool no_low = false;  // a two-entry pending stack overflowed: full stacks
   };
   std::map<uint64_t, FrameHist> bucket_hist;
+  // frames whose two-entry pending stacks overflowed once: full stacks from
+  // then on
+  std::set<uint64_t> full_stack_keys;
+  // rtx_render calls so far (a frame's sequence number), the wrong frames
+  // found since the last rtx_frame_status, pipelined renders counted for
+  // rtx_overlap_count
+  int64_t frame_seq = 0;
+  int64_t bad_first = -1, bad_n = 0;
+  int64_t n_renders = 0, n_pipelined = 0;
   int64_t last_work[RTX_STATS_N] = {};  // raw counters of the last counting render (rtx_last_work)
   std::vector<hipEvent_t> ev_pool;
   size_t ev_used = 0;
@@ -2880,11 +2893,71 @@ rtx_status rtx_scene_create(int device, const RtxSceneDesc* d, void** out) {
   return RTX_OK;
 }
 
+// Context X's last history-sized frame: did its history fall short?  (wait:
+// block until the check has run, else only take it if it has.)  A refused
+// bucket set (bit 1) drops ray-tree colours and a push that fit neither a
+// fork slot nor a two-entry stack (bit 2) drops a ray: either way the frame
+// is wrong.  Its history is corrected — bucket pool back to a first render's
+// size, full pending stacks — so the frame's later renders are right; the
+// frame itself is recorded (rtx_frame_status) and reported.  Returns whether
+// that frame was wrong.
+static bool collect_check(SceneState* st, FrameCtx& X, bool wait) {
+  if (!X.chk_pending) return false;
+  if (wait) {
+    if (hipEventSynchronize(X.chk_ev) != hipSuccess) return false;
+  } else if (hipEventQuery(X.chk_ev) != hipSuccess) {
+    return false;
+  }
+  X.chk_pending = false;
+  const unsigned int bits = X.h_bstat[2];
+  if (!(bits & 7u)) return false;
+  for (uint64_t k : X.chk_keys) {
+    if (bits & 3u) st->bucket_hist.erase(k);
+    if (bits & 4u) st->full_stack_keys.insert(k);
+  }
+  if (st->bad_n++ == 0) st->bad_first = X.chk_seq;
+  fprintf(stderr,
+          "rtx_render: frame %lld (this scene's render %lld) is wrong: %s; its later renders use full-size "
+          "buffers (rtx_frame_status reports it)\n",
+          static_cast<long long>(X.chk_seq), static_cast<long long>(X.chk_seq),
+          (bits & 4u) ? "a two-entry pending stack overflowed" : "the bucket-set pool refused a set");
+  return true;
+}
+
+rtx_status rtx_frame_status(void* scene, int64_t* first_bad, int64_t* bad_frames) {
+  if (!scene) return RTX_ERR_INVALID;
+  SceneState* st = static_cast<SceneState*>(scene);
+  HIP_TRY(hipSetDevice(st->device));
+  for (FrameCtx& X : st->cx) collect_check(st, X, true);
+  const int64_t fb = st->bad_first, nb = st->bad_n;
+  st->bad_first = -1;
+  st->bad_n = 0;
+  if (first_bad) *first_bad = fb;
+  if (bad_frames) *bad_frames = nb;
+  if (nb > 0) {
+    g_err = "rtx_frame_status: " + std::to_string(nb) + " frame(s) came out wrong, the first is render " +
+            std::to_string(fb) + " of this scene";
+    return RTX_ERR_FRAME;
+  }
+  return RTX_OK;
+}
+
+rtx_status rtx_overlap_count(void* scene, int64_t* overlapped, int64_t* renders) {
+  if (!scene) return RTX_ERR_INVALID;
+  SceneState* st = static_cast<SceneState*>(scene);
+  if (overlapped) *overlapped = st->n_pipelined;
+  if (renders) *renders = st->n_renders;
+  st->n_pipelined = 0;
+  st->n_renders = 0;
+  return RTX_OK;
+}
+
 rtx_status rtx_scene_destroy(void* scene) {
   if (!scene) return RTX_OK;
   SceneState* st = static_cast<SceneState*>(scene);
   (void)hipSetDevice(st->device);
   (void)hipDeviceSynchronize();  // (pipelined frames may still be in flight)
+  for (FrameCtx& X : st->cx) collect_check(st, X, true);  // (reported on stderr)
   for (void* p : st->allocs) (void)hipFree(p);
   if (st->d_work) (void)hipFree(st->d_work);
   if (st->d_stats) (void)hipFree(st->d_stats);
@@ -2897,7 +2970,7 @@ rtx_status rtx_scene_destroy(void* scene) {
     if (X.d_bstat) (void)hipFree(X.d_bstat);
     if (X.h_bstat) (void)hipHostFree(X.h_bstat);
     if (X.bstat_ev) (void)hipEventDestroy(X.bstat_ev);
-    if (X.ovf_ev) (void)hipEventDestroy(X.ovf_ev);
+    if (X.chk_ev) (void)hipEventDestroy(X.chk_ev);
     for (void* p : X.d_level)
       if (p) (void)hipFree(p);
     if (X.d_offv) (void)hipFree(X.d_offv);
@@ -3054,13 +3127,12 @@ rtx_status rtx_shard_pixels(const RtxRenderParams* p, int64_t* npix) {
   return RTX_OK;
 }
 
-rtx_status rtx_render(void* scene, const RtxRenderParams* params, uint8_t* rgb8, double* rgb_f64,
-                      RtxHitRecord* hits, int device_ptrs, void* stream_v, RtxStats* stats) {
-  if (!scene || !params) {
-    g_err = "rtx_render: null argument";
-    return RTX_ERR_INVALID;
-  }
-  SceneState* st = static_cast<SceneState*>(scene);
+// One render of frame `seq` (rtx_render below).  *redo: this synchronous
+// render found its history-sized buffers short (collect_check) — the image
+// is wrong and the caller renders again, now with full-size buffers.
+static rtx_status render_once(SceneState* st, const RtxRenderParams* params, uint8_t* rgb8, double* rgb_f64,
+                              RtxHitRecord* hits, int device_ptrs, void* stream_v, RtxStats* stats, int64_t seq,
+                              bool retry, bool* redo) {
   HIP_TRY(hipSetDevice(st->device));
   hipStream_t stream = static_cast<hipStream_t>(stream_v);
   // Frame context (DESIGN.md "Frame contexts"): a render into device buffers
@@ -3074,27 +3146,34 @@ rtx_status rtx_render(void* scene, const RtxRenderParams* params, uint8_t* rgb8,
   std::vector<double> offv;
   rtx_status rc = build_frame(st, params, F, offv);
   if (rc != RTX_OK) return rc;
-  // Which frames overlap: up to 20 M work units (samples x DoF camera rays:
-  // the shards of a multi-GPU frame; a 4-way shard gains 12 %, 8.8 vs 10.0
-  // ms, profiles/r04k_*), and up to RTX_PIPELINE_SAMPLES (default 40 M: the
-  // headline and C4 frames) when context 0 holds at most 36 GiB of frame
-  // buffers, since the scene then holds two sets: a whole headline frame's
-  // last iterations are a small share of it (32.5 vs 33.0 ms, bench 32.4 vs
-  // 33.1 ms, r04pipe1_*) — not worth R1's 2 x 71 GB.  RTX_PIPELINE=0: never.
+  // Which frames overlap: at most RTX_PIPELINE_SAMPLES work units (samples x
+  // DoF camera rays; default 20 M: the shards of a multi-GPU frame — a 4-way
+  // shard gains 12 %, 8.8 vs 10.0 ms, an 8-way one 20 %, profiles/r04k_*).
+  // A whole frame renders on one context, with one set of frame buffers: its
+  // last iterations are a small share of it (the headline frame back to back
+  // 32.5 vs 33.0 ms with two ~31-GiB sets, r04pipe1_*), not worth a second
+  // set.  RTX_PIPELINE=0: never.
   const char* mk_env0 = getenv("RTX_MEGAKERNEL");
   const char* pipe_env = getenv("RTX_PIPELINE");
-  int64_t pipe_max = 40000000;
+  int64_t pipe_max = 20000000;
   if (const char* e = getenv("RTX_PIPELINE_SAMPLES")) pipe_max = atoll(e);
   int64_t npix0 = 0;
   rtx_shard_pixels(params, &npix0);
   const int64_t units0 = npix0 * int64_t(F.spp) * int64_t(F.ncam);
-  const FrameCtx& C0 = st->cx[0];
-  const size_t held0 = C0.lane_bytes + C0.pbuf_bytes + C0.wf_bytes + C0.fbuf_bytes + C0.fmask_bytes +
-                       C0.wterm_bytes + C0.sbuf_bytes + C0.bidx_bytes + C0.free_bytes;
   const bool pipelined = !(pipe_env && atoi(pipe_env) == 0) && device_ptrs && !hits && !stats &&
                          params->aa_mode != RTX_AA_ADAPTIVE && !(mk_env0 && atoi(mk_env0) != 0) &&
-                         (units0 <= 20000000 || (units0 <= pipe_max && held0 > 0 && held0 <= (size_t(36) << 30)));
+                         units0 <= pipe_max;
   FrameCtx* X = pipelined ? &st->cx[(st->next_cx++) & 1u] : &st->cx[0];
+  if (!retry) {
+    ++st->n_renders;
+    if (pipelined) ++st->n_pipelined;
+  }
+  // the frame checks of earlier renders: this context's (its frame is long
+  // done: the check is read before its buffers are reused), the other's if
+  // it has run
+  collect_check(st, *X, true);
+  collect_check(st, st->cx[X == &st->cx[0] ? 1 : 0], false);
+  std::vector<uint64_t> chk_keys;  // this frame's history-sized runs (run_wavefront)
   if (!X->free_ev) HIP_TRY(hipEventCreateWithFlags(&X->free_ev, hipEventDisableTiming));
   if (X->wf_streams.empty()) {
     hipStream_t s0;
@@ -3382,29 +3461,23 @@ rtx_status rtx_render(void* scene, const RtxRenderParams* params, uint8_t* rgb8,
       for (FrameCtx& C : st->cx)  // the first-time frames' counts (either context's; long done by now)
         if (C.bstat_pending) {
           HIP_TRY(hipEventSynchronize(C.bstat_ev));
-          if (C.h_bstat[1] == 0u) {
+          if ((C.h_bstat[1] & 3u) == 0u) {  // (bit 2, a two-entry stack's overflow: the frame check's)
             int64_t fm = C.bstat_groups > 0 ? 0 : -1;
             for (int g = 0; g < C.bstat_groups; ++g) fm = std::max<int64_t>(fm, C.h_bstat[4 + g]);
-            st->bucket_hist[C.bstat_key] = {C.h_bstat[0], fm, false};
+            st->bucket_hist[C.bstat_key] = {C.h_bstat[0], fm};
           } else {
             fprintf(stderr, "rtx_render: bucket pool refused a set (%u taken); frame pool reset\n", C.h_bstat[0]);
             st->bucket_hist.erase(C.bstat_key);
           }
           C.bstat_pending = false;
         }
-      if (X->ovf_pending) {  // this context's last two-entry-stack frame (long done by now)
-        HIP_TRY(hipEventSynchronize(X->ovf_ev));
-        if (X->h_bstat[2] & 4u) {
-          fprintf(stderr,
-                  "rtx_render: a two-entry pending stack overflowed: the frame rendered before this one is "
-                  "wrong; this frame and later ones use full stacks\n");
-          st->bucket_hist[X->ovf_key].no_low = true;
-        }
-        X->ovf_pending = false;
-      }
       const auto it = st->bucket_hist.find(bkey);
       if (it != st->bucket_hist.end()) {
         bcap = std::min<size_t>(nunit_out, size_t(it->second.sets) + 64);
+        // (test knob: a history that falls short, so the frame check and the
+        // re-render can be exercised — tests/test_gpu_parity.py)
+        if (const char* e = getenv("RTX_TEST_SHORT_POOL"))
+          if (atoi(e) != 0) bcap = std::max<size_t>(1, size_t(it->second.sets) / 2);
         // (never more than the half slot per sample of the default pool)
         if (it->second.forks >= 0) {
           fspare = std::min<int64_t>(it->second.forks, (F.n_samples + G - 1) / G * spare_pct / 100);
@@ -3426,7 +3499,10 @@ rtx_status rtx_render(void* scene, const RtxRenderParams* params, uint8_t* rgb8,
       if (bucket_need > avail / 2) fork_ok = false;  // buckets would crowd out the slots: plain accumulation
       // what the pooled sets take (bcap sets, a mask and a set index per unit)
       const size_t pool_need = fork_ok ? bcap * npos * 3 * sizeof(double) + nunit_out * 2 * sizeof(unsigned) : 0;
-      size_t slot_budget = std::min<size_t>(size_t(96) << 30, avail - pool_need);
+      // (unsigned: with less free memory than the pool needs the slots get
+      // nothing — the pool is then floored below — never a wrapped-around
+      // 96 GiB)
+      size_t slot_budget = avail > pool_need ? std::min<size_t>(size_t(96) << 30, avail - pool_need) : 0;
       // Frame-memory cap (RTX_MEM_GB GiB, default none): the slot pool
       // gets what the cap leaves after the sample sums and the buckets.  The
       // buckets keep their size — whether a frame has buckets must not
@@ -3466,6 +3542,16 @@ rtx_status rtx_render(void* scene, const RtxRenderParams* params, uint8_t* rgb8,
     const int64_t gslots = per * WG;
     if (!fork) gsamp = gslots;
     nslot64 = gslots * G;
+    // What the kernels assume of this geometry, checked before anything is
+    // launched: slot ids, sample slots and bucket owners are int32 (LaneRef,
+    // slot_unit, claim_sample's sample_slot / bunit), every group's sample
+    // slots lie inside its slots (fork slots follow them), and the output
+    // slots' samples fit the sample buffer.
+    if (nslot64 > INT32_MAX || gsamp * G > INT32_MAX || gsamp > gslots || gslots < WG ||
+        int64_t(nout) * F.spp * (F.cam_split ? F.ncam : 1) > INT32_MAX || F.n_samples > INT64_C(1) << 40) {
+      g_err = "rtx_render: frame too large for this build (slot, sample or bucket index past int32)";
+      return RTX_ERR_CAPACITY;
+    }
     F.wf_nslot = static_cast<int>(gsamp * G);
     F.wf_gs = static_cast<int>(gslots);
     F.wf_gsamp = static_cast<int>(gsamp);
@@ -3496,7 +3582,9 @@ rtx_status rtx_render(void* scene, const RtxRenderParams* params, uint8_t* rgb8,
       if (!X->d_bstat) HIP_TRY(hipMalloc(&X->d_bstat, 4 * sizeof(unsigned int)));
       if (!X->h_bstat) HIP_TRY(hipHostMalloc(&X->h_bstat, (4 + 16) * sizeof(unsigned int)));
       if (!X->bstat_ev) HIP_TRY(hipEventCreateWithFlags(&X->bstat_ev, hipEventDisableTiming));
-      HIP_TRY(hipMemsetAsync(X->d_bstat, 0, 4 * sizeof(unsigned int), ws));
+      // ([taken] per run; [bover] once per render: the frame check reads it
+      // after the frame's last run)
+      HIP_TRY(hipMemsetAsync(X->d_bstat, 0, (X->wf_call == 0 ? 4 : 1) * sizeof(unsigned int), ws));
       F.fbuf = X->d_fbuf;
       F.fmask = X->d_fmask;
       F.bidx = X->d_bidx;
@@ -3555,14 +3643,17 @@ rtx_status rtx_render(void* scene, const RtxRenderParams* params, uint8_t* rgb8,
     // A push that would not fit sets bit 2 of *bover, read back after the
     // frame: the host reports it and the frame's later renders use full
     // stacks (RTX_LOW_STACK=0: never two entries).
+    // (RTX_LOW_STACK=2, a test knob: two entries whatever the history says,
+    // so the overflow check and the re-render can be exercised)
     bool low_stack = false;
     {
       const char* e = getenv("RTX_LOW_STACK");
-      const auto h = st->bucket_hist.find(bkey);
-      low_stack = !(e && atoi(e) == 0) && fuse && fork && spares_enough && spare_fit && !adaptive &&
-                  params->depth <= fork_depth + 1 && gslots > tail_slots &&
-                  (tail_iter == 0 || tail_iter >= params->depth - 1) && h != st->bucket_hist.end() &&
-                  !h->second.no_low;
+      const int ls_mode = e ? atoi(e) : 1;
+      const bool proven = spares_enough && spare_fit && params->depth <= fork_depth + 1 && gslots > tail_slots &&
+                          (tail_iter == 0 || tail_iter >= params->depth - 1) &&
+                          st->bucket_hist.find(bkey) != st->bucket_hist.end();
+      low_stack = fuse && fork && !adaptive && !st->full_stack_keys.count(bkey) &&
+                  (ls_mode == 2 || (ls_mode == 1 && proven));
     }
     const int pcap_run = low_stack ? std::min(pcap, 2) : pcap;
     // the slot buffers follow the pool: a first render sizes them for the
@@ -3662,6 +3753,10 @@ rtx_status rtx_render(void* scene, const RtxRenderParams* params, uint8_t* rgb8,
         c += std::min<int64_t>(std::min<int64_t>(64, gsamp - b * 64), F.n_samples - base);
       }
       cam_n[size_t(g)] = static_cast<int>(c);
+      if (c > gsamp) {  // (never: the first units are a prefix of the sample slots)
+        g_err = "rtx_render: internal error: first-launch claims exceed a group's sample slots";
+        return RTX_ERR_INVALID;
+      }
     }
     if ((rc = stage_copy(st, X->d_frame, &F, sizeof(FrameParams), ws)) != RTX_OK) return rc;
     // every slot starts ST_IDLE, kdone = 0, outside a discoverMat walk, no
@@ -3957,13 +4052,9 @@ rtx_status rtx_render(void* scene, const RtxRenderParams* params, uint8_t* rgb8,
     for (int g = 1; g < G; ++g) HIP_TRY(hipStreamWaitEvent(ws, X->wf_join[size_t(g)], 0));
     HIP_TRY(hipEventRecord(e1, ws));
     frame_events.push_back({e0, e1});
-    if (low_stack) {  // did a push not fit?  (read at this context's next render)
-      if (!X->ovf_ev) HIP_TRY(hipEventCreateWithFlags(&X->ovf_ev, hipEventDisableTiming));
-      HIP_TRY(hipMemcpyAsync(X->h_bstat + 2, X->d_bstat + 1, sizeof(unsigned int), hipMemcpyDeviceToHost, ws));
-      HIP_TRY(hipEventRecord(X->ovf_ev, ws));
-      X->ovf_pending = true;
-      X->ovf_key = bkey;
-    }
+    // a run sized from its history (two-entry stacks, a pool of the last
+    // render's set count) is checked once the frame has run (rtx_render's end)
+    if (low_stack || (fork_ok && bcap < nunit_out)) chk_keys.push_back(bkey);
     if (fork_ok && st->bucket_hist.find(bkey) == st->bucket_hist.end() && !X->bstat_pending) {
       // first render of this frame: its set count, read at the next call
       HIP_TRY(hipMemcpyAsync(X->h_bstat, X->d_bstat, 2 * sizeof(unsigned int), hipMemcpyDeviceToHost, ws));
@@ -4068,6 +4159,15 @@ rtx_status rtx_render(void* scene, const RtxRenderParams* params, uint8_t* rgb8,
     st->ev_start.push_back(pr.first);
     st->ev_stop.push_back(pr.second);
   }
+  // the frame check (collect_check): the runs' *bover, once they have run
+  if (!chk_keys.empty()) {
+    if (!X->chk_ev) HIP_TRY(hipEventCreateWithFlags(&X->chk_ev, hipEventDisableTiming));
+    HIP_TRY(hipMemcpyAsync(X->h_bstat + 2, X->d_bstat + 1, sizeof(unsigned int), hipMemcpyDeviceToHost, ws));
+    HIP_TRY(hipEventRecord(X->chk_ev, ws));
+    X->chk_pending = true;
+    X->chk_seq = seq;
+    X->chk_keys = chk_keys;
+  }
   // the context is free again once the caller's stream has passed the frame
   // (its reduce on the caller's stream; ws == stream for the other renders)
   HIP_TRY(hipEventRecord(X->free_ev, stream));
@@ -4077,6 +4177,18 @@ rtx_status rtx_render(void* scene, const RtxRenderParams* params, uint8_t* rgb8,
     if (rgb_f64) HIP_TRY(hipMemcpyAsync(rgb_f64, d_rgbf, npix * 3 * sizeof(double), hipMemcpyDeviceToHost, ws));
     if (hits) HIP_TRY(hipMemcpyAsync(hits, d_hits, npix * F.spp * sizeof(RtxHitRecord), hipMemcpyDeviceToHost, ws));
     HIP_TRY(hipStreamSynchronize(ws));
+  }
+  // a synchronous render (host buffers, counters, adaptive levels) knows its
+  // outcome now: a wrong frame is rendered again (rtx_render), never returned
+  if (X->chk_pending && (!device_ptrs || stats || adaptive)) {
+    HIP_TRY(hipStreamSynchronize(ws));
+    const int64_t nb = st->bad_n, fb = st->bad_first;
+    if (collect_check(st, *X, true)) {
+      st->bad_n = nb;  // (not recorded: the caller gets the re-rendered frame)
+      st->bad_first = fb;
+      *redo = true;
+      return RTX_OK;
+    }
   }
   if (stats) {
     unsigned long long c[RTX_STATS_N];
@@ -4124,6 +4236,28 @@ rtx_status rtx_render(void* scene, const RtxRenderParams* params, uint8_t* rgb8,
     for (int k = 0; k < RTX_STATS_N; ++k) st->last_work[k] = static_cast<int64_t>(c[k]);
   }
   return RTX_OK;
+}
+
+rtx_status rtx_render(void* scene, const RtxRenderParams* params, uint8_t* rgb8, double* rgb_f64,
+                      RtxHitRecord* hits, int device_ptrs, void* stream_v, RtxStats* stats) {
+  if (!scene || !params) {
+    g_err = "rtx_render: null argument";
+    return RTX_ERR_INVALID;
+  }
+  SceneState* st = static_cast<SceneState*>(scene);
+  const int64_t seq = st->frame_seq++;
+  bool redo = false;
+  rtx_status rc = render_once(st, params, rgb8, rgb_f64, hits, device_ptrs, stream_v, stats, seq, false, &redo);
+  if (rc == RTX_OK && redo) {
+    fprintf(stderr, "rtx_render: rendering frame %lld again with full-size buffers\n", static_cast<long long>(seq));
+    redo = false;
+    rc = render_once(st, params, rgb8, rgb_f64, hits, device_ptrs, stream_v, stats, seq, true, &redo);
+    if (rc == RTX_OK && redo) {
+      g_err = "rtx_render: the frame came out wrong twice (history-sized buffers short after a full-size re-render)";
+      return RTX_ERR_FRAME;
+    }
+  }
+  return rc;
 }
 
 rtx_status rtx_last_work(void* scene, int64_t* out, int n) {

@@ -197,6 +197,12 @@ int run_rank(const rtxh::CliOptions& o, void* hs, int rank, int nranks, Rendezvo
   }
   NCCL_CHECK(ncclGather(d_send, d_recv, shard_bytes, ncclUint8, 0, comm, stream), "ncclGather");
   HIP_CHECK(hipStreamSynchronize(stream), "hipStreamSynchronize");
+  // the device-buffer render's outcome (rtx_frame_status): a frame known to
+  // be wrong fails the rank, and with it the job
+  if (rtx_frame_status(scene, nullptr, nullptr) != RTX_OK) {
+    std::cerr << "rank " << rank << ": rtx: " << rtx_last_error() << std::endl;
+    return 2;
+  }
   rv->rank_ms[rank % 64] = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   rv->rank_rays[rank % 64] = o.stats ? st.rays : 0;
   int rc = 0;

@@ -39,7 +39,9 @@ enum {
   RTX_ERR_INVALID = -1,   /* bad argument / unsupported option         */
   RTX_ERR_HIP = -2,       /* HIP runtime error (see rtx_last_error)     */
   RTX_ERR_NODEVICE = -3,  /* no gfx950 device visible                   */
-  RTX_ERR_CAPACITY = -4   /* scene exceeds a compiled limit             */
+  RTX_ERR_CAPACITY = -4,  /* scene exceeds a compiled limit             */
+  RTX_ERR_FRAME = -5      /* a frame rendered into device buffers came
+                             out wrong (rtx_frame_status names it)       */
 };
 
 /* ---- flat scene layout (host arrays; the library copies them to HBM) ---- */
@@ -239,6 +241,12 @@ rtx_status rtx_scene_destroy(void* scene);
  * outputs are device (HBM) pointers written asynchronously on `stream`
  * (a hipStream_t, NULL = default stream); otherwise they are host pointers
  * and the call is synchronous.
+ * A synchronous render (host pointers, or `stats`) never returns RTX_OK with
+ * a wrong image: when a frame sized from its own history (two-entry pending
+ * stacks, a bucket-set pool of the last render's size) finds the history
+ * short, the call renders the frame again with full-size buffers
+ * (RTX_ERR_FRAME if that fails too).  An asynchronous render's outcome is
+ * known only once its stream has run it: rtx_frame_status reports it.
  *   rgb8    : 3 bytes per pixel, (int)(255*c) truncation (RayTracer.cpp:388-394)
  *   rgb_f64 : 3 doubles per pixel, the value setPixel receives
  *   hits    : aa samples per pixel records (sample order si-major)
@@ -267,6 +275,23 @@ rtx_status rtx_last_work(void* scene, int64_t* out, int n);
 /* Device time (ms) of render kernels launched since the last call, read
  * from hipEvents recorded on the render stream; synchronizes those events. */
 rtx_status rtx_kernel_time(void* scene, double* total_ms, int* launches);
+
+/* Outcome of the asynchronous (device-buffer) renders issued so far on this
+ * scene: waits for their device-side checks, then returns RTX_OK when every
+ * one produced the image the reference would, or RTX_ERR_FRAME when one
+ * did not (a history-sized buffer overflowed: the frame's later renders
+ * already use full-size buffers).  *first_bad (may be NULL) receives the
+ * 0-based sequence number of the first wrong frame among this scene's
+ * rtx_render calls, -1 if none; *bad_frames (may be NULL) how many.  The
+ * record is cleared by the call.  (Reference: traceImage always fills the
+ * whole image, RayTracer.cpp:279-314 — a wrong frame is an error.) */
+rtx_status rtx_frame_status(void* scene, int64_t* first_bad, int64_t* bad_frames);
+
+/* How many rtx_render calls since the scene was created (or this counter
+ * was last read) were pipelined — ran on the scene's alternating frame
+ * contexts, free to overlap the frame before them (DESIGN.md "Frame
+ * contexts") — out of *renders calls.  Either pointer may be NULL. */
+rtx_status rtx_overlap_count(void* scene, int64_t* overlapped, int64_t* renders);
 
 #ifdef __cplusplus
 }

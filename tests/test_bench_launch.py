@@ -84,20 +84,23 @@ def test_bench_gpus_more_than_visible_fails_fast():
 
 
 @pytest.mark.gpu
-def test_bench_two_ranks_rehearsal_on_one_gpu():
+@pytest.mark.parametrize("n", [2, 4])
+def test_bench_ranks_rehearsal_on_one_gpu(n):
     """The N-rank bench path end to end on the one-GPU box: `bench.py --gpus 2`
     with RTX_BENCH_REHEARSAL=1 starts two ranks on device 0 (gloo instead of
     RCCL, which cannot hold two ranks on one device), each renders its tile
     shard, rank 0 gathers them and prints one line with n_gpus 2 and the
     slowest rank's time; the line says it is a rehearsal."""
     t0 = time.monotonic()
-    r = _bench(["--gpus", "2", "--no-cpu", "--steps", "2", "--warmup", "1"], timeout=240,
+    r = _bench(["--gpus", str(n), "--no-cpu", "--steps", "2", "--warmup", "1"], timeout=240,
                env={"RTX_BENCH_REHEARSAL": "1"})
     assert r.returncode == 0, r.stderr[-3000:]
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
     assert len(lines) == 1
     line = json.loads(lines[0])
-    assert line["n_gpus"] == 2 and line["steps"] == 2
+    assert line["n_gpus"] == n and line["steps"] == 2
+    assert line["frame_check"]["bad_frames"] == 0
+    assert line["gather_check"]["rgb8_mismatch_pixels"] == 0
     assert line["value"] > 0 and line["ms_per_step"] > 0
     assert "REHEARSAL" in line["config"]["parallelism"]
     assert time.monotonic() - t0 < 240

@@ -149,7 +149,11 @@ def test_repeat_deterministic(pkg):
     ("trimesh2_glass.ray", "-w 96 -r 5 -O r -A 2", 0, 1),
     ("trimesh2.ray", "-w 128 -r 5 -O r -A 4", 32, 3),
     ("trimesh2.ray", "-w 64 -r 5 -O d -A 2.5 -B 4 -C 0.05", 0, 1),
-])
+    # the headline frame at full size, as two 16.6M-unit shards (the largest
+    # frames that overlap on the frame contexts by default): eight frames,
+    # four per shard, alternating contexts
+    ("trimesh2.ray", "-w 1920 -r 5 -O r -A 4", 32, 2),
+], ids=["glass", "tiles3", "dof", "headline_full_x2"])
 def test_pipelined_frames_identical(pkg, scene, flags, tile, nshards):
     """Renders into device buffers alternate between the scene's two frame
     contexts and overlap each other (rtx_render: frame contexts).  Eight such
@@ -326,3 +330,69 @@ def test_no_device_fallback_error(pkg):
     host = pkg.HostScene(scene_path("spheres_overlap.ray"))
     with pytest.raises(pkg.RtxError):
         pkg.DeviceScene(host, 97)
+
+
+def _device_render_bytes(pkg, dev, opts, nbytes):
+    """one render into a device buffer (the library's own HIP runtime), then
+    its bytes"""
+    import ctypes as C
+
+    hip = C.CDLL("libamdhip64.so.7")
+    hip.hipMalloc.argtypes = [C.POINTER(C.c_void_p), C.c_size_t]
+    hip.hipFree.argtypes = [C.c_void_p]
+    hip.hipMemcpy.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int]
+    buf = C.c_void_p()
+    assert hip.hipMalloc(C.byref(buf), nbytes) == 0
+    try:
+        dev.render_device(opts, buf.value, 0, 0)
+        assert hip.hipDeviceSynchronize() == 0
+        got = np.zeros(nbytes, np.uint8)
+        assert hip.hipMemcpy(got.ctypes.data, buf, nbytes, 2) == 0
+        return got
+    finally:
+        hip.hipFree(buf)
+
+
+@pytest.mark.parametrize("knob", ["low_stack", "short_pool"])
+def test_wrong_frame_never_ok(pkg, capfd, monkeypatch, knob):
+    """A frame sized from its history (two-entry pending stacks, a bucket-set
+    pool of the last render's size) whose history falls short is wrong.  The
+    test knobs force that: RTX_LOW_STACK=2 with RTX_SPARE=1 gives a glass
+    frame (every hit reflects and refracts) two-entry stacks and almost no
+    fork slots, so pushes overflow; RTX_TEST_SHORT_POOL=1 halves the pool
+    below the sets the frame takes.  A synchronous (host-buffer) render must
+    render such a frame again and return the right image; an asynchronous
+    (device-buffer) render is reported by rtx_frame_status, naming the frame,
+    and the frame's next render is right (rtx_render, collect_check)."""
+    path = scene_path("trimesh2_glass.ray")
+    opts = pkg.RenderOptions.from_cli("-w 64 -r 5 -O r -A 2".split())
+    host = pkg.HostScene(path)
+    want = pkg.DeviceScene(host, 0).render(opts, want_f64=False)["rgb8"].reshape(-1)
+    env = {"low_stack": {"RTX_LOW_STACK": "2", "RTX_SPARE": "1"}, "short_pool": {"RTX_TEST_SHORT_POOL": "1"}}[knob]
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    # host buffers: every call returns the right image
+    dev = pkg.DeviceScene(host, 0)
+    capfd.readouterr()
+    for _ in range(3):
+        got = dev.render(opts, want_f64=False)["rgb8"].reshape(-1)
+        assert np.array_equal(got, want)
+    err = capfd.readouterr().err
+    assert "again with full-size buffers" in err, err[-2000:]
+    # device buffers: the wrong frame is named by rtx_frame_status
+    dev = pkg.DeviceScene(host, 0)
+    seen_bad = []
+    for k in range(4):
+        got = _device_render_bytes(pkg, dev, opts, want.size)
+        fb, nb = dev.frame_status(raise_on_bad=False)
+        if nb:
+            seen_bad.append(fb)
+            assert fb == k, (fb, k)
+        else:
+            assert np.array_equal(got, want), f"render {k} reported right but differs"
+    assert seen_bad, "no frame was reported wrong"
+    with pytest.raises(pkg.RtxError):  # (a wrong frame raises by default)
+        dev2 = pkg.DeviceScene(host, 0)
+        for _ in range(3):
+            _device_render_bytes(pkg, dev2, opts, want.size)
+        dev2.frame_status()

@@ -10,7 +10,11 @@ import os
 
 # frame contexts: 2 x 3 slot-group streams want their own hardware queues; the
 # environment may hold HIP's default of 4 (the GPU box does), so raise it
+import sys  # (before the queue override below)
 if int(os.environ.get("GPU_MAX_HW_QUEUES", "0") or 0) < 16:
+    if os.environ.get("GPU_MAX_HW_QUEUES"):
+        print(f"{os.path.basename(__file__)}: GPU_MAX_HW_QUEUES={os.environ['GPU_MAX_HW_QUEUES']} raised to 16",
+              file=sys.stderr)
     os.environ["GPU_MAX_HW_QUEUES"] = "16"
 import sys
 import time
