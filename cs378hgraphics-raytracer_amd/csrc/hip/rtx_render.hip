@@ -209,8 +209,8 @@ __device__ RTX_RESOLVE_ATTR HitRef resolve_hit(const DevScene& S, const dvec3& P
   HitRef r;
   const RtxObject& o = S.objs[oi];
   const RtxMaterial& mat = S.mats[o.material];
-  const dvec3 pos = rtm::xform_point(o.inv, P);
-  dvec3 dir = rtm::xform_point(o.inv, P + D) - pos;
+  dvec3 pos, dir;
+  obj_local(o, P, D, pos, dir);
   dir = rtm::normalize(dir);
   dvec3 nl = mk3(0.0, 0.0, 1.0);
   dvec2 uv = rtm::mk2(0.0, 0.0);
@@ -2838,6 +2838,8 @@ rtx_status rtx_scene_create(int device, const RtxSceneDesc* d, void** out) {
     UP(tt.tfaces.data(), tt.tfaces.size(), S.tfaces);
     UP(tt.trank.data(), tt.trank.size(), S.trank);
     UP(tt.tmeta.data(), tt.tmeta.size(), S.tmeta);
+    UP(tt.tfacef.data(), tt.tfacef.size(), S.tfacef);
+    S.mext = mesh_extent_f(d);
 #undef UP
   }
   for (int k = 0; k < 6; ++k) {

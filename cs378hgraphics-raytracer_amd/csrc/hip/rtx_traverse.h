@@ -95,8 +95,28 @@ RT_HD bool leaf_ok(const Trav& T, const DevScene& S, int leaf) {
 // to [lo, hi]), continue with the nearest entry hit and push the
 // other hits farthest first, so the walk stays near-first.  False if no
 // entry was hit (the caller pops).
+// A record's 128 bytes as eight 16-byte loads (visit4's operand).
+struct Rec4 {
+  float4 lx, ly, lz, hx, hy, hz;
+  int4 ch;
+  int nrec;
+};
+RT_HD Rec4 load_rec4(const DevNode4& nd) {
+  const float4* q4 = reinterpret_cast<const float4*>(&nd);
+  Rec4 r;
+  r.lx = q4[0];
+  r.ly = q4[1];
+  r.lz = q4[2];
+  r.hx = q4[3];
+  r.hy = q4[4];
+  r.hz = q4[5];
+  r.ch = reinterpret_cast<const int4*>(&nd)[6];
+  r.nrec = reinterpret_cast<const int4*>(&nd)[7].x;
+  return r;
+}
+
 template <bool STATS>
-RT_HD bool visit4(const DevNode4& nd, const RayF& rf, const double hi, const double lo, int* __restrict__ stk,
+RT_HD bool visit4(const Rec4& R, const RayF& rf, const double hi, const double lo, int* __restrict__ stk,
                   const int lane, int& sp, int& ref, Counters& C) {
   const float NOHIT = __builtin_inff();
   // prune bounds widened to floats (hi up, lo down): pruning stays safe
@@ -104,6 +124,8 @@ RT_HD bool visit4(const DevNode4& nd, const RayF& rf, const double hi, const dou
   float a0 = NOHIT, a1 = NOHIT, a2 = NOHIT, a3 = NOHIT;
   int r0 = 0, r1 = 0, r2 = 0, r3 = 0;
 #ifdef RTX_PACKED_RECORDS
+#error "RTX_PACKED_RECORDS: rework for the Rec4 operand (visit4 takes the loaded record)"
+
   const int cnt = nd.count;
   // Opt-in: two entries per packed float pair (box_cons32x2; entries past
   // `count` are empty boxes, which the slab rule does not reject: masked
@@ -125,14 +147,14 @@ RT_HD bool visit4(const DevNode4& nd, const RayF& rf, const double hi, const dou
   pair(0, a0, r0, a1, r1);
   pair(1, a2, r2, a3, r3);
 #else
-  // the whole record in one burst of 16-byte loads before any test: the
-  // entries used to be loaded inside their own `k < count` branches, up to
-  // nine dependent round trips per record for a wave stepping alone.
-  // Every entry is tested (empty ones are masked by the count).
-  const float4* q4 = reinterpret_cast<const float4*>(&nd);
-  const float4 lx = q4[0], ly = q4[1], lz = q4[2], hx = q4[3], hy = q4[4], hz = q4[5];
-  const int4 ch = reinterpret_cast<const int4*>(&nd)[6];
-  const int nrec = reinterpret_cast<const int4*>(&nd)[7].x;
+  // the whole record in one burst of 16-byte loads before any test (the
+  // caller issues them, load_rec4): the entries used to be loaded inside
+  // their own `k < count` branches, up to nine dependent round trips per
+  // record for a wave stepping alone.  Every entry is tested (empty ones are
+  // masked by the count).
+  const float4 lx = R.lx, ly = R.ly, lz = R.lz, hx = R.hx, hy = R.hy, hz = R.hz;
+  const int4 ch = R.ch;
+  const int nrec = R.nrec;
   auto test = [&](int k, float lox, float loy, float loz, float hix, float hiy, float hiz, int child, float& ak,
                   int& rk) {
     if (STATS && k < nrec) C.nodes++;
@@ -253,6 +275,13 @@ RT_HD bool trav_step(Trav& T, const DevScene& S, int* __restrict__ stk, const in
   // kernel carries one inlined copy)
   const bool mesh = T.mode == 2;
   if (T.mode != 1 && ref >= 0) {
+    // the record's loads first, then the prune bounds (FP64) while they are
+    // in flight (the scheduler used to place the loads after the bounds)
+    const DevNode4* recs = !mesh ? S.snode4 : (ref < S.n_mhot ? S.mhot : S.mnode4);
+    const Rec4 rec = load_rec4(recs[ref]);
+#ifdef RTX_EARLY_REC  // (measured: no gain, 33.16 vs 33.11-33.15 ms, profiles/r05e_ab_ident_early.txt)
+    sched_fence();
+#endif
     double hi = bt + S.margin, lo = tlo;
     if (mesh) {
       const double len = T.len;
@@ -260,8 +289,7 @@ RT_HD bool trav_step(Trav& T, const DevScene& S, int* __restrict__ stk, const in
       if (closest && T.mhave) hi = rtm::gmin(hi, T.mbest + S.lmargin);
       lo = closest ? -RTX_INF : tlo * len * (1.0 - 1e-12) - S.lmargin;
     }
-    const DevNode4* recs = !mesh ? S.snode4 : (ref < S.n_mhot ? S.mhot : S.mnode4);
-    if (visit4<STATS>(recs[ref], T.rf, hi, lo, stk, lane, sp, ref, C)) return false;
+    if (visit4<STATS>(rec, T.rf, hi, lo, stk, lane, sp, ref, C)) return false;
     if (!mesh) {
       if (sp == 0) return true;
       --sp;
@@ -283,8 +311,8 @@ RT_HD bool trav_step(Trav& T, const DevScene& S, int* __restrict__ stk, const in
     double a, b;
     // Geometry::intersect's world-box test (scene.cpp:15) + prune
     if (box_test(o.wmin, o.wmax, T.P, T.D, T.ri, a, b) && !(a > bt + S.margin) && !(b < tlo)) {
-      const dvec3 pos = rtm::xform_point(o.inv, T.P);
-      dvec3 dir = rtm::xform_point(o.inv, T.P + T.D) - pos;
+      dvec3 pos, dir;
+      obj_local(o, T.P, T.D, pos, dir);
       const double ln = rtm::length(dir);
       dir = rtm::normalize(dir);
       if (o.type == RTX_OBJ_TRIMESH) {
@@ -491,6 +519,32 @@ RT_HD bool trav_step(Trav& T, const DevScene& S, int* __restrict__ stk, const in
     // strictly farther than the mesh's best; next: farther than the
     // current best key) — tri_hit stops before the edge tests
     const double tcap = closest && T.mhave ? rtm::gmin(whi, T.mbest) : whi;
+#ifndef RTX_NO_TRI_PRE
+    // The leaf's faces as floats in one burst (3 x 48 B; a leaf of fewer
+    // faces loads its last one again), the conservative float prefilter on
+    // each (tri_pre), and the exact FP64 tri_hit only on the faces it
+    // cannot reject — the double face (96 B) then, not for every face.
+    const FaceF* ff = S.tfacef + T.mfoff + f0;
+    const int nf = f1 - f0;
+    const FaceF q0 = ff[0], q1 = ff[nf > 1 ? 1 : 0], q2 = ff[nf > 2 ? 2 : 0];
+    const RayTF rt = ray_tf(T.lp, T.ld, S.mext);
+    const float tcf = f_up_wide(tcap);
+    unsigned int surv = (tri_pre(q0.a, q0.b, q0.c, rt, tcf) ? 1u : 0u) |
+                        (nf > 1 && tri_pre(q1.a, q1.b, q1.c, rt, tcf) ? 2u : 0u) |
+                        (nf > 2 && tri_pre(q2.a, q2.b, q2.c, rt, tcf) ? 4u : 0u);
+    const int rk0 = __builtin_bit_cast(int, q0.a.w), rk1 = __builtin_bit_cast(int, q1.a.w),
+              rk2 = __builtin_bit_cast(int, q2.a.w);
+    const int lf0 = __builtin_bit_cast(int, q0.b.w), lf1 = __builtin_bit_cast(int, q1.b.w),
+              lf2 = __builtin_bit_cast(int, q2.b.w);
+    if (STATS) C.tris += nf;
+    while (surv) {
+      const int k = __builtin_ctz(surv);
+      surv &= surv - 1;
+      const int f = f0 + k;
+      double tf;
+      const bool hit = tri_hit(S.tfaces[T.mfoff + f], T.lp, T.ld, tcap, tf);
+      const TMeta meta = {k == 0 ? rk0 : (k == 1 ? rk1 : rk2), k == 0 ? lf0 : (k == 1 ? lf1 : lf2)};
+#else
     for (int f = f0; f < f1; ++f) {
       if (STATS) C.tris++;
       double tf;
@@ -500,6 +554,7 @@ RT_HD bool trav_step(Trav& T, const DevScene& S, int* __restrict__ stk, const in
       const bool hit = tri_hit(S.tfaces[T.mfoff + f], T.lp, T.ld, tcap, tf);
       pin(meta.rank);
       pin(meta.leaf);
+#endif
       if (hit) {
         const int rk = meta.rank;
         if (closest) {
@@ -830,6 +885,7 @@ struct TravTrees {
   std::vector<RtxFace> tfaces;
   std::vector<int32_t> trank;
   std::vector<TMeta> tmeta;
+  std::vector<FaceF> tfacef;    // tfaces as floats + rank / leaf (tri_pre)
   std::vector<RtxObject> objs;  // the objects with their mesh fields in pad (augment_objects)
   int sneed = 0, mneed = 0;
   int n_mhot = 0;  // mesh records [0, n_mhot) are the hot ones (renumbered first)
@@ -887,6 +943,12 @@ inline void augment_objects(const RtxSceneDesc* d, std::vector<RtxObject>& objs)
     o.pad[RTX_OBJ_MFLAGS] = (me.node_count > 0 ? RTX_MESH_TREE : 0) | (me.has_normals ? RTX_MESH_NORMALS : 0) |
                             (me.has_vmats ? RTX_MESH_VMATS : 0);
   }
+  for (RtxObject& o : objs) {  // identity M^-1 (obj_local)
+    static const double id[12] = {1, 0, 0, 0, 1, 0, 0, 0, 1, 0, 0, 0};
+    bool ident = true;
+    for (int k = 0; k < 12; ++k) ident = ident && o.inv[k] == id[k] && !std::signbit(o.inv[k]);
+    if (ident) o.pad[RTX_OBJ_MFLAGS] |= RTX_OBJ_IDENT;
+  }
 }
 
 inline bool build_trav_trees(const RtxSceneDesc* d, TravTrees& T) {
@@ -923,6 +985,7 @@ inline bool build_trav_trees(const RtxSceneDesc* d, TravTrees& T) {
   T.tfaces.assign(size_t(d->n_faces), RtxFace());
   T.trank.assign(size_t(d->n_faces), 0);
   T.tmeta.assign(size_t(d->n_faces), TMeta{0, 0});
+  T.tfacef.assign(size_t(d->n_faces), FaceF{});
   for (int m = 0; m < d->n_meshes; ++m) {
     const RtxMesh& me = d->meshes[m];
     std::memset(&T.mroots[size_t(m)], 0, sizeof(DevRoot));
@@ -940,6 +1003,14 @@ inline bool build_trav_trees(const RtxSceneDesc* d, TravTrees& T) {
       T.tfaces[size_t(me.face_off + j)] = d->faces[me.face_off + order[size_t(j)]];
       T.trank[size_t(me.face_off + j)] = order[size_t(j)];
       T.tmeta[size_t(me.face_off + j)] = TMeta{order[size_t(j)], me.node_off + d->face_ids[me.face_off + order[size_t(j)]].leaf};
+    }
+    for (int j = 0; j < me.face_count; ++j) {  // the float copy for tri_pre (rounded to nearest)
+      const RtxFace& F = T.tfaces[size_t(me.face_off + j)];
+      const TMeta& tm = T.tmeta[size_t(me.face_off + j)];
+      FaceF& q = T.tfacef[size_t(me.face_off + j)];
+      q.a = make_float4(float(F.v0[0]), float(F.v0[1]), float(F.v0[2]), __builtin_bit_cast(float, tm.rank));
+      q.b = make_float4(float(F.v1[0]), float(F.v1[1]), float(F.v1[2]), __builtin_bit_cast(float, tm.leaf));
+      q.c = make_float4(float(F.v2[0]), float(F.v2[1]), float(F.v2[2]), 0.0f);
     }
     int need = 0;
     if (!build_node4(nodes.data(), static_cast<int>(nodes.size()), T.mn4, T.mroots[size_t(m)], need)) return false;
@@ -977,6 +1048,16 @@ inline double mesh_extent(const RtxSceneDesc* d) {
       e = fmax(e, fabs(d->mesh_nodes[i].bmax[k]));
     }
   return e;
+}
+
+// tri_pre's bound on every mesh-local vertex coordinate, as a float rounded
+// up: the largest |coordinate| of any face vertex (every vertex, whether or
+// not a mesh tree holds it)
+inline float mesh_extent_f(const RtxSceneDesc* d) {
+  double e = 1.0;
+  for (int f = 0; f < d->n_faces; ++f)
+    for (int k = 0; k < 3; ++k) e = fmax(e, fmax(fabs(d->faces[f].v0[k]), fmax(fabs(d->faces[f].v1[k]), fabs(d->faces[f].v2[k]))));
+  return round_up_f(e);
 }
 
 }  // namespace rtxd

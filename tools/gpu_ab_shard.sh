@@ -15,6 +15,9 @@ for cfg in "$@"; do
     esac
   done
   env $envs timeout -k 10 200 python tools/shard_probe.py 1 8 | sed "s|^|[$cfg] |" || exit 1
+  if [ -n "$AB_R1" ]; then
+    env $envs timeout -k 10 200 python tools/shard_probe.py --scene trimesh2_glass.ray 1 | sed "s|^|[$cfg] |" || exit 1
+  fi
   if [ -n "$AB_C4" ]; then
     env $envs timeout -k 10 200 python tools/shard_probe.py --flags "-w 1920 -r 5 -O d -A 2.5 -B 16 -C 0.05" 1 8 | sed "s|^|[$cfg] |" || exit 1
   fi
