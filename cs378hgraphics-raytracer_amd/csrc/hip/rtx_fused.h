@@ -37,7 +37,26 @@ enum {
   QF_LAST,                           //   t of the last hit
   QF_D
 };
-#define QF_I 2  // ints: 0 -1 before the walk's first hit (else the last hit's object), 1 light
+#define QF_I 2  // ints: 0 -1 before the walk's first hit (else the last hit's object), 1 the walk's code
+
+// Area lights (AreaLight::shadowAttenuation, light.cpp:76-87): an area or spot
+// light's shadow attenuation is (1 + the srsAttenuation walks toward its
+// valid picks, in pick order) / (softShadowRes - 1), so each pick is a walk
+// record of its own, and the light's term is formed when the hit's colour is
+// flushed (flush_terms), from the picks' attenuations and the factors the
+// shading left (dattn, d + s, and mode 1: a spot light whose cone misses the
+// hit, term dattn * 0 * color * (d + s)).  A record's code is its light, with
+// pick + 1 in bits 8 and up (0: a point or directional light's walk).
+__device__ __forceinline__ int walk_code(int li, int pick) { return li | ((pick + 1) << 8); }
+__device__ __forceinline__ int walk_light(int code) { return code & 255; }
+__device__ __forceinline__ int walk_pick(int code) { return (code >> 8) - 1; }
+// the walk's direction: toward the light (getDirection, light.cpp:59, :73),
+// or toward the pick (glm::normalize(lpos - pb), light.cpp:84)
+__device__ __forceinline__ dvec3 walk_dir(const DevScene& S, int code, const dvec3& pb) {
+  const int li = walk_light(code), pick = walk_pick(code);
+  if (pick < 0) return light_dir(S.lights[li], pb);
+  return rtm::normalize(ld3(S.picks + (size_t(li) * S.ss_res + pick) * 3) - pb);
+}
 
 struct WalkState {
   dvec3 wpos, sattn;
@@ -60,6 +79,22 @@ __device__ __forceinline__ bool walk_hit(const DevScene& S, const RtxLight& L, c
   if (L.type == RTX_LIGHT_POINT && rtm::dot(ld3(L.pos) - rtm::ray_at(w.wpos, sdir, t), sdir) <= 0) {
     res = w.sattn;
     return true;
+  }
+  if (L.type >= RTX_LIGHT_AREA_RECT) {
+    // AreaLight::sattnLimitCheck (light.cpp:88-95): past the light's impact
+    // point — the walk ray's crossing of the light's plane (impact,
+    // light.cpp:101-105), for a disc or spot light (0, 0, 0) when it falls
+    // outside the radius (light.cpp:133-141)
+    const dvec3 ori = ld3(L.orient), lpos = ld3(L.pos);
+    double ti = rtm::dot(ori, sdir);
+    ti = rtm::dot(lpos - w.wpos, ori) / ti;
+    dvec3 imp = rtm::ray_at(w.wpos, sdir, ti);
+    if (L.type != RTX_LIGHT_AREA_RECT && !(rtm::dot(imp - lpos, imp - lpos) < (L.radius * L.radius)))
+      imp = mk3(0.0, 0.0, 0.0);
+    if (rtm::dot(imp - rtm::ray_at(w.wpos, sdir, t), sdir) <= 0) {
+      res = w.sattn;
+      return true;
+    }
   }
   // An object opaque to walks (not transmissive, kt a constant 0, no
   // per-vertex materials): entered from outside the walk returns 0; left
@@ -97,19 +132,22 @@ __device__ __noinline__ bool walk_hit_ool(const DevScene* Sg, int li, const dvec
 struct WalkEmit {
   QList q;
   unsigned int* cnt;
-  int fixed_base;  // >= 0 (tail kernel): record (slot - fixed_base) * n_lights + light, no append
-  int n_lights;
+  int fixed_base;  // >= 0 (tail kernel): record (slot - fixed_base) * nrec + rec, no append
+  int nrec;
 };
 
 // Append a walk record for the lanes with `on` (wave-aggregated: one atomic
 // per call per wave, offsets by mbcnt).  Called from divergent code: the
 // ballot covers the lanes executing it, the lowest of them claims.
-__device__ __forceinline__ void emit_walk(const WalkEmit& E, bool on, int slot, int li, const dvec3& pb,
-                                          double dattn, const dvec3& dscomp) {
+// (rec: the record's index among the slot's nrec, for the tail's fixed
+// positions; factors: a point or directional light's walk, whose record
+// carries dattn and d + s — an area pick's walk needs neither)
+__device__ __forceinline__ void emit_walk(const WalkEmit& E, bool on, int slot, int rec, int code, const dvec3& pb,
+                                          double dattn, const dvec3& dscomp, bool factors = true) {
   size_t k;
   if (E.fixed_base >= 0) {
     if (!on) return;
-    k = static_cast<size_t>(slot - E.fixed_base) * E.n_lights + li;
+    k = static_cast<size_t>(slot - E.fixed_base) * E.nrec + rec;
   } else {
     const unsigned long long m = __ballot(on);
     if (!on) return;
@@ -125,13 +163,27 @@ __device__ __forceinline__ void emit_walk(const WalkEmit& E, bool on, int slot, 
   d[QF_PX * cap + k] = pb.x;
   d[QF_PY * cap + k] = pb.y;
   d[QF_PZ * cap + k] = pb.z;
-  d[QF_DATTN * cap + k] = dattn;
-  d[QF_SCX * cap + k] = dscomp.x;
-  d[QF_SCY * cap + k] = dscomp.y;
-  d[QF_SCZ * cap + k] = dscomp.z;
+  if (factors) {
+    d[QF_DATTN * cap + k] = dattn;
+    d[QF_SCX * cap + k] = dscomp.x;
+    d[QF_SCY * cap + k] = dscomp.y;
+    d[QF_SCZ * cap + k] = dscomp.z;
+  }
   E.q.iv[0 * cap + k] = -1;
-  E.q.iv[1 * cap + k] = li;
+  E.q.iv[1 * cap + k] = code;
   E.q.slot[k] = slot;
+}
+// a walk that ended: a point or directional light's term dattn * sattn *
+// color * (d + s) (material.cpp:62), or an area pick's attenuation
+// (rtx_fused.h "Area lights"), into its wterm unit
+__device__ __forceinline__ void walk_store(double* wterm, const int* lunit, size_t n, size_t slot, int code,
+                                           const RtxLight& L, double dattn, const dvec3& dsc, const dvec3& res) {
+  const int li = walk_light(code), pick = walk_pick(code);
+  double* o = wterm + (static_cast<size_t>(lunit[li] + (pick < 0 ? 0 : 2 + pick)) * n + slot) * 3;
+  const dvec3 v = pick < 0 ? dattn * res * ld3(L.color) * dsc : res;
+  o[0] = v.x;
+  o[1] = v.y;
+  o[2] = v.z;
 }
 
 // colour c into bucket pos of the lane's sample (the root's bucket is acc)
@@ -141,15 +193,33 @@ __device__ __forceinline__ void contrib_at(LaneRef& LR, const FrameParams& F, in
 }
 
 // The deferred colour of the lane's last hit: W * (i_out + its lights'
-// terms in light order) (material.cpp:45-66, RayTracer.cpp:125).
-__device__ __forceinline__ void flush_terms(LaneRef& LR, const FrameParams& F) {
+// terms in light order) (material.cpp:45-66, RayTracer.cpp:125).  An area or
+// spot light's term is formed here from its picks' attenuations in pick
+// order (AreaLight::shadowAttenuation, light.cpp:76-87, as ST_SRS sums them).
+__device__ __forceinline__ void flush_terms(LaneRef& LR, const FrameParams& F, const DevScene& S) {
   unsigned int m = static_cast<unsigned int>(LR.wmask());
   if (!m) return;
   dvec3 col = LR.i_out();
+  const size_t n = LR.m.n;
   while (m) {
     const int l = __builtin_ctz(m);
     m &= m - 1;
-    col += ld3(F.wterm + (size_t(l) * LR.m.n + LR.g) * 3);
+    const double* u = F.wterm + (size_t(F.lunit[l]) * n + LR.g) * 3;
+    if (!((F.area_mask >> l) & 1)) {
+      col += ld3(u);
+      continue;
+    }
+    const double dattn = u[0];
+    const dvec3 dsc = mk3(u[1], u[2], u[n * 3]);
+    const RtxLight& L = S.lights[l];
+    if (u[n * 3 + 1] != 0.0) {  // a spot light whose cone misses the hit (light.cpp:147-149)
+      col += dattn * mk3(0.0, 0.0, 0.0) * ld3(L.color) * dsc;
+      continue;
+    }
+    dvec3 sa = mk3(1.0, 1.0, 1.0);
+    for (int i = 0; i < S.ss_res; ++i) sa += ld3(u + size_t(2 + i) * n * 3);  // (invalid picks hold +0)
+    sa *= (1.0 / (S.ss_res - 1));
+    col += dattn * sa * ld3(L.color) * dsc;
   }
   contrib_at(LR, F, LR.rpos(), LR.W() * col);
   LR.wmask() = 0;
@@ -286,13 +356,49 @@ __device__ __forceinline__ void shade_hit(LaneRef& LR, const DevScene& S, const 
       const dvec3 s_comp = ks * rtm::splat3(rtm::rpow(rtm::gmax(0.0, rtm::dot(l_r, rd)), sh));
       const dvec3 dscomp = d_comp + s_comp;
       const double dattn = light_dist_atten(L, X);
+      if (L.type >= RTX_LIGHT_AREA_RECT) {
+        // AreaLight::shadowAttenuation (light.cpp:76-87): a walk per valid
+        // pick; the term is formed in flush_terms from the factors here
+        double* u = F.wterm + (size_t(F.lunit[li]) * nlanes + LR.g) * 3;
+        u[0] = dattn;
+        u[1] = dscomp.x;
+        u[2] = dscomp.y;
+        u[nlanes * 3] = dscomp.z;
+        const dvec3 ori = ld3(L.orient), lpos = ld3(L.pos);
+        // SpotLight::validImpact(r, p) at the hit (light.cpp:144-146)
+        const bool cone = L.type != RTX_LIGHT_SPOT ||
+                          ((rtm::dot(light_dir(L, X), ori) <= 0) &&
+                           (rtm::dot(rtm::normalize(X - (lpos - L.offset * ori)), ori) > S.cos45));
+        u[nlanes * 3 + 1] = cone ? 0.0 : 1.0;
+        wm |= 1u << li;
+        if (!cone) continue;
+        for (int i = 0; i < S.ss_res; ++i) {
+          const dvec3 lp = ld3(S.picks + (size_t(li) * S.ss_res + i) * 3);
+          // validImpact(r, pb, lp) (light.cpp:147-149; always for rect / disc)
+          const bool valid = L.type != RTX_LIGHT_SPOT ||
+                             ((rtm::dot(light_dir(L, pb), ori) <= 0) && (rtm::dot(rtm::normalize(pb - lp), ori) > S.cos45));
+          if (STATS && valid) {
+            C.shadow++;
+            C.shadow_traced++;
+          }
+          if (valid) ++nr;
+          emit_walk(*we, valid, static_cast<int>(LR.g), F.lrec[li] + i, walk_code(li, i), pb, 0.0, dscomp, false);
+          if (!valid) {  // no walk: the pick adds +0 (ST_SRS skips it)
+            double* o = u + size_t(2 + i) * nlanes * 3;
+            o[0] = o[1] = o[2] = 0.0;
+            if (we->fixed_base >= 0)  // (the tail's fixed record: marked, not walked)
+              we->q.iv[1 * we->q.cap + static_cast<size_t>(LR.g - we->fixed_base) * we->nrec + F.lrec[li] + i] = -1;
+          }
+        }
+        continue;
+      }
       if (STATS) C.shadow++;
       ++nr;
       // a zero colour factor with finite attenuations adds +0 (DESIGN.md:
       // dark lights are counted, not traced)
       const bool on = !(S.skip_dark && dscomp.x == 0.0 && dscomp.y == 0.0 && dscomp.z == 0.0);
       if (STATS && on) C.shadow_traced++;
-      emit_walk(*we, on, static_cast<int>(LR.g), li, pb, dattn, dscomp);
+      emit_walk(*we, on, static_cast<int>(LR.g), F.lrec[li], walk_code(li, -1), pb, dattn, dscomp);
       if (on) wm |= 1u << li;
     }
     LR.nrays() += nr;
@@ -592,7 +698,7 @@ __global__ void __launch_bounds__(WG, RTX_FUSED_ADV_WAVES)
   // a fork slot (past the group's sample slots) running a sub-tree
   const bool was_fork = FORK && valid && slot - slot_off >= F.wf_gsamp && L.st() != ST_IDLE;
   if (valid && (L.st() != ST_IDLE || slot_unit(F, slot, L.kdone()) >= 0)) {
-    flush_terms(L, F);
+    flush_terms(L, F, *Sg);
     L.qmode() = Q_NONE;
     for (;;) {
       claim_sample(L, F, hits, slot);
@@ -671,25 +777,53 @@ __global__ void __launch_bounds__(WG) tail_fused_kernel(DevScene S, const DevSce
   const int slot = valid ? live_in[tid] : 0;
   LaneRef L(lm, static_cast<size_t>(slot));
   const DevScene& SS = *Sg;
-  const WalkEmit we = {qn, nullptr, slot_off, SS.n_lights};
+  const WalkEmit we = {qn, nullptr, slot_off, F.nrec};
   const size_t cap = qn.cap;
-  unsigned int todo = 0;  // lights whose walk is still to run (records at the slot's positions)
+  unsigned int todo = 0;  // lights whose walks are still to run (records at the slot's positions)
   int wl = -1;            // the light being walked; w: its state
+  int wp = 0;             // an area light's next pick
+  int wcode = 0;          // the walk's code (walk_code)
   WalkState w = {mk3(0.0, 0.0, 0.0), mk3(0.0, 0.0, 0.0), 0.0};
   dvec3 pb = mk3(0.0, 0.0, 0.0), sdir = pb;
   double tp = -RTX_INF;
   int rp = -1, sq = -1;
-  if (valid) flush_terms(L, F);
+  if (valid) flush_terms(L, F, SS);
   while (valid) {
     int qm;
     dvec3 qP, qD;
     double qlim = RTX_INF;
     if (todo) {
-      if (wl < 0) {  // start the next walk (light order)
-        wl = __builtin_ctz(todo);
-        const size_t k = static_cast<size_t>(slot - slot_off) * SS.n_lights + wl;
+      if (wl < 0) {
+        // the next walk: light order, an area light's picks in pick order
+        // (records marked -1 — spot picks outside the cone — are skipped, and
+        // a spot light whose cone misses the hit has none)
+        bool found = false;
+        while (todo && !found) {
+          const int l = __builtin_ctz(todo);
+          if (!((F.area_mask >> l) & 1)) {
+            wl = l;
+            wcode = walk_code(l, -1);
+            found = true;
+            break;
+          }
+          const double* u = F.wterm + (size_t(F.lunit[l]) * lm.n + slot) * 3;
+          if (u[lm.n * 3 + 1] != 0.0 || wp >= SS.ss_res) {
+            todo &= todo - 1;
+            wp = 0;
+            continue;
+          }
+          if (qn.iv[1 * cap + static_cast<size_t>(slot - slot_off) * F.nrec + F.lrec[l] + wp] < 0) {
+            ++wp;
+            continue;
+          }
+          wl = l;
+          wcode = walk_code(l, wp);
+          found = true;
+        }
+        if (!found) continue;  // every walk done: the lane's next closest query
+        const size_t k = static_cast<size_t>(slot - slot_off) * F.nrec + F.lrec[wl] + (walk_pick(wcode) < 0 ? 0 : wp);
         pb = mk3(qn.d[QF_PX * cap + k], qn.d[QF_PY * cap + k], qn.d[QF_PZ * cap + k]);
-        sdir = light_dir(SS.lights[wl], pb);
+        sdir = walk_dir(SS, wcode, pb);
         w.wpos = pb;
         w.sattn = mk3(1.0, 1.0, 1.0);
         w.last_t = 0.0;
@@ -703,7 +837,7 @@ __global__ void __launch_bounds__(WG) tail_fused_kernel(DevScene S, const DevSce
       qP = pb;
       qD = sdir;
     } else {
-      flush_terms(L, F);
+      flush_terms(L, F, SS);
       L.qmode() = Q_NONE;
       claim_sample(L, F, hits, slot);
       if (L.st() == ST_IDLE) break;
@@ -723,14 +857,15 @@ __global__ void __launch_bounds__(WG) tail_fused_kernel(DevScene S, const DevSce
     if (qm == Q_NEXT) {
       dvec3 res;
       if (walk_hit(SS, SS.lights[wl], pb, sdir, have, bt, bobj, bsub, w, res)) {
-        const size_t k = static_cast<size_t>(slot - slot_off) * SS.n_lights + wl;
-        const dvec3 dsc = mk3(qn.d[QF_SCX * cap + k], qn.d[QF_SCY * cap + k], qn.d[QF_SCZ * cap + k]);
-        const dvec3 term = qn.d[QF_DATTN * cap + k] * res * ld3(SS.lights[wl].color) * dsc;
-        double* o = F.wterm + (static_cast<size_t>(wl) * lm.n + slot) * 3;
-        o[0] = term.x;
-        o[1] = term.y;
-        o[2] = term.z;
-        todo &= todo - 1;
+        if (walk_pick(wcode) < 0) {
+          const size_t k = static_cast<size_t>(slot - slot_off) * F.nrec + F.lrec[wl];
+          const dvec3 dsc = mk3(qn.d[QF_SCX * cap + k], qn.d[QF_SCY * cap + k], qn.d[QF_SCZ * cap + k]);
+          walk_store(F.wterm, F.lunit, lm.n, slot, wcode, SS.lights[wl], qn.d[QF_DATTN * cap + k], dsc, res);
+          todo &= todo - 1;
+        } else {
+          walk_store(F.wterm, F.lunit, lm.n, slot, wcode, SS.lights[wl], 0.0, res, res);
+          ++wp;
+        }
         wl = -1;
       } else {
         tp = bt;

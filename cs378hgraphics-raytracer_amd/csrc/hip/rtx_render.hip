@@ -120,9 +120,16 @@ struct FrameParams {
   unsigned int* bover;
   int bcap;
   // fused shadow walks (rtx_fused.h): the finished terms of the walks,
-  // wterm[(light * nslot + slot) * 3 + c]
+  // wterm[(unit * nslot + slot) * 3 + c].  Light l's units start at
+  // lunit[l]: a point or directional light has one (its term); an area or
+  // spot light (area_mask bit l) has 2 + ss_res — its factors (dattn, d + s;
+  // mode) and one attenuation per pick (rtx_fused.h "Area lights").  A slot's
+  // walk records of light l start at record lrec[l] of its nrec (the tail
+  // kernel's fixed positions).
   int fuse;
   double* wterm;
+  int lunit[8], lrec[8];
+  int nrec, area_mask;
   // adaptive AA on the wavefront path: a work unit is (region, Hammersley
   // index k) — level 0's regions are the pixels (item_pixel), a deeper
   // level's are aregs[0 .. n_samples / spp) (adapt_stats_kernel)
@@ -2037,10 +2044,10 @@ __global__ void __launch_bounds__(WG, !FUSED ? RTX_TRACE_WAVES : (MODE == Q_CLOS
       // back as dependent scratch loads (the LaneRef::refresh idea)
       size_t k = kq;
       asm volatile("" : "+v"(k));
-      const int li = Q.iv[1 * cap + k];
-      const RtxLight& L = Sg->lights[li];
+      const int code = Q.iv[1 * cap + k];
+      const RtxLight& L = Sg->lights[walk_light(code)];
       const dvec3 pb = mk3(Q.d[QF_PX * cap + k], Q.d[QF_PY * cap + k], Q.d[QF_PZ * cap + k]);
-      const dvec3 sdir = light_dir(L, pb);  // as the emitter computed it
+      const dvec3 sdir = walk_dir(*Sg, code, pb);  // as the emitter computed it
       WalkState w;
       if (Q.iv[0 * cap + k] < 0) {  // the walk's first hit (light.cpp:28-29)
         w.wpos = pb;
@@ -2060,12 +2067,12 @@ __global__ void __launch_bounds__(WG, !FUSED ? RTX_TRACE_WAVES : (MODE == Q_CLOS
       if (walk_hit(*Sg, L, pb, sdir, w_have, bt, bo, bs, w, res)) {
 #endif
         const size_t slot = static_cast<size_t>(Q.slot[k]);
-        const dvec3 dsc = mk3(Q.d[QF_SCX * cap + k], Q.d[QF_SCY * cap + k], Q.d[QF_SCZ * cap + k]);
-        const dvec3 term = Q.d[QF_DATTN * cap + k] * res * ld3(L.color) * dsc;
-        double* o = wterm + (static_cast<size_t>(li) * lm.n + slot) * 3;
-        o[0] = term.x;
-        o[1] = term.y;
-        o[2] = term.z;
+        if (walk_pick(code) < 0) {
+          const dvec3 dsc = mk3(Q.d[QF_SCX * cap + k], Q.d[QF_SCY * cap + k], Q.d[QF_SCZ * cap + k]);
+          walk_store(wterm, SA.Fp->lunit, lm.n, slot, code, L, Q.d[QF_DATTN * cap + k], dsc, res);
+        } else {
+          walk_store(wterm, SA.Fp->lunit, lm.n, slot, code, L, 0.0, res, res);  // an area pick's attenuation
+        }
         pend = false;
       } else {
         Q.d[QF_WPX * cap + k] = w.wpos.x;
@@ -2158,11 +2165,12 @@ __global__ void __launch_bounds__(WG, !FUSED ? RTX_TRACE_WAVES : (MODE == Q_CLOS
           const dvec3 D = mk3(Q.d[3 * cap + kq], Q.d[4 * cap + kq], Q.d[5 * cap + kq]);
           active = trav_init<STATS, MODE>(T, S, P, D, -RTX_INF, -1, -1, RTX_INF, -RTX_INF, C);
         } else {  // a walk's first query (continuations restart in walk_phase)
-          const RtxLight& L = Sg->lights[Q.iv[1 * cap + kq]];
+          const int code = Q.iv[1 * cap + kq];
+          const RtxLight& L = Sg->lights[walk_light(code)];
           const dvec3 pb = mk3(Q.d[QF_PX * cap + kq], Q.d[QF_PY * cap + kq], Q.d[QF_PZ * cap + kq]);
           double qlim, qblk;
           shadow_bounds(*Sg, L, pb, true, qlim, qblk);
-          active = trav_init<STATS, MODE>(T, S, pb, light_dir(L, pb), -RTX_INF, -1, -1, qlim, qblk, C);
+          active = trav_init<STATS, MODE>(T, S, pb, walk_dir(*Sg, code, pb), -RTX_INF, -1, -1, qlim, qblk, C);
         }
         if (!active) {
           if (FUSED) pend = !noq;  // (a slot without a sample: nothing to shade)
@@ -3411,10 +3419,33 @@ static rtx_status render_once(SceneState* st, const RtxRenderParams* params, uin
     // light, no overlapping media, no adaptive termination (RTX_FUSE=0: the
     // sequential machine)
     const char* fuse_env = getenv("RTX_FUSE");
+    // (area and spot lights too: a walk per pick, rtx_fused.h "Area lights";
+    // their term units and records per slot counted here)
     bool fuse = !(fuse_env && atoi(fuse_env) == 0) && !media && !(params->aterm_thresh > 0.0) &&
                 st->lights.size() <= 8;
-    for (const auto& L : st->lights) fuse &= L.type == RTX_LIGHT_POINT || L.type == RTX_LIGHT_DIRECTIONAL;
+    int w_units = 0, w_recs = 0, w_amask = 0;
+    {
+      const int res = std::max(0, params->ss_res);
+      for (size_t l = 0; l < st->lights.size() && l < 8; ++l) {
+        F.lunit[l] = w_units;
+        F.lrec[l] = w_recs;
+        if (st->lights[l].type >= RTX_LIGHT_AREA_RECT) {
+          w_units += 2 + res;
+          w_recs += res;
+          w_amask |= 1 << l;
+        } else {
+          w_units += 1;
+          w_recs += 1;
+        }
+      }
+      // (RTX_FUSE_AREA=0: area / spot light frames on the sequential machine)
+      const char* fa_env = getenv("RTX_FUSE_AREA");
+      if (w_amask && ((fa_env && atoi(fa_env) == 0) || w_recs > 64)) fuse = false;
+    }
+    F.nrec = fuse ? w_recs : 0;
+    F.area_mask = fuse ? w_amask : 0;
     const size_t nl = fuse ? st->lights.size() : 0;
+    const size_t n_units = fuse ? size_t(w_units) : 0;
     // pending-stack entries: a ray at entry i has depth <= P.depth - i (the
     // camera ray is entry 0, a forked sub-tree's root entry 0 with less; a
     // hit overwrites its own entry with one child and pushes the other), and
@@ -3428,9 +3459,9 @@ static rtx_status render_once(SceneState* st, const RtxRenderParams* params, uin
     const size_t qc_d = fuse ? 6 : QL_D, qc_i = fuse ? 0 : 2;
     const size_t rec_c = sizeof(int) + qc_d * sizeof(double) + qc_i * sizeof(int);
     const size_t rec_n = fuse ? sizeof(int) + QF_D * sizeof(double) + QF_I * sizeof(int) : rec_c;
-    const size_t nrec_n = fuse ? std::max<size_t>(1, nl) : 1;
+    const size_t nrec_n = fuse ? std::max<size_t>(1, size_t(w_recs)) : 1;
     const size_t per_slot = lane_mem_bytes(1, fuse) - 512 + size_t(pcap) * 13 * sizeof(double) + rec_c +
-                            nrec_n * rec_n + 2 * sizeof(int) + nl * 3 * sizeof(double);
+                            nrec_n * rec_n + 2 * sizeof(int) + n_units * 3 * sizeof(double);
     // the bucket-set pool: as many sets as this frame took on its last
     // render (deterministic: one per unit whose root has a node child), the
     // full count (a set per unit) the first time.  Whether the frame has
@@ -3676,7 +3707,7 @@ static rtx_status render_once(SceneState* st, const RtxRenderParams* params, uin
     F.fuse = fuse ? 1 : 0;
     F.wterm = nullptr;
     if (fuse && nl > 0) {
-      if ((rc = fit(reinterpret_cast<void**>(&X->d_wterm), &X->wterm_bytes, nl * ns * 3 * sizeof(double))) !=
+      if ((rc = fit(reinterpret_cast<void**>(&X->d_wterm), &X->wterm_bytes, n_units * ns * 3 * sizeof(double))) !=
           RTX_OK)
         return rc;
       F.wterm = X->d_wterm;

@@ -10,6 +10,8 @@ Configs (BASELINE.json "configs"):
   C5 dragon (1M triangles) 3840x2160 -r 5 -O a -A 8
   R1 trimesh2_glass 1920x1080 -r 5 -O r -A 4 (recursion-heavy: the headline
      geometry with reflective / transmissive materials; not a BASELINE config)
+  A1 lava_box (rect area light) 1920 wide -r 5 -O s -A 4 (soft shadows, 4 picks)
+  A2 box_cyl_opaque_shadow_spotlight (spot light) 1920 wide -r 5
 The headline (trimesh2 1920x1080 -r 5 -O r -A 4) is bench.py's.
 usage: python tools/bench_configs.py [C1 C2 ...]  (on the GPU box)
 """
@@ -38,6 +40,10 @@ CONFIGS = {
     "C4": ("trimesh2.ray", "-w 1920 -r 5 -O d -A 2.5 -B 16 -C 0.05"),
     "C5": ("dragon.ray", "-w 3840 -r 5 -O a -A 8"),
     "R1": ("trimesh2_glass.ray", "-w 1920 -r 5 -O r -A 4"),
+    # area / spot lights on the fused walks: the bundled
+    # fixtures (ray/newScene) at 1920 wide, their own aspect ratios
+    "A1": ("../tests/golden/newScene/lava_box.ray", "-w 1920 -r 5 -O s -A 4"),
+    "A2": ("../tests/golden/newScene/box_cyl_opaque_shadow_spotlight.ray", "-w 1920 -r 5"),
 }
 
 
@@ -68,12 +74,13 @@ def main():
             dev.render(opts, want_f64=False)
             walls.append(time.time() - t0)
         wall = sorted(walls)[1]  # median of 3 (host-synchronous renders: wall clock)
-        line = {"config": name, "scene": scene, "flags": flags, "width": opts.width, "height": h,
+        line = {"config": name, "scene": os.path.basename(scene), "flags": flags, "width": opts.width, "height": h,
                 "triangles": host.info.n_faces, "load_s": round(t_load, 2), "upload_and_trees_s": round(t_up, 2),
                 "frame_ms": round(wall * 1e3, 2), "rays": st["rays"],
                 "mrays_per_s": round(st["rays"] / wall / 1e6, 2),
                 "work": {k: st[k] for k in ("camera_rays", "secondary_rays", "shadow_rays", "node_visits",
                                             "object_tests", "tri_tests")},
+                "fused_walks": os.environ.get("RTX_FUSE", "1") != "0" and os.environ.get("RTX_FUSE_AREA", "1") != "0",
                 "path": ("megakernel" if os.environ.get("RTX_MEGAKERNEL", "0") not in ("", "0") else
                          "wavefront (adaptive levels)" if opts.aa_mode == pkg.RTX_AA_ADAPTIVE else "wavefront")}
         print(json.dumps(line), flush=True)
