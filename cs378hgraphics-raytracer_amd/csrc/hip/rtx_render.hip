@@ -3536,13 +3536,17 @@ static rtx_status render_once(SceneState* st, const RtxRenderParams* params, uin
       // nothing — the pool is then floored below — never a wrapped-around
       // 96 GiB)
       size_t slot_budget = avail > pool_need ? std::min<size_t>(size_t(96) << 30, avail - pool_need) : 0;
-      // Frame-memory cap (RTX_MEM_GB GiB, default none): the slot pool
+      // Frame-memory cap (RTX_MEM_GB GiB, default 48): the slot pool
       // gets what the cap leaves after the sample sums and the buckets.  The
       // buckets keep their size — whether a frame has buckets must not
       // depend on the cap, the image would change with it — so the cap only
       // sets how many samples are in flight at once (the rest are claimed
       // as slots free up, kdone).
-      size_t cap_gb = 0;
+      // Default 48 GiB: the knee of R1, the recursion-heavy glass frame (71 GB
+      // uncapped, 255 ms; capped at 48 GiB 52 GB, 255 ms; at 40 GiB 44 GB,
+      // 270 ms: profiles/r05a_r1_mem_knee.jsonl); the headline, C3, C4 and the
+      // shards stay under it (RTX_MEM_GB=0: no cap).
+      size_t cap_gb = 48;
       if (const char* e = getenv("RTX_MEM_GB")) cap_gb = static_cast<size_t>(atoll(e));
       if (cap_gb > 0) {
         const size_t cap_b = cap_gb << 30, fixed = sbuf_need + pool_need;

@@ -519,11 +519,15 @@ RT_HD bool trav_step(Trav& T, const DevScene& S, int* __restrict__ stk, const in
     // strictly farther than the mesh's best; next: farther than the
     // current best key) — tri_hit stops before the edge tests
     const double tcap = closest && T.mhave ? rtm::gmin(whi, T.mbest) : whi;
-#ifndef RTX_NO_TRI_PRE
-    // The leaf's faces as floats in one burst (3 x 48 B; a leaf of fewer
-    // faces loads its last one again), the conservative float prefilter on
-    // each (tri_pre), and the exact FP64 tri_hit only on the faces it
-    // cannot reject — the double face (96 B) then, not for every face.
+#ifdef RTX_TRI_PRE
+    // Opt-in: the leaf's faces as floats in one burst (3 x 48 B; a leaf of
+    // fewer faces loads its last one again), the conservative float
+    // prefilter on each (tri_pre), and the exact FP64 tri_hit only on the
+    // faces it cannot reject — the double face (96 B) then, not for every
+    // face.  Exact (tests/test_record_test_host.py) but measured slower:
+    // headline 33.9-34.1 vs 33.2-33.4 ms, R1 265-267 vs 255 ms
+    // (profiles/r05h_ab_tri_pre.txt) — the kernels are bound neither by the
+    // FP64 face tests nor by the faces' round trips.
     const FaceF* ff = S.tfacef + T.mfoff + f0;
     const int nf = f1 - f0;
     const FaceF q0 = ff[0], q1 = ff[nf > 1 ? 1 : 0], q2 = ff[nf > 2 ? 2 : 0];
