@@ -767,7 +767,9 @@ __device__ __forceinline__ void bucket_add(const FrameParams& F, int s, int b, c
 // A bucket set for unit s (lanes with `want`: a root ray about to push a
 // node child), wave-aggregated like fork_claim.  Past the pool's capacity
 // the unit gets none and *bover says so (bucket_add then drops its colours:
-// the host re-renders with a full-size pool, rtx_render).
+// collect_check reads the bit back per frame — a synchronous render is
+// rendered again with a full-size pool, a device-buffer render reports
+// RTX_ERR_FRAME).
 __device__ __forceinline__ void bucket_alloc(const FrameParams& F, int s, bool want) {
   const unsigned long long m = __ballot(want);
   if (m == 0ull) return;

@@ -279,6 +279,16 @@ RT_HD bool trav_step(Trav& T, const DevScene& S, int* __restrict__ stk, const in
     // in flight (the scheduler used to place the loads after the bounds)
     const DevNode4* recs = !mesh ? S.snode4 : (ref < S.n_mhot ? S.mhot : S.mnode4);
     const Rec4 rec = load_rec4(recs[ref]);
+#ifdef RTX_AMP_LOADS
+    // (diagnostic: the record loaded a second time — L1 hits issued in the
+    // same burst — to tell memory-pipeline throughput from latency)
+    {
+      int zero = 0;
+      asm volatile("" : "+v"(zero));
+      const Rec4 r2 = load_rec4(recs[ref + zero]);
+      pin(r2.lx.x), pin(r2.ly.y), pin(r2.lz.z), pin(r2.hx.w), pin(r2.hy.x), pin(r2.hz.y), pin(r2.ch.z), pin(r2.nrec);
+    }
+#endif
 #ifdef RTX_EARLY_REC  // (measured: no gain, 33.16 vs 33.11-33.15 ms, profiles/r05e_ab_ident_early.txt)
     sched_fence();
 #endif
