@@ -2003,6 +2003,10 @@ __global__ void __launch_bounds__(WG, !FUSED ? RTX_TRACE_WAVES : (MODE == Q_CLOS
   const bool cam = CAM && FUSED && MODE == Q_CLOSEST && SA.cam_n > 0;  // first iteration: claims + camera rays here
   const unsigned int nq = cam ? static_cast<unsigned int>(SA.cam_n) : counters[CNT_Q + (MODE - 1) * CNT_LINE];
   unsigned int* claim = counters + CNT_CLAIM + (MODE - 1) * CNT_LINE;
+
+#if defined(RTX_EARLYOUT) && RTX_TEAM
+#error "RTX_TEAM: a helper's answer does not carry the early-out's blocked flag"
+#endif
 #ifdef RTX_EARLYOUT
   using Blk = typename std::conditional<MODE == Q_NEXT, ShadowBlocker, NoBlocker>::type;
 #else
@@ -2189,6 +2193,12 @@ __global__ void __launch_bounds__(WG, !FUSED ? RTX_TRACE_WAVES : (MODE == Q_CLOS
     if (__ballot(active || pend) == 0ull) break;  // nothing claimed and nothing left
     const int thresh = exhausted ? 1 : RTX_REFILL;
     do {
+#if RTX_TEAM
+      // idle lanes help with pending mesh subtrees (team_donate; RTX_TEAM 2:
+      // also before the wave's query list is exhausted)
+      if (FUSED && (RTX_TEAM >= 2 || exhausted)) team_donate(T, stk, lane, active, stack_cap - TEAM_STASH);
+      bool hdone = false;
+#endif
       // Postponed costly units (Aila & Laine's while-while, one call site):
       // while at least leaf_k lanes of the wave are at a 4-wide record, only
       // those lanes step, so most steps run the record test alone instead of
@@ -2209,6 +2219,11 @@ __global__ void __launch_bounds__(WG, !FUSED ? RTX_TRACE_WAVES : (MODE == Q_CLOS
       if (go) {
         if (STATS) qsteps++;
         if (trav_step<STATS, MODE>(T, S, stk, lane, blk, C)) {
+#if RTX_TEAM
+          if (FUSED && (T.team & TEAM_HELPER))
+            hdone = true;
+          else
+#endif
           if (FUSED) pend = true;
           else finish();
           active = false;
@@ -2219,6 +2234,9 @@ __global__ void __launch_bounds__(WG, !FUSED ? RTX_TRACE_WAVES : (MODE == Q_CLOS
           qsteps = 0;
         }
       }
+#if RTX_TEAM
+      if (FUSED) team_merge(T, stk, lane, hdone, MODE == Q_CLOSEST, stack_cap - TEAM_STASH);
+#endif
       if (STATS) {
         const uint64_t dt = clock64() - st0;
 #pragma unroll
@@ -2837,6 +2855,9 @@ rtx_status rtx_scene_create(int device, const RtxSceneDesc* d, void** out) {
     S.sroot = tt.sroot;
     // per-lane LDS stack: scene-level entries stay below a mesh walk's
     st->stack_cap = tt.sneed + tt.mneed + 2;
+#if RTX_TEAM
+    st->stack_cap = std::max(st->stack_cap, tt.mneed + TEAM_STASH);  // a helper's walk + its parked answer
+#endif
 #define UP(src, n, dst) \
   if ((rc = upload(*st, src, size_t(n), &dst)) != RTX_OK) { rtx_scene_destroy(st); return rc; }
     UP(tt.sn4.data(), tt.sn4.size(), S.snode4);
@@ -3818,6 +3839,8 @@ static rtx_status render_once(SceneState* st, const RtxRenderParams* params, uin
     HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, tfn, WG, lds));
     if (per_cu < 1) per_cu = 1;
     int64_t tgrid = static_cast<int64_t>(st->n_cu) * per_cu;
+    const int64_t tgrid_full = std::min<int64_t>(per, tgrid);
+    int64_t small_frame = 10000000;
     {
       // Persistent trace grids of 1/div of the resident workgroups, so the
       // groups' kernels share the GPU instead of each filling it: on small
@@ -3827,10 +3850,9 @@ static rtx_status render_once(SceneState* st, const RtxRenderParams* params, uin
       // space behind the other groups' persistent kernels (8-way headline
       // shard 7.85-8.08 -> 7.61 ms; the whole frame 36.9 -> 38.4 ms, so not
       // there).  RTX_TGRID_DIV overrides (1: whole-GPU grids).
-      int64_t small = 10000000;
       const char* es = getenv("RTX_TGRID_SMALL");
-      if (es) small = atoll(es);
-      int div = F.n_samples <= small ? G : 1;
+      if (es) small_frame = atoll(es);
+      int div = F.n_samples <= small_frame ? G : 1;
       const char* e = getenv("RTX_TGRID_DIV");
       if (e && atoi(e) > 0) div = atoi(e);
       if (div > 1) tgrid = std::max<int64_t>(1, tgrid / div);
@@ -3839,6 +3861,7 @@ static rtx_status render_once(SceneState* st, const RtxRenderParams* params, uin
     // the fused kernels' own residency (their launch bounds differ:
     // RTX_SHADE_WAVES / RTX_WALK_WAVES)
     int64_t tgrid_c = tgrid, tgrid_n = tgrid;
+    int64_t tfull_c = tgrid_full, tfull_n = tgrid_full;  // whole-GPU residency
     if (fuse) {
       int pc = 0, pn = 0;
       HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(
@@ -3847,7 +3870,22 @@ static rtx_status render_once(SceneState* st, const RtxRenderParams* params, uin
           &pn, reinterpret_cast<const void*>(trace_kernel<false, Q_NEXT, true>), WG, lds));
       tgrid_c = std::min<int64_t>(per, std::max<int64_t>(1, tgrid * std::max(1, pc) / per_cu));
       tgrid_n = std::min<int64_t>(per, std::max<int64_t>(1, tgrid * std::max(1, pn) / per_cu));
+      tfull_c = std::min<int64_t>(per, std::max<int64_t>(1, tgrid_full * std::max(1, pc) / per_cu));
+      tfull_n = std::min<int64_t>(per, std::max<int64_t>(1, tgrid_full * std::max(1, pn) / per_cu));
     }
+    // The first iteration's closest-hit / walk grids as a percentage of the
+    // whole GPU's residency (RTX_TG0_C / RTX_TG0_N; 0 = the grids above).
+    // On whole frames (div 1) the groups' first launches otherwise each take
+    // the whole GPU in turn: group 0's camera rays first, then its walks
+    // beside the others' camera rays, and its advance launch starved of CUs
+    // until their walks end, so all three groups reach their advance launches
+    // together and the GPU streams lane state with no traversal beside it.
+    // Half-GPU first launches stagger the groups: headline 31.5-31.9 vs
+    // 32.6-33.0 ms, C4 42.2-42.6 vs 43.9 (profiles/r05l_ab_first_grid.txt).
+    // Shards keep their 1/G grids (no change measured there).
+    int tg0_c = F.n_samples > small_frame ? 50 : 0, tg0_n = F.n_samples > small_frame ? 50 : 0;
+    if (const char* e = getenv("RTX_TG0_C")) tg0_c = std::max(0, std::min(100, atoi(e)));
+    if (const char* e = getenv("RTX_TG0_N")) tg0_n = std::max(0, std::min(100, atoi(e)));
     const char* dbg_env = getenv("RTX_DEBUG");
     const bool dbg = dbg_env && atoi(dbg_env) != 0;
     const int dbg_level = dbg_env ? atoi(dbg_env) : 0;
@@ -3928,7 +3966,10 @@ static rtx_status render_once(SceneState* st, const RtxRenderParams* params, uin
         const int first = it == 0 ? 1 : (cam_first && it == 1 ? 2 : 0);
         const int64_t lb = grid_bound[size_t(g)];
         const int64_t agrid = first ? per : std::max<int64_t>(1, std::min<int64_t>(per, (lb + WG - 1) / WG));
-        const int64_t tg = std::max<int64_t>(1, std::min<int64_t>(fuse ? tgrid_c : tgrid, (lb + WG - 1) / WG));
+        const int64_t tgc_it =
+            fuse && it == 0 && tg0_c > 0 ? std::max<int64_t>(1, tfull_c * tg0_c / 100) : (fuse ? tgrid_c : tgrid);
+        const int64_t tgn_it = fuse && it == 0 && tg0_n > 0 ? std::max<int64_t>(1, tfull_n * tg0_n / 100) : tgrid_n;
+        const int64_t tg = std::max<int64_t>(1, std::min<int64_t>(std::min<int64_t>(per, tgc_it), (lb + WG - 1) / WG));
         const bool cam_it = cam_first && it == 0;
         if (cam_it) {
           // the slots the first launch does not claim start idle
@@ -3952,7 +3993,8 @@ static rtx_status render_once(SceneState* st, const RtxRenderParams* params, uin
           });
         }
         // the next-hit grid: fused walks can outnumber the live slots
-        const int64_t tgn = fuse ? std::max<int64_t>(1, std::min<int64_t>(tgrid_n, (lb * int64_t(nrec_n) + WG - 1) / WG))
+        const int64_t tgn = fuse ? std::max<int64_t>(1, std::min<int64_t>(std::min<int64_t>(per * nrec_n, tgn_it),
+                                                                          (lb * int64_t(nrec_n) + WG - 1) / WG))
                                  : tg;
         ShadeArgs sa;
         std::memset(&sa, 0, sizeof(sa));

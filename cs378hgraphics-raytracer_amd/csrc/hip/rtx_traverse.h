@@ -18,6 +18,14 @@
 #define Q_CLOSEST 1
 #define Q_NEXT 2
 
+// Teams (team_donate below): lanes of a wave without a query of their own
+// walk pending mesh subtrees of lanes that still have work.  0 = off.
+#ifndef RTX_TEAM
+#define RTX_TEAM 0
+#endif
+#define TEAM_HELPER 0x80
+#define TEAM_STASH 5  // stack entries a helper's own answer is parked in (top of its column)
+
 namespace rtxd {
 
 // Unified query over the two-level BVH.
@@ -66,6 +74,9 @@ struct Trav {
   int moi, mbase, mfoff, mnoff, mface;
   bool mhave;
   bool closest;  // the query's mode (read by the Q_ANY instantiations)
+#if RTX_TEAM
+  int team;  // teams (team_donate): 0, a helper (TEAM_HELPER | owner lane) or an owner (helpers << 8)
+#endif
 };
 
 // QMODE Q_ANY: one instantiation for both query kinds, the mode read from
@@ -210,6 +221,9 @@ RT_HD bool trav_init(Trav& T, const DevScene& S, const dvec3& P, const dvec3& D,
   T.bsub = INT_MAX;
   T.have = false;
   T.blocked = false;
+#if RTX_TEAM
+  T.team = 0;
+#endif
   if (QMODE != Q_ANY) T.closest = QMODE == Q_CLOSEST;  // Q_ANY: set by the caller first
   if (S.n_snodes == 0) return false;
   T.tlo = QMODE == Q_CLOSEST ? -RTX_INF : tp - S.margin;  // Q_ANY: tp = -inf for a closest query
@@ -250,6 +264,9 @@ RT_HD void trav_reset(Trav& T) {
   T.rp = T.sq = T.bobj = T.bsub = T.sp = T.ref = T.mode = T.oc = T.oe = 0;
   T.moi = T.mbase = T.mfoff = T.mnoff = T.mface = 0;
   T.have = T.blocked = T.mhave = T.closest = false;
+#if RTX_TEAM
+  T.team = 0;
+#endif
 }
 
 // The lane's next unit is a 4-wide record (scene or mesh): the cheap step.
@@ -604,6 +621,15 @@ RT_HD bool trav_step(Trav& T, const DevScene& S, int* __restrict__ stk, const in
     ref = stk[sp * 64 + lane];
     return false;
   }
+#if RTX_TEAM
+  if (T.team != 0) {
+    // a helper's subtree is done (the wave merges its minimum into the
+    // owner's); an owner waits here, at its mesh's end, for its helpers
+    if (T.team & TEAM_HELPER) return true;
+    ref = ~0;  // an empty leaf: the next steps come back here
+    return false;
+  }
+#endif
   // mesh finished: Trimesh::intersectLocal's result enters Scene::intersect
   T.rf = ray_f(T.P, T.D, T.ri);
   if (closest && T.mhave) {
@@ -625,6 +651,151 @@ RT_HD bool trav_step(Trav& T, const DevScene& S, int* __restrict__ stk, const in
   T.mode = 0;
   return false;
 }
+
+#if RTX_TEAM
+// Teams.  A query's answer is a minimum under a total order — the closest
+// hit: per mesh the (t, face rank)-smallest face passing leaf_ok; the next
+// hit: the (t, object, sub)-smallest key after the previous one — and every
+// pruning bound only drops candidates that cannot be that minimum.  So a
+// pending subtree of a lane's mesh walk (an entry of its stack above
+// T.mbase) can be walked by another lane with a copy of the ray, the bounds
+// and the best so far, and the two minima merged: the answer is the same
+// candidate ("Teams").
+//
+// team_donate (wave-uniform, when the wave's query list is exhausted): the
+// k-th lane without an active query takes the bottom mesh entry (the largest
+// pending subtree: entries are pushed farthest-first, deeper ones above) of
+// the k-th lane walking a mesh with entries left; the owner moves its top
+// entry into the hole.  A helper that holds a finished answer (pend) parks it
+// in the TEAM_STASH top entries of its own stack column (a mesh walk from a
+// subtree needs at most stack_cap - TEAM_STASH entries, host-sized).
+__device__ inline void team_donate(Trav& T, int* __restrict__ stk, const int lane, bool& active, const int stash) {
+  const unsigned long long idle = __ballot(!active);
+  if (idle == 0ull) return;
+  const unsigned long long dmask =
+      __ballot(active && !(T.team & TEAM_HELPER) && T.mode == 2 && T.sp > T.mbase);
+  if (dmask == 0ull) return;
+  int src = lane;
+  bool newh = false, give = false;
+  unsigned long long im = idle, dm = dmask;
+  while (im != 0ull && dm != 0ull) {
+    const int h = __builtin_ctzll(im), d = __builtin_ctzll(dm);
+    im &= im - 1ull;
+    dm &= dm - 1ull;
+    if (lane == h) {
+      src = d;
+      newh = true;
+    }
+    if (lane == d) give = true;
+  }
+  int e = 0;
+  if (give) {
+    const int b = T.mbase;
+    e = stk[b * 64 + lane];
+    stk[b * 64 + lane] = stk[(T.sp - 1) * 64 + lane];
+    T.sp--;
+    T.team += 256;
+  }
+  if (newh) {
+    stk[(stash + 0) * 64 + lane] = T.have ? 1 : 0;
+    stk[(stash + 1) * 64 + lane] = __double2loint(T.bt);
+    stk[(stash + 2) * 64 + lane] = __double2hiint(T.bt);
+    stk[(stash + 3) * 64 + lane] = T.bobj;
+    stk[(stash + 4) * 64 + lane] = T.bsub;
+  }
+  // the owner's ray (mesh frame), bounds and best so far; identity elsewhere
+  e = __shfl(e, src);
+#pragma unroll
+  for (int a = 0; a < 3; ++a) {
+    T.rf.olo[a] = __shfl(T.rf.olo[a], src);
+    T.rf.ohi[a] = __shfl(T.rf.ohi[a], src);
+    T.rf.inv[a] = __shfl(T.rf.inv[a], src);
+  }
+  T.rf.err = __shfl(T.rf.err, src);
+  T.lp.x = __shfl(T.lp.x, src);
+  T.lp.y = __shfl(T.lp.y, src);
+  T.lp.z = __shfl(T.lp.z, src);
+  T.ld.x = __shfl(T.ld.x, src);
+  T.ld.y = __shfl(T.ld.y, src);
+  T.ld.z = __shfl(T.ld.z, src);
+  T.tp = __shfl(T.tp, src);
+  T.tlimit = __shfl(T.tlimit, src);
+  T.tlo = __shfl(T.tlo, src);
+  T.rp = __shfl(T.rp, src);
+  T.sq = __shfl(T.sq, src);
+  T.bt = __shfl(T.bt, src);
+  T.bobj = __shfl(T.bobj, src);
+  T.bsub = __shfl(T.bsub, src);
+  T.have = __shfl(T.have ? 1 : 0, src) != 0;
+  T.len = __shfl(T.len, src);
+  T.mbest = __shfl(T.mbest, src);
+  T.moi = __shfl(T.moi, src);
+  T.mfoff = __shfl(T.mfoff, src);
+  T.mnoff = __shfl(T.mnoff, src);
+  T.mface = __shfl(T.mface, src);
+  T.mhave = __shfl(T.mhave ? 1 : 0, src) != 0;
+  T.closest = __shfl(T.closest ? 1 : 0, src) != 0;
+  if (newh) {
+    T.ref = e;
+    T.sp = 0;
+    T.mbase = 0;
+    T.mode = 2;
+    T.oc = T.oe = 0;
+    T.blocked = false;
+    T.team = TEAM_HELPER | src;
+    active = true;
+  }
+}
+
+// Helpers whose subtree is done (hdone) merge their minimum into their
+// owner's — closest: the mesh's best face (the owner waits at its mesh's
+// end, so the merge is at mesh level, with the face-rank tie rule); next
+// hit: the key — and take their own answer back from the stash.
+__device__ inline void team_merge(Trav& T, const int* __restrict__ stk, const int lane, const bool hdone, const bool closest,
+                      const int stash) {
+  unsigned long long hm = __ballot(hdone);
+  while (hm != 0ull) {
+    const int h = __builtin_ctzll(hm);
+    hm &= hm - 1ull;
+    const int o = __builtin_amdgcn_readlane(T.team & 63, h);
+    if (closest) {
+      const bool hh = __builtin_amdgcn_readlane(T.mhave ? 1 : 0, h) != 0;
+      const double hb = __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(T.mbest), h),
+                                         __builtin_amdgcn_readlane(__double2loint(T.mbest), h));
+      const int hf = __builtin_amdgcn_readlane(T.mface, h);
+      if (lane == o) {
+        if (hh && (!T.mhave || hb < T.mbest || (hb == T.mbest && hf < T.mface))) {
+          T.mbest = hb;
+          T.mface = hf;
+          T.mhave = true;
+        }
+        T.team -= 256;
+      }
+    } else {
+      const bool hh = __builtin_amdgcn_readlane(T.have ? 1 : 0, h) != 0;
+      const double hb = __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(T.bt), h),
+                                         __builtin_amdgcn_readlane(__double2loint(T.bt), h));
+      const int ho = __builtin_amdgcn_readlane(T.bobj, h), hs = __builtin_amdgcn_readlane(T.bsub, h);
+      if (lane == o) {
+        if (hh && (!T.have || key_less(hb, ho, hs, T.bt, T.bobj, T.bsub))) {
+          T.bt = hb;
+          T.bobj = ho;
+          T.bsub = hs;
+          T.have = true;
+        }
+        T.team -= 256;
+      }
+    }
+  }
+  if (hdone) {
+    T.have = stk[(stash + 0) * 64 + lane] != 0;
+    T.bt = __hiloint2double(stk[(stash + 2) * 64 + lane], stk[(stash + 1) * 64 + lane]);
+    T.bobj = stk[(stash + 3) * 64 + lane];
+    T.bsub = stk[(stash + 4) * 64 + lane];
+    T.team = 0;
+  }
+}
+#endif
 
 // One query to completion (no shadow early-out).
 template <bool STATS>
