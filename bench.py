@@ -4,7 +4,7 @@ trimesh2.ray (stand-in, tools/gen_scenes.py) at 1920x1080, depth 5, 4x4
 regular AA (`ray -w 1920 -r 5 -O r -A 4`).
 
 One step = one frame.  On N GPUs (one process per GPU, torch.distributed over
-RCCL) the frame is cut into 32x32 tiles dealt round-robin along rotated rows
+RCCL) the frame is cut into 16x16 tiles dealt round-robin along rotated rows
 (diagonal stripes, deal index % N == rank),
 each rank renders its tiles into a packed HBM buffer and rank 0 gathers them
 over xGMI (dist.gather) — total work is fixed, so scaling is strong.
@@ -351,7 +351,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--scene", default=os.path.join(ROOT, "scenes", "trimesh2.ray"))
     ap.add_argument("--flags", default="-w 1920 -r 5 -O r -A 4")
-    ap.add_argument("--tile", type=int, default=32)
+    ap.add_argument("--tile", type=int, default=16)
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     ap.add_argument("--cpu-budget", type=float, default=10.0, help="seconds of CPU work per baseline run")
     ap.add_argument("--no-parity", action="store_true", help="skip the parity block of the timed frame")

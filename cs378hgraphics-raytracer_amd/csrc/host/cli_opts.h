@@ -47,7 +47,7 @@ struct CliOptions {
   // extensions
   int device = 0;      // first GPU (ranks use device + rank)
   int gpus = 0;        // > 0: tile-shard the frame over this many GPUs (multi_gpu.cpp)
-  int tile = 32;       // shard tile size with --gpus
+  int tile = 16;       // shard tile size with --gpus (16: the 8-way headline's slowest shard 2-3 % faster than with 32, profiles/r05o_ab_tile.txt)
   bool stats = false;
   std::string dump_f64, dump_hits;
 };
@@ -66,8 +66,8 @@ inline void cli_usage(const char* prog, const CliOptions& o) {
             << "  -B <?>      a: adaptive AA threshold, d: DoF samples\n"
             << "  -C <?>      d: aperture size\n"
             << "  --device N  GPU index (extension)   --stats  print JSON stats (extension)\n"
-            << "  --gpus N    one process per GPU, 32x32 tiles dealt over N GPUs, RCCL gather (extension)\n"
-            << "  --tile T    tile size with --gpus (default 32)\n"
+            << "  --gpus N    one process per GPU, 16x16 tiles dealt over N GPUs, RCCL gather (extension)\n"
+            << "  --tile T    tile size with --gpus (default 16)\n"
             << "  --dump-f64 FILE / --dump-hits FILE  raw float64 RGB / hit records (extension)\n";
 }
 

@@ -7,7 +7,7 @@
 //             reaps them as they end; on the first failing rank it ends the
 //             others (SIGTERM, then SIGKILL) and returns that rank's status.
 //   rank r  : device r; rtx_scene_create; ncclCommInitRank over a unique id
-//             that rank 0 publishes in a shared page; renders the 32x32 tiles
+//             that rank 0 publishes in a shared page; renders the 16x16 tiles
 //             the deal gives shard r (rtx_render, packed tile order, output
 //             left in HBM); ncclGather of the packed RGB8 shards to rank 0.
 //   rank 0  : rtx_unpack_tiles of every shard into the frame, writeImage.
@@ -108,7 +108,7 @@ bool rendezvous_join(Rendezvous* rv, int rank, int nranks) {
   } while (0)
 
 int run_rank(const rtxh::CliOptions& o, void* hs, int rank, int nranks, Rendezvous* rv) {
-  const int tile = o.tile > 0 ? o.tile : 32;
+  const int tile = o.tile > 0 ? o.tile : 16;
   if (rank == 0) {
     ncclUniqueId id;
     const ncclResult_t r = ncclGetUniqueId(&id);

@@ -61,7 +61,7 @@ def test_multi_gpu_cli_equals_single(pkg, tmp_path, scene, flags):
 
 def test_bad_numeric_options_refused():
     """--gpus / --tile / --device take whole numbers in range:
-    no silent fallback to one GPU or to 32x32 tiles."""
+    no silent fallback to one GPU or to the default tiles."""
     for args in (["--gpus", "abc"], ["--gpus", "0"], ["--tile", "0"], ["--tile", "-4"], ["--device", "x1"]):
         r = _run(args + [scene_path("hitchcock.ray"), "/tmp/never.png"])
         assert r.returncode == 1, (args, r.returncode, r.stderr)

@@ -47,7 +47,7 @@ def main():
     for n in ns:
         seq, pipe = [], []
         for r in range(n):
-            tile = 32 if n > 1 else 0
+            tile = 16 if n > 1 else 0
             npix = pkg.shard_pixels(opts, h, tile, r, n, n > 1)
             outs = [torch.zeros(npix * 3, dtype=torch.uint8, device="cuda") for _ in range(2)]
 

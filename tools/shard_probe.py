@@ -4,7 +4,7 @@ GPU (back-to-back frames, which overlap on the scene's two frame contexts,
 and one frame alone): rank r of N renders tiles t % N == r (what bench.py --gpus N runs on
 each GPU).  The slowest shard's time bounds the N-GPU frame (plus the RCCL
 gather of a few MB).  Prints one JSON line per N.
-usage (GPU box): python tools/shard_probe.py [--scene NAME.ray] [--flags "-w 1920 ..."] [--rank R] [N ...]
+usage (GPU box): python tools/shard_probe.py [--scene NAME.ray] [--flags "-w 1920 ..."] [--rank R] [--tile T] [N ...]
 (--rank R: only rank R of each N > 1, e.g. for a kernel trace of one shard;
  --own-stream: a created stream, not the default one)
 (dragon.ray, C5's scene, is generated when missing: tools/gen_scenes.py --dragon)"""
@@ -37,7 +37,8 @@ def main():
     scene = "trimesh2.ray"
     only_rank = None
     own_stream = False
-    while args and args[0] in ("--flags", "--scene", "--rank", "--own-stream"):
+    tile_px = 16  # bench.py's default
+    while args and args[0] in ("--flags", "--scene", "--rank", "--own-stream", "--tile"):
         if args[0] == "--own-stream":  # render on a created stream instead of torch's default (null) stream
             own_stream = True
             args = args[1:]
@@ -46,6 +47,8 @@ def main():
             flags = args[1]
         elif args[0] == "--rank":
             only_rank = int(args[1])
+        elif args[0] == "--tile":
+            tile_px = int(args[1])
         else:
             scene = args[1]
         args = args[2:]
@@ -65,7 +68,7 @@ def main():
         for r in range(n):
             if only_rank is not None and n > 1 and r != only_rank:
                 continue
-            tile = 32 if n > 1 else 0
+            tile = tile_px if n > 1 else 0
             npix = pkg.shard_pixels(opts, h, tile, r, n, n > 1)
             out = torch.zeros(npix * 3, dtype=torch.uint8, device="cuda")
             for _ in range(4):  # warm both frame contexts (buffers, bucket-pool sizes)

@@ -27,7 +27,7 @@ def main():
     rank, n = (int(args[0]), int(args[1])) if len(args) >= 2 else (0, 1)
     opts = pkg.RenderOptions.from_cli(flags.split())
     dev = pkg.DeviceScene(pkg.HostScene(os.path.join(ROOT, "scenes", scene)), 0)
-    tile = 32 if n > 1 else 0
+    tile = 16 if n > 1 else 0
     out = dev.render(opts, want_f64=False, stats=True, tile=tile, shard=rank, nshards=n, packed=n > 1)
     print({k: v for k, v in out["stats"].items() if k != "kernels"}, flush=True)
 
