@@ -3160,12 +3160,15 @@ rtx_status rtx_shard_pixels(const RtxRenderParams* p, int64_t* npix) {
   return RTX_OK;
 }
 
-// One render of frame `seq` (rtx_render below).  *redo: this synchronous
+// One render of frame `seq` (rtx_render below).  *redo 1: this synchronous
 // render found its history-sized buffers short (collect_check) — the image
-// is wrong and the caller renders again, now with full-size buffers.
+// is wrong and the caller renders again, now with full-size buffers.  2: the
+// frame's first render at the default fork depth found more fork requests
+// than spares — the caller renders it again at fork depth 3, as every later
+// render of the frame will be (run_wavefront, "forks outgrow the spares").
 static rtx_status render_once(SceneState* st, const RtxRenderParams* params, uint8_t* rgb8, double* rgb_f64,
                               RtxHitRecord* hits, int device_ptrs, void* stream_v, RtxStats* stats, int64_t seq,
-                              bool retry, bool* redo) {
+                              bool retry, int* redo) {
   HIP_TRY(hipSetDevice(st->device));
   hipStream_t stream = static_cast<hipStream_t>(stream_v);
   // Frame context (DESIGN.md "Frame contexts"): a render into device buffers
@@ -3207,6 +3210,11 @@ static rtx_status render_once(SceneState* st, const RtxRenderParams* params, uin
   collect_check(st, *X, true);
   collect_check(st, st->cx[X == &st->cx[0] ? 1 : 0], false);
   std::vector<uint64_t> chk_keys;  // this frame's history-sized runs (run_wavefront)
+  // the fork-depth probe (run_wavefront): a frame's first render at the
+  // default depth, whose per-group fork requests are compared with its spares
+  // before the render returns (>= 0: the spares; the history key)
+  int64_t depth_probe_spares = -1;
+  uint64_t depth_probe_key = 0;
   if (!X->free_ev) HIP_TRY(hipEventCreateWithFlags(&X->free_ev, hipEventDisableTiming));
   if (X->wf_streams.empty()) {
     hipStream_t s0;
@@ -3490,7 +3498,6 @@ static rtx_status render_once(SceneState* st, const RtxRenderParams* params, uin
     // full count (a set per unit) the first time.  Whether the frame has
     // buckets at all was decided above on the full count, so the image never
     // depends on the pool.
-    const size_t npos_b = (size_t(1) << (fork_depth + 1)) - 2;  // (as npos below)
     size_t bcap = nunit_out;
     bool spares_enough = false;  // the spares cover every fork request (no free list needed)
     // spare slots per sample slot at most, in percent (RTX_SPARE): 50 on
@@ -3505,15 +3512,23 @@ static rtx_status render_once(SceneState* st, const RtxRenderParams* params, uin
     // spare slots; with at least that many spares every request is granted
     // as on the first render).  -1: unknown, half a slot per sample.
     int64_t fspare = -1;
-    uint64_t bkey = 1469598103934665603ull;
-    {
+    bool forks_outgrow = false;  // (the history shows more fork requests than spares: depth 3, the lower cap)
+    // the frame's history key: its parameters, this run of the render and the
+    // bucket layout (fork depth)
+    auto frame_key = [&](int depth) {
+      uint64_t k = 1469598103934665603ull;
       auto mix = [&](const void* p, size_t n) {
         const unsigned char* c = static_cast<const unsigned char*>(p);
-        for (size_t k = 0; k < n; ++k) bkey = (bkey ^ c[k]) * 1099511628211ull;
+        for (size_t i = 0; i < n; ++i) k = (k ^ c[i]) * 1099511628211ull;
       };
       mix(&F.P, sizeof(F.P));
-      const int64_t ks[6] = {F.n_samples, nout, level0 ? 1 : 0, X->wf_call, int64_t(npos_b), int64_t(nunit_out)};
+      const int64_t npos = (int64_t(1) << (depth + 1)) - 2;
+      const int64_t ks[6] = {F.n_samples, nout, level0 ? 1 : 0, X->wf_call, npos, int64_t(nunit_out)};
       mix(ks, sizeof(ks));
+      return k;
+    };
+    uint64_t bkey = frame_key(fork_depth);
+    {
       for (FrameCtx& C : st->cx)  // the first-time frames' counts (either context's; long done by now)
         if (C.bstat_pending) {
           HIP_TRY(hipEventSynchronize(C.bstat_ev));
@@ -3527,6 +3542,31 @@ static rtx_status render_once(SceneState* st, const RtxRenderParams* params, uin
           }
           C.bstat_pending = false;
         }
+      // A frame whose fork requests outgrow the spare slots it may have (R1,
+      // the glass frame: forks at nearly every hit) forks down to heap depth
+      // 3: 14 bucket positions a set instead of 30, so the lower memory cap
+      // below keeps more slots in flight — R1 at 252-254 ms in 38.7 GB
+      // against 255 ms in 55.9 GB at depth 4 (profiles/r05q_ab_r1_memory.txt).
+      // The depth moves the line between bucket sums and the running sum
+      // (f64 images differ in the last bit), so every render of a frame uses
+      // the same one: the frame's first render at depth 4 reads its fork
+      // requests back before it returns and, when they outgrow the spares,
+      // is rendered again at depth 3 (rtx_render); the depth-4 history then
+      // decides every later render the same way.
+      if (fork_ok && fork_depth == 4 && !fd_env && !adaptive) {
+        const int64_t spares = (F.n_samples + G - 1) / G * spare_pct / 100;
+        const auto h4 = st->bucket_hist.find(bkey);
+        if (h4 == st->bucket_hist.end()) {
+          depth_probe_spares = spares;
+          depth_probe_key = bkey;
+        } else if (h4->second.forks > spares) {
+          fork_depth = 3;
+          bkey = frame_key(fork_depth);
+          forks_outgrow = true;
+          if (const char* e = getenv("RTX_DEBUG"))
+            if (atoi(e) != 0) fprintf(stderr, "rtx: forks outgrow the spares: fork depth 3, 34-GiB cap\n");
+        }
+      }
       const auto it = st->bucket_hist.find(bkey);
       if (it != st->bucket_hist.end()) {
         bcap = std::min<size_t>(nunit_out, size_t(it->second.sets) + 64);
@@ -3559,17 +3599,23 @@ static rtx_status render_once(SceneState* st, const RtxRenderParams* params, uin
       // nothing — the pool is then floored below — never a wrapped-around
       // 96 GiB)
       size_t slot_budget = avail > pool_need ? std::min<size_t>(size_t(96) << 30, avail - pool_need) : 0;
-      // Frame-memory cap (RTX_MEM_GB GiB, default 48): the slot pool
+      // Frame-memory cap (RTX_MEM_GB GiB, default 48, 34 for frames whose
+      // forks outgrow their spares): the slot pool
       // gets what the cap leaves after the sample sums and the buckets.  The
       // buckets keep their size — whether a frame has buckets must not
       // depend on the cap, the image would change with it — so the cap only
       // sets how many samples are in flight at once (the rest are claimed
       // as slots free up, kdone).
-      // Default 48 GiB: the knee of R1, the recursion-heavy glass frame (71 GB
-      // uncapped, 255 ms; capped at 48 GiB 52 GB, 255 ms; at 40 GiB 44 GB,
-      // 270 ms: profiles/r05a_r1_mem_knee.jsonl); the headline, C3, C4 and the
-      // shards stay under it (RTX_MEM_GB=0: no cap).
-      size_t cap_gb = 48;
+      // 48 GiB: the headline, C3, C4, C5 and the shards stay under it (the
+      // headline's buckets alone are 24 GB: at 34 GiB its pool falls below a
+      // slot per sample, 34.4 vs 32.0 ms).  34 GiB where the forks outgrow
+      // the spares: the knee of R1, the recursion-heavy glass frame, with its
+      // buckets at fork depth 3 (above) — 36 / 38 / 42 / 50 GiB of frame
+      // buffers at caps of 34 / 36 / 40 / 48 GiB, 254 / 251 / 252 / 251 ms,
+      // 34 GiB at a cap of 32: 260 ms (profiles/r05q_ab_r1_memory.txt; at
+      // depth 4: 71 GB uncapped, 255 ms, 44 GB at a 40-GiB cap, 270 ms,
+      // r05a_r1_mem_knee.jsonl).  RTX_MEM_GB=0: no cap.
+      size_t cap_gb = forks_outgrow ? 34 : 48;
       if (const char* e = getenv("RTX_MEM_GB")) cap_gb = static_cast<size_t>(atoll(e));
       if (cap_gb > 0) {
         const size_t cap_b = cap_gb << 30, fixed = sbuf_need + pool_need;
@@ -4267,7 +4313,17 @@ static rtx_status render_once(SceneState* st, const RtxRenderParams* params, uin
     if (collect_check(st, *X, true)) {
       st->bad_n = nb;  // (not recorded: the caller gets the re-rendered frame)
       st->bad_first = fb;
-      *redo = true;
+      *redo = 1;
+      return RTX_OK;
+    }
+  }
+  // the fork-depth probe: this first render's fork requests, before it returns
+  if (depth_probe_spares >= 0 && X->bstat_pending && X->bstat_key == depth_probe_key && X->bstat_groups > 0) {
+    HIP_TRY(hipEventSynchronize(X->bstat_ev));
+    int64_t fm = 0;
+    for (int g = 0; g < X->bstat_groups; ++g) fm = std::max<int64_t>(fm, X->h_bstat[4 + g]);
+    if ((X->h_bstat[1] & 3u) == 0u && fm > depth_probe_spares) {
+      *redo = 2;  // (the pending counts become the depth-4 history at the re-render)
       return RTX_OK;
     }
   }
@@ -4327,11 +4383,12 @@ rtx_status rtx_render(void* scene, const RtxRenderParams* params, uint8_t* rgb8,
   }
   SceneState* st = static_cast<SceneState*>(scene);
   const int64_t seq = st->frame_seq++;
-  bool redo = false;
+  int redo = 0;
   rtx_status rc = render_once(st, params, rgb8, rgb_f64, hits, device_ptrs, stream_v, stats, seq, false, &redo);
   if (rc == RTX_OK && redo) {
-    fprintf(stderr, "rtx_render: rendering frame %lld again with full-size buffers\n", static_cast<long long>(seq));
-    redo = false;
+    if (redo == 1)
+      fprintf(stderr, "rtx_render: rendering frame %lld again with full-size buffers\n", static_cast<long long>(seq));
+    redo = 0;
     rc = render_once(st, params, rgb8, rgb_f64, hits, device_ptrs, stream_v, stats, seq, true, &redo);
     if (rc == RTX_OK && redo) {
       g_err = "rtx_render: the frame came out wrong twice (history-sized buffers short after a full-size re-render)";

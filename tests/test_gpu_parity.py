@@ -396,3 +396,65 @@ def test_wrong_frame_never_ok(pkg, capfd, monkeypatch, knob):
         for _ in range(3):
             _device_render_bytes(pkg, dev2, opts, want.size)
         dev2.frame_status()
+
+
+@pytest.mark.gpu
+def test_fork_depth_from_history(pkg, orc, capfd, monkeypatch):
+    """A frame whose fork requests outgrow its spare slots (the glass scene,
+    R1's) forks down to heap depth 3 under the lower frame-memory cap
+    (rtx_render, "forks outgrow the spares").  The depth changes the f64
+    image in the last bit, so the frame's first render — which finds out —
+    is rendered again at depth 3 before it returns: every render of the frame,
+    host-mode or into device buffers, must be the same bytes, and match the
+    CPU restatement."""
+    import ctypes as C
+
+    monkeypatch.setenv("RTX_DEBUG", "1")
+    scene, flags = "trimesh2_glass.ray", "-w 64 -r 5 -O r -A 4"
+    path = scene_path(scene)
+    opts = pkg.RenderOptions.from_cli(flags.split())
+    host = pkg.HostScene(path)
+    dev = pkg.DeviceScene(host, 0)
+    first = dev.render(opts, want_f64=True)
+    err = capfd.readouterr().err
+    assert "fork depth 3" in err, err[-2000:]  # (the first render's own re-render)
+    later = [dev.render(opts, want_f64=True) for _ in range(2)]
+    err = capfd.readouterr().err
+    assert "fork depth 3" in err, err[-2000:]
+    for r in later:
+        assert np.array_equal(r["rgb8"], first["rgb8"])
+        assert np.array_equal(r["rgb"], first["rgb"])
+    # into device buffers (pipelined frame contexts), against the first render
+    hip = C.CDLL("libamdhip64.so.7")
+    hip.hipMalloc.argtypes = [C.POINTER(C.c_void_p), C.c_size_t]
+    hip.hipFree.argtypes = [C.c_void_p]
+    hip.hipMemcpy.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int]
+    n = first["rgb8"].size
+    buf = C.c_void_p()
+    assert hip.hipMalloc(C.byref(buf), n) == 0
+    try:
+        for _ in range(3):
+            dev.render_device(opts, buf.value, 0, 0)
+        assert hip.hipDeviceSynchronize() == 0
+        got = np.zeros(n, np.uint8)
+        assert hip.hipMemcpy(got.ctypes.data, buf, n, 2) == 0
+        assert np.array_equal(got, first["rgb8"].reshape(-1))
+    finally:
+        hip.hipFree(buf)
+    ref = orc.render(pkg, path, opts, want_hits=False)
+    assert np.abs(first["rgb"] - ref["rgb"]).max() <= 1e-4
+    scaled = 255.0 * ref["rgb"]
+    boundary = np.abs(scaled - np.round(scaled)) < 1e-9
+    assert not ((first["rgb8"] != ref["rgb8"]) & ~boundary).any()
+
+
+@pytest.mark.gpu
+def test_fork_depth_first_render_is_depth3(pkg, capfd, monkeypatch):
+    """The first render of a frame whose forks outgrow the spares is itself
+    the depth-3 image: equal, in f64, to a render with RTX_FORK_DEPTH=3."""
+    scene, flags = "trimesh2_glass.ray", "-w 64 -r 5 -O r -A 4"
+    opts = pkg.RenderOptions.from_cli(flags.split())
+    a = pkg.DeviceScene(pkg.HostScene(scene_path(scene)), 0).render(opts, want_f64=True)
+    monkeypatch.setenv("RTX_FORK_DEPTH", "3")
+    b = pkg.DeviceScene(pkg.HostScene(scene_path(scene)), 0).render(opts, want_f64=True)
+    assert np.array_equal(a["rgb"], b["rgb"])
