@@ -3560,9 +3560,13 @@ static rtx_status render_once(SceneState* st, const RtxRenderParams* params, uin
           depth_probe_spares = spares;
           depth_probe_key = bkey;
         } else if (h4->second.forks > spares) {
+          const uint64_t key4 = bkey;
           fork_depth = 3;
           bkey = frame_key(fork_depth);
           forks_outgrow = true;
+          // (a frame whose two-entry stacks overflowed at depth 4 keeps full
+          // stacks at depth 3 too)
+          if (st->full_stack_keys.count(key4)) st->full_stack_keys.insert(bkey);
           if (const char* e = getenv("RTX_DEBUG"))
             if (atoi(e) != 0) fprintf(stderr, "rtx: forks outgrow the spares: fork depth 3, 34-GiB cap\n");
         }
@@ -4323,6 +4327,16 @@ static rtx_status render_once(SceneState* st, const RtxRenderParams* params, uin
     int64_t fm = 0;
     for (int g = 0; g < X->bstat_groups; ++g) fm = std::max<int64_t>(fm, X->h_bstat[4 + g]);
     if ((X->h_bstat[1] & 3u) == 0u && fm > depth_probe_spares) {
+      // this render's own frame check, now (its image is replaced: not a
+      // wrong frame, but a stack overflow still sends the re-render to full
+      // stacks)
+      if (X->chk_pending) {
+        HIP_TRY(hipStreamSynchronize(ws));
+        const int64_t nb = st->bad_n, fb = st->bad_first;
+        collect_check(st, *X, true);
+        st->bad_n = nb;
+        st->bad_first = fb;
+      }
       *redo = 2;  // (the pending counts become the depth-4 history at the re-render)
       return RTX_OK;
     }
