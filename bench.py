@@ -47,7 +47,7 @@ _HWQ_ENV = os.environ.get("GPU_MAX_HW_QUEUES")  # as the job got it (reported in
 if int(_HWQ_ENV or 0) < 16:
     if _HWQ_ENV:
         print(f"bench.py: GPU_MAX_HW_QUEUES={_HWQ_ENV} in the environment raised to 16 (the frame contexts' "
-              "six group streams need queues of their own)", file=sys.stderr)
+              "nine group streams need queues of their own)", file=sys.stderr)
     os.environ["GPU_MAX_HW_QUEUES"] = "16"
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
@@ -472,6 +472,7 @@ def main():
     # printed), and how many of them ran on the alternating frame contexts
     frame_check = dev.frame_status()
     pipelined, renders = dev.overlap_count()
+    n_ctx = dev.frame_contexts()
     # the last timed frame, for the byte comparison in the parity block
     timed_rgb8 = rgb8.cpu().numpy() if world == 1 else None
     # one frame alone (the frame before it finished, no overlap): the
@@ -635,7 +636,7 @@ def main():
             # timed frames that ran pipelined on the two frame contexts
             # (rtx_overlap_count), and the frame check of the timed frames
             # (rtx_frame_status: first wrong frame, wrong frames)
-            "frame_contexts": 2 if pipelined == renders and renders > 0 else (1 if pipelined == 0 else "mixed"),
+            "frame_contexts": n_ctx if pipelined == renders and renders > 0 else (1 if pipelined == 0 else "mixed"),
             "pipelined_frames": [pipelined, renders],
             "frame_check": {"first_bad": frame_check[0], "bad_frames": frame_check[1]},
             "gather_check": gather_check,

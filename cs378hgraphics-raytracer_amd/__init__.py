@@ -158,13 +158,15 @@ def hip_lib():
         lib.rtx_last_work.argtypes = [C.c_void_p, C.POINTER(C.c_int64), C.c_int]
         lib.rtx_frame_status.argtypes = [C.c_void_p, C.POINTER(C.c_int64), C.POINTER(C.c_int64)]
         lib.rtx_overlap_count.argtypes = [C.c_void_p, C.POINTER(C.c_int64), C.POINTER(C.c_int64)]
+        lib.rtx_frame_contexts.argtypes = [C.c_void_p, C.POINTER(C.c_int32)]
         _hip = lib
     return _hip
 
 
 # symbols include/*.h declare (checked by the CPU test suite)
 HIP_SYMBOLS = ["rtx_last_error", "rtx_device_count", "rtx_scene_create", "rtx_scene_destroy", "rtx_render",
-               "rtx_shard_pixels", "rtx_kernel_time", "rtx_last_work", "rtx_frame_status", "rtx_overlap_count"]
+               "rtx_shard_pixels", "rtx_kernel_time", "rtx_last_work", "rtx_frame_status", "rtx_overlap_count",
+               "rtx_frame_contexts"]
 HOST_SYMBOLS = ["rtx_host_last_error", "rtx_host_load", "rtx_host_desc", "rtx_host_info", "rtx_host_free",
                 "rtx_host_cubemap", "rtx_write_image", "rtx_image_height", "rtx_read_image", "rtx_shard_tiles",
                 "rtx_unpack_tiles", "rtx_host_tokens", "rtx_host_raw_records"]
@@ -410,6 +412,13 @@ class DeviceScene:
         a, b = C.c_int64(), C.c_int64()
         _check(lib.rtx_overlap_count(self._s, C.byref(a), C.byref(b)), lib, "rtx_overlap_count")
         return a.value, b.value
+
+    def frame_contexts(self):
+        """How many frame contexts pipelined renders rotate over (rtx_frame_contexts)."""
+        lib = hip_lib()
+        n = C.c_int32()
+        _check(lib.rtx_frame_contexts(self._s, C.byref(n)), lib, "rtx_frame_contexts")
+        return n.value
 
     def close(self):
         if self._s:

@@ -2646,8 +2646,13 @@ struct SceneState {
   unsigned long long* d_stats = nullptr;
   double* d_picks = nullptr;
   int picks_res = -1;
-  FrameCtx cx[2];
+  FrameCtx cx[4];
   unsigned int next_cx = 0;
+  // frame contexts pipelined renders rotate over (RTX_CONTEXTS 2..4): 3 —
+  // a frame's latency-bound tail then overlaps the next two frames' first
+  // iterations (8-way headline shard 4.78-4.87 vs 5.08-5.09 ms with 2, C4's
+  // 6.12-6.17 vs 6.35-6.40; 4 contexts no better: profiles/r05v_ab_contexts.txt)
+  unsigned int n_cx = 3;
   bool any_recur = true;  // some material reflects or refracts (no: no ray tree, no buckets)
   // Pinned staging for the frame's host-to-device copies (frame record,
   // scene record, DoF offsets).  A hipMemcpyAsync from pageable memory may
@@ -2914,8 +2919,11 @@ rtx_status rtx_scene_create(int device, const RtxSceneDesc* d, void** out) {
   // never recurse: their flags are 0, hit_flags)
   st->any_recur = false;
   for (int m = 0; m < d->n_materials; ++m) st->any_recur |= (d->materials[m].flags & RTX_MF_RECUR) != 0;
+  if (const char* e = getenv("RTX_CONTEXTS")) st->n_cx = static_cast<unsigned>(std::max(2, std::min(4, atoi(e))));
   if (hipMalloc(&st->cx[0].d_frame, sizeof(FrameParams)) != hipSuccess ||
       hipMalloc(&st->cx[1].d_frame, sizeof(FrameParams)) != hipSuccess ||
+      hipMalloc(&st->cx[2].d_frame, sizeof(FrameParams)) != hipSuccess ||
+      hipMalloc(&st->cx[3].d_frame, sizeof(FrameParams)) != hipSuccess ||
       hipMalloc(&st->d_work, sizeof(unsigned long long)) != hipSuccess ||
       hipMalloc(&st->d_stats, RTX_STATS_N * sizeof(unsigned long long)) != hipSuccess) {
     g_err = "rtx_scene_create: hipMalloc failed";
@@ -2982,6 +2990,12 @@ rtx_status rtx_overlap_count(void* scene, int64_t* overlapped, int64_t* renders)
   if (renders) *renders = st->n_renders;
   st->n_pipelined = 0;
   st->n_renders = 0;
+  return RTX_OK;
+}
+
+rtx_status rtx_frame_contexts(void* scene, int32_t* n) {
+  if (!scene || !n) return RTX_ERR_INVALID;
+  *n = static_cast<int32_t>(static_cast<SceneState*>(scene)->n_cx);
   return RTX_OK;
 }
 
@@ -3199,7 +3213,7 @@ static rtx_status render_once(SceneState* st, const RtxRenderParams* params, uin
   const bool pipelined = !(pipe_env && atoi(pipe_env) == 0) && device_ptrs && !hits && !stats &&
                          params->aa_mode != RTX_AA_ADAPTIVE && !(mk_env0 && atoi(mk_env0) != 0) &&
                          units0 <= pipe_max;
-  FrameCtx* X = pipelined ? &st->cx[(st->next_cx++) & 1u] : &st->cx[0];
+  FrameCtx* X = pipelined ? &st->cx[(st->next_cx++) % st->n_cx] : &st->cx[0];
   if (!retry) {
     ++st->n_renders;
     if (pipelined) ++st->n_pipelined;
@@ -3208,7 +3222,8 @@ static rtx_status render_once(SceneState* st, const RtxRenderParams* params, uin
   // done: the check is read before its buffers are reused), the other's if
   // it has run
   collect_check(st, *X, true);
-  collect_check(st, st->cx[X == &st->cx[0] ? 1 : 0], false);
+  for (FrameCtx& C : st->cx)
+    if (&C != X) collect_check(st, C, false);
   std::vector<uint64_t> chk_keys;  // this frame's history-sized runs (run_wavefront)
   // the fork-depth probe (run_wavefront): a frame's first render at the
   // default depth, whose per-group fork requests are compared with its spares

@@ -293,6 +293,13 @@ rtx_status rtx_frame_status(void* scene, int64_t* first_bad, int64_t* bad_frames
  * contexts") — out of *renders calls.  Either pointer may be NULL. */
 rtx_status rtx_overlap_count(void* scene, int64_t* overlapped, int64_t* renders);
 
+/* How many frame contexts the scene's pipelined renders rotate over (a
+ * render waits only for the frame that last used its context: with n
+ * contexts up to n frames are in flight).  The library's choice
+ * (RTX_CONTEXTS overrides, 2..4).  No reference counterpart (an extension
+ * of the pipelining above). */
+rtx_status rtx_frame_contexts(void* scene, int32_t* n);
+
 #ifdef __cplusplus
 }
 #endif
