@@ -677,7 +677,7 @@ __device__ __forceinline__ void advance_fused(LaneRef& LR, const DevScene& S, co
 #define RTX_FUSED_ADV_WAVES RTX_ADV_WAVES
 #endif
 template <bool STATS, bool FORK>
-__global__ void __launch_bounds__(WG, RTX_FUSED_ADV_WAVES)
+__global__ void __launch_bounds__(WG, STATS ? 1 : RTX_FUSED_ADV_WAVES)
     advance_fused_kernel(DevScene S, const DevScene* __restrict__ Sg, const FrameParams* __restrict__ Fp, LaneMem lm,
                          double* __restrict__ sbuf, RtxHitRecord* __restrict__ hits, double* __restrict__ pbuf,
                          int pend_cap, QList q0, QList q1, unsigned int* __restrict__ counters,
