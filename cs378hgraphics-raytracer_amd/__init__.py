@@ -414,7 +414,7 @@ class DeviceScene:
         return a.value, b.value
 
     def frame_contexts(self):
-        """How many frame contexts pipelined renders rotate over (rtx_frame_contexts)."""
+        """How many frame contexts the last render rotated over (rtx_frame_contexts; 1: not pipelined)."""
         lib = hip_lib()
         n = C.c_int32()
         _check(lib.rtx_frame_contexts(self._s, C.byref(n)), lib, "rtx_frame_contexts")

@@ -2648,11 +2648,14 @@ struct SceneState {
   int picks_res = -1;
   FrameCtx cx[4];
   unsigned int next_cx = 0;
-  // frame contexts pipelined renders rotate over (RTX_CONTEXTS 2..4): 3 —
-  // a frame's latency-bound tail then overlaps the next two frames' first
-  // iterations (8-way headline shard 4.78-4.87 vs 5.08-5.09 ms with 2, C4's
-  // 6.12-6.17 vs 6.35-6.40; 4 contexts no better: profiles/r05v_ab_contexts.txt)
+  // frame contexts pipelined renders rotate over (RTX_CONTEXTS 2..4): 3 on
+  // frames of at most 10 M work units — a frame's latency-bound tail then
+  // overlaps the next two frames' first iterations (8-way headline shard
+  // 4.78-4.87 vs 5.08-5.09 ms with 2, C4's 6.12-6.17 vs 6.35-6.40; 4
+  // contexts no better: profiles/r05v_ab_contexts.txt) — 2 on larger ones
+  // (a 2-way shard's third set of buffers would take it from 31 to 47 GiB)
   unsigned int n_cx = 3;
+  unsigned int last_ncx = 1;  // contexts the last render rotated over (1: not pipelined)
   bool any_recur = true;  // some material reflects or refracts (no: no ray tree, no buckets)
   // Pinned staging for the frame's host-to-device copies (frame record,
   // scene record, DoF offsets).  A hipMemcpyAsync from pageable memory may
@@ -2995,7 +2998,7 @@ rtx_status rtx_overlap_count(void* scene, int64_t* overlapped, int64_t* renders)
 
 rtx_status rtx_frame_contexts(void* scene, int32_t* n) {
   if (!scene || !n) return RTX_ERR_INVALID;
-  *n = static_cast<int32_t>(static_cast<SceneState*>(scene)->n_cx);
+  *n = static_cast<int32_t>(static_cast<SceneState*>(scene)->last_ncx);
   return RTX_OK;
 }
 
@@ -3213,7 +3216,9 @@ static rtx_status render_once(SceneState* st, const RtxRenderParams* params, uin
   const bool pipelined = !(pipe_env && atoi(pipe_env) == 0) && device_ptrs && !hits && !stats &&
                          params->aa_mode != RTX_AA_ADAPTIVE && !(mk_env0 && atoi(mk_env0) != 0) &&
                          units0 <= pipe_max;
-  FrameCtx* X = pipelined ? &st->cx[(st->next_cx++) % st->n_cx] : &st->cx[0];
+  const unsigned int ncx = units0 <= 10000000 ? st->n_cx : std::min(st->n_cx, 2u);
+  FrameCtx* X = pipelined ? &st->cx[(st->next_cx++) % ncx] : &st->cx[0];
+  st->last_ncx = pipelined ? ncx : 1u;
   if (!retry) {
     ++st->n_renders;
     if (pipelined) ++st->n_pipelined;

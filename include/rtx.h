@@ -293,11 +293,12 @@ rtx_status rtx_frame_status(void* scene, int64_t* first_bad, int64_t* bad_frames
  * contexts") — out of *renders calls.  Either pointer may be NULL. */
 rtx_status rtx_overlap_count(void* scene, int64_t* overlapped, int64_t* renders);
 
-/* How many frame contexts the scene's pipelined renders rotate over (a
- * render waits only for the frame that last used its context: with n
- * contexts up to n frames are in flight).  The library's choice
- * (RTX_CONTEXTS overrides, 2..4).  No reference counterpart (an extension
- * of the pipelining above). */
+/* How many frame contexts the scene's last render rotated over (a
+ * pipelined render waits only for the frame that last used its context:
+ * with n contexts up to n frames are in flight; 1: the render was not
+ * pipelined).  The library's choice: 3 for frames of at most 10 M work
+ * units, 2 above (RTX_CONTEXTS caps it, 2..4).  No reference counterpart
+ * (an extension of the pipelining above). */
 rtx_status rtx_frame_contexts(void* scene, int32_t* n);
 
 #ifdef __cplusplus
