@@ -364,6 +364,11 @@ def test_wrong_frame_never_ok(pkg, capfd, monkeypatch, knob):
     render such a frame again and return the right image; an asynchronous
     (device-buffer) render is reported by rtx_frame_status, naming the frame,
     and the frame's next render is right (rtx_render, collect_check)."""
+    # (the knobs force what only the default machine has: two-entry stacks
+    # are the fused machine's, bucket pools the forks'; tools/robust_suite.sh
+    # runs this file with those switched off too)
+    if os.environ.get("RTX_FORK") == "0" or (knob == "low_stack" and os.environ.get("RTX_FUSE") == "0"):
+        pytest.skip("no two-entry stacks / bucket pool in this mode")
     path = scene_path("trimesh2_glass.ray")
     opts = pkg.RenderOptions.from_cli("-w 64 -r 5 -O r -A 2".split())
     host = pkg.HostScene(path)
@@ -414,6 +419,8 @@ def test_fork_depth_from_history(pkg, orc, capfd, monkeypatch):
     CPU restatement."""
     import ctypes as C
 
+    if os.environ.get("RTX_FORK") == "0" or os.environ.get("RTX_FORK_DEPTH") or os.environ.get("RTX_FUSE") == "0":
+        pytest.skip("no forks / a fixed fork depth / the sequential machine (its own fork counts) in this mode")
     monkeypatch.setenv("RTX_DEBUG", "1")
     scene, flags = "trimesh2_glass.ray", "-w 64 -r 5 -O r -A 4"
     path = scene_path(scene)
@@ -457,6 +464,8 @@ def test_fork_depth_from_history(pkg, orc, capfd, monkeypatch):
 def test_fork_depth_first_render_is_depth3(pkg, capfd, monkeypatch):
     """The first render of a frame whose forks outgrow the spares is itself
     the depth-3 image: equal, in f64, to a render with RTX_FORK_DEPTH=3."""
+    if os.environ.get("RTX_FORK") == "0" or os.environ.get("RTX_FORK_DEPTH") or os.environ.get("RTX_FUSE") == "0":
+        pytest.skip("no forks / a fixed fork depth / the sequential machine (its own fork counts) in this mode")
     scene, flags = "trimesh2_glass.ray", "-w 64 -r 5 -O r -A 4"
     opts = pkg.RenderOptions.from_cli(flags.split())
     a = pkg.DeviceScene(pkg.HostScene(scene_path(scene)), 0).render(opts, want_f64=True)
