@@ -132,16 +132,19 @@ def host_cpu():
     return model, ncpu, aff, quota, share
 
 
-def cpu_baseline(pkg, path, opts, height, budget_s=10.0, repeats=3):
+def cpu_baseline(pkg, path, opts, height, budget_s=10.0, repeats=3, o0=False):
     """Time the CPU restatement (oracle/, OpenMP over pixels, every core this
     job may use) on the same frame: the whole frame when one render fits in
     ~budget_s of CPU time (median of 3 full renders), else row
     bands spread over the image with the band height calibrated to ~budget_s;
-    the median of `repeats` runs is reported."""
+    the median of `repeats` runs is reported.  o0: the restatement built at
+    the reference's own -O0 (ray/cmake/env.cmake:9) — BASELINE.md's labelled
+    context row, never the denominator."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle  # test infrastructure: the CPU baseline leg
 
-    if not os.path.exists(oracle.LIB):
+    libp = oracle.LIB_O0 if o0 else oracle.LIB
+    if not os.path.exists(libp):
         oracle.build()
     model, ncpu, aff, quota, share = host_cpu()
     threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or share
@@ -151,12 +154,13 @@ def cpu_baseline(pkg, path, opts, height, budget_s=10.0, repeats=3):
 
     def bands(band):
         if band >= height:  # the whole frame
-            r = oracle.render(pkg, path, opts, threads=threads, want_hits=False)
+            r = oracle.render(pkg, path, opts, threads=threads, want_hits=False, lib_path=libp)
             return r["stats"]["rays"], r["stats"]["kernel_ms"] * 1e-3
         rays, secs = 0, 0.0
         for yc in y_centres:
             y0 = max(0, min(height - band, yc - band // 2))
-            r = oracle.render(pkg, path, opts, rect=(0, y0, w, y0 + band), threads=threads, want_hits=False)
+            r = oracle.render(pkg, path, opts, rect=(0, y0, w, y0 + band), threads=threads, want_hits=False,
+                              lib_path=libp)
             secs += r["stats"]["kernel_ms"] * 1e-3  # render loop only, parse excluded
             rays += r["stats"]["rays"]
         return rays, secs
@@ -181,7 +185,8 @@ def cpu_baseline(pkg, path, opts, height, budget_s=10.0, repeats=3):
             "runs_mrays_s": [round(x, 3) for x in rates], "full_frame": band >= height,
             "spread": round((rates[-1] - rates[0]) / med, 4),
             "omp": {"proc_bind": os.environ.get("OMP_PROC_BIND"), "places": os.environ.get("OMP_PLACES")},
-            "sample": f"CPU restatement (oracle/, g++ -O2, OpenMP {threads} threads) on {what}, median of {repeats} runs",
+            "sample": (f"CPU restatement (oracle/, g++ {'-O0, the reference build flags (ray/cmake/env.cmake:9): a context row, never the denominator' if o0 else '-O2'}, "
+                       f"OpenMP {threads} threads) on {what}, median of {repeats} runs"),
             "_band": band, "_threads": threads}
 
 
@@ -580,10 +585,14 @@ def main():
         kernels = st.get("kernels") or {}
         for w in kernels.values():
             w["algorithmic_bytes"] = kernel_bytes(w)
-        cpu, parity = None, None
+        cpu, parity, cpu_o0 = None, None, None
         if not args.no_cpu and world == 1:
             cpu = cpu_baseline(pkg, args.scene, opts, height, args.cpu_budget)
             band, threads = cpu.pop("_band"), cpu.pop("_threads")
+            # BASELINE.md's optional context row: the restatement at the
+            # reference's -O0, a bounded sample (a few row bands), one run
+            cpu_o0 = cpu_baseline(pkg, args.scene, opts, height, min(args.cpu_budget, 5.0), repeats=1, o0=True)
+            cpu_o0.pop("_band"), cpu_o0.pop("_threads")
             if not args.no_parity:
                 parity = parity_block(pkg, dev, args.scene, opts, height, band, threads, timed_rgb8)
         line = {
@@ -615,6 +624,7 @@ def main():
                          "launches_per_frame": launches_per_frame,
                          "algorithmic_bytes_per_launch": algo_bytes},
             "cpu_baseline": cpu,
+            "cpu_baseline_O0": cpu_o0,
             # the timed frame against the CPU restatement (tests/parity.py bar)
             "parity": parity,
             # traversal work of one frame (the counting pass of the same kernels)

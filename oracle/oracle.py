@@ -16,9 +16,10 @@ import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB = os.path.join(HERE, "_build", "liboracle.so")
+LIB_O0 = os.path.join(HERE, "_build", "liboracle_O0.so")  # the reference's -O0 (bench context row)
 CLI = os.path.join(HERE, "_build", "ray_oracle")
 
-_lib = None
+_libs = {}
 
 
 def build(quiet: bool = True):
@@ -30,14 +31,14 @@ class OracleRect(C.Structure):
                 ("threads", C.c_int32)]
 
 
-def lib(pkg):
-    """Load liboracle.so; `pkg` is the loaded cs378hgraphics-raytracer_amd
-    module (for the shared struct definitions of rtx.h)."""
-    global _lib
-    if _lib is None:
-        if not os.path.exists(LIB):
+def lib(pkg, path: str = LIB):
+    """Load liboracle.so (or its -O0 build, LIB_O0); `pkg` is the loaded
+    cs378hgraphics-raytracer_amd module (for the shared struct definitions of
+    rtx.h)."""
+    if path not in _libs:
+        if not os.path.exists(path):
             build()
-        L = C.CDLL(LIB)
+        L = C.CDLL(path)
         L.oracle_last_error.restype = C.c_char_p
         L.oracle_aspect.restype = C.c_double
         L.oracle_aspect.argtypes = [C.c_char_p]
@@ -52,8 +53,8 @@ def lib(pkg):
                                          C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]
         for fn in (L.oracle_raw_records, L.oracle_tokens):
             fn.argtypes = [C.c_char_p, C.c_char_p, C.c_int64, C.POINTER(C.c_int64)]
-        _lib = L
-    return _lib
+        _libs[path] = L
+    return _libs[path]
 
 
 def _text(fn, path: str) -> str:
@@ -107,10 +108,11 @@ def height_for(pkg, path: str, width: int) -> int:
     return int(width / a + 0.5)
 
 
-def render(pkg, path: str, opts, rect=None, threads: int = 0, want_hits: bool = True):
+def render(pkg, path: str, opts, rect=None, threads: int = 0, want_hits: bool = True, lib_path: str = LIB):
     """Render with the restatement.  Returns dict(rgb8, rgb, hits, stats) in
-    the same layout as DeviceScene.render (full frame)."""
-    L = lib(pkg)
+    the same layout as DeviceScene.render (full frame).  lib_path: LIB_O0 for
+    the -O0 build."""
+    L = lib(pkg, lib_path)
     h = height_for(pkg, path, opts.width)
     p = opts.params(h)
     w = opts.width

@@ -406,3 +406,16 @@ def test_kat_per_vertex_materials(pkg, orc):
     rgb = r["rgb"][hit]
     assert np.abs(rgb.sum(axis=1) - 1.0).max() < 1e-12  # barycentric weights sum to 1
     assert (rgb >= -1e-12).all()
+
+
+def test_oracle_O0_build_equals_O2(pkg, orc):
+    """bench.py's -O0 context row times the restatement built at the
+    reference's own optimisation level (ray/cmake/env.cmake:9): the same
+    arithmetic (-ffp-contract=off, SSE2 doubles), so the same image and the
+    same ray counts as the -O2 checker."""
+    path = scene_path("hitchcock.ray")
+    opts = cli_opts(pkg, "-w 48 -r 3 -O r -A 2")
+    a = orc.render(pkg, path, opts, want_hits=False)
+    b = orc.render(pkg, path, opts, want_hits=False, lib_path=orc.LIB_O0)
+    assert np.array_equal(a["rgb"], b["rgb"])
+    assert a["stats"]["rays"] == b["stats"]["rays"]
