@@ -36,10 +36,10 @@ import time
 _AFFINITY0 = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
 os.environ.setdefault("OMP_PROC_BIND", "close")
 os.environ.setdefault("OMP_PLACES", "cores")
-# Consecutive frames overlap on the scene's two frame contexts, each with its
-# slot groups on streams of its own (rtx_render, DESIGN.md "Frame
-# contexts"): with HIP's default of 4 hardware queues per process, the 2 x 3
-# group streams share queues and frame k + 1 queues behind frame k's tail
+# Consecutive frames overlap on the scene's frame contexts (three on frames
+# of at most 10 M units, two above), each with its slot groups on streams of
+# its own (rtx_render, DESIGN.md "Frame contexts"): with HIP's default of 4
+# hardware queues per process, the contexts' group streams share queues and frame k + 1 queues behind frame k's tail
 # (kernel trace, profiles/r04i_timeline_q4.txt).  The environment may hold the
 # default explicitly (the GPU box does), so a lower value is raised.  Read
 # when HIP initialises.
@@ -643,8 +643,9 @@ def main():
             # throughput, frame_latency_ms one frame rendered alone (render
             # + gather, max over ranks)
             "frame_latency_ms": round(frame_latency_ms, 3),
-            # timed frames that ran pipelined on the two frame contexts
-            # (rtx_overlap_count), and the frame check of the timed frames
+            # timed frames that ran pipelined on the frame contexts (how many
+            # contexts: rtx_frame_contexts; rtx_overlap_count), and the frame
+            # check of the timed frames
             # (rtx_frame_status: first wrong frame, wrong frames)
             "frame_contexts": n_ctx if pipelined == renders and renders > 0 else (1 if pipelined == 0 else "mixed"),
             "pipelined_frames": [pipelined, renders],

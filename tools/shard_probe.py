@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Per-rank frame time of the tile-sharded headline frame, measured on ONE
-GPU (back-to-back frames, which overlap on the scene's two frame contexts,
+GPU (back-to-back frames, which overlap on the scene's frame contexts,
 and one frame alone): rank r of N renders tiles t % N == r (what bench.py --gpus N runs on
 each GPU).  The slowest shard's time bounds the N-GPU frame (plus the RCCL
 gather of a few MB).  Prints one JSON line per N.
