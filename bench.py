@@ -532,9 +532,12 @@ def main():
     value = frame_rays * args.steps / elapsed / 1e6
 
     if rank == 0:
-        # the default wavefront path renders a frame as ~80 iterations of
-        # advance_kernel + trace_kernel<closest> + trace_kernel<next> on 3
-        # streams, so the roofline is priced per frame: algorithmic bytes of
+        # the default wavefront path renders a frame as a few dozen iterations
+        # of advance_fused_kernel + trace_kernel<closest, fused> (closest hit +
+        # shading) + trace_kernel<next, fused> (whole shadow walks) on 3
+        # streams, then tail_fused_kernel and reduce_kernel (launches_per_frame:
+        # the library's count of its kernel launches, rtx_kernel_time), so the
+        # roofline is priced per frame: algorithmic bytes of
         # one frame / GPU time of one frame (the event pair around the K
         # timed frames on the render stream, / K; frame_span_ms is one
         # frame's own span, rtx_kernel_time, which overlaps the frames
@@ -618,8 +621,11 @@ def main():
                          "simd_cycles_per_s": SIMD_CYCLES_PER_S,
                          "traffic_source": traffic_src,
                          "kernel": ("render_kernel<false,false> (megakernel, 1 launch per frame)" if mega else
-                                    "frame: advance_kernel + trace_kernel<false,1|2> iterations on 3 streams, "
-                                    "GPU time = HIP events on the render stream around the K frames / K"),
+                                    "frame: trace_kernel<false,1,true,*,true> (first camera rays), then "
+                                    "advance_fused_kernel + trace_kernel<false,1,true,*> (closest hit + shading) + "
+                                    "trace_kernel<false,2,true> (shadow walks) iterations on 3 streams, "
+                                    "tail_fused_kernel, reduce_kernel; GPU time = HIP events on the render stream "
+                                    "around the K frames / K"),
                          "avg_kernel_ms": round(avg_kernel_ms, 3), "frame_span_ms": round(frame_span_ms, 3),
                          "launches_per_frame": launches_per_frame,
                          "algorithmic_bytes_per_launch": algo_bytes},

@@ -37,9 +37,6 @@
 #define RTX_MESH_TREE 1
 #define RTX_MESH_NORMALS 2
 #define RTX_MESH_VMATS 4
-// MFLAGS bit 8 (any object type): M^-1 is exactly the identity (rows 0..2 of
-// inv are (1 0 0 0), (0 1 0 0), (0 0 1 0)) — obj_local's shortcut
-#define RTX_OBJ_IDENT 256
 
 namespace rtxd {
 
@@ -118,19 +115,9 @@ struct TMeta {
   int32_t rank, leaf;
 };
 
-// A traversal face as floats for tri_pre (the conservative prefilter of
-// tri_hit): the three vertices rounded to nearest, and in the w slots the
-// face's reference rank (a: int bits) and reference leaf node (b: int bits,
-// a global mnodes index) — one 48-byte burst per face instead of TMeta plus
-// the 96-byte double face.
-struct FaceF {
-  float4 a, b, c;
-};
-
 struct DevScene {
   const DevNode4* snode4;  // scene BVH records
   const DevNode4* mnode4;  // all mesh BVHs' records (global indices)
-  const DevNode4* mhot;    // mesh records [0, n_mhot): a copy in LDS where a kernel stages one (else = mnode4)
   const DevRoot* mroots;   // per mesh (valid when meshes[m].node_count > 0)
   DevRoot sroot;           // scene BVH root
   const RtxNode* snodes;
@@ -144,8 +131,6 @@ struct DevScene {
   const RtxFace* tfaces;   // faces in traversal-tree leaf order (per mesh)
   const int32_t* trank;    // reference rank (index in faces) of each tfaces entry
   const TMeta* tmeta;      // rank + reference leaf node of each tfaces entry
-  const FaceF* tfacef;     // tfaces as floats (+ rank, leaf) for tri_pre
-  float mext;              // every mesh-local vertex coordinate has |x| <= mext (rounded up)
   const double* vnormals;
   const RtxVertexMaterial* vmats;
   const RtxLight* lights;
@@ -153,7 +138,7 @@ struct DevScene {
   const uint8_t* texels;
   const double* picks;   // area-light sample positions [light][ss_res][3]
   int32_t n_snodes, n_objs, n_lights, ss_res;
-  int32_t n_srec, n_mhot;  // scene-tree records; hot mesh records (mesh roots first)
+  int32_t n_srec;        // scene-tree records
   double margin;         // world-space pruning slack
   double lmargin;        // mesh-local pruning slack
   double cos45;          // glm::cos(PI / 4) computed on the host (light.cpp:145)
@@ -199,24 +184,9 @@ __host__ __device__ __forceinline__ bool cone_good(const double* prm, const dvec
 }
 
 // Geometry::intersect's ray into the object frame (scene.cpp:17-19): pos =
-// M^-1 (p, 1), dir = M^-1 (p + d, 1) - pos (not yet normalised).  For an
-// identity M^-1 (RTX_OBJ_IDENT) glm's pairing (c0 x + c1 y) + (c2 z + c3 w)
-// gives x for x != 0 and +0 for x = +-0 (for finite coordinates: the 0 * y
-// and 0 * z products are +-0, the translation term +0), which is x + 0.0
-// exactly, so the shortcut is bit-identical to the full product — and skips
-// its 42 FP64 multiplies and adds on every object step of such scenes (every
-// object of the trimesh2 stand-ins).  Opt-in (-DRTX_IDENT): measured slower
-// on the headline frame, 34.0-34.1 vs 33.1 ms (profiles/r05e_ab_ident_early.txt;
-// the kernels are not FP64-issue-bound, and the extra branch cost more).
+// M^-1 (p, 1), dir = M^-1 (p + d, 1) - pos (not yet normalised).  (A
+// shortcut for identity transforms measured slower: DESIGN.md §8, round 5.)
 RT_HD void obj_local(const RtxObject& o, const dvec3& P, const dvec3& D, dvec3& pos, dvec3& dir) {
-#ifdef RTX_IDENT
-  if (o.pad[RTX_OBJ_MFLAGS] & RTX_OBJ_IDENT) {
-    pos = mk3(P.x + 0.0, P.y + 0.0, P.z + 0.0);
-    const dvec3 s = P + D;
-    dir = mk3(s.x + 0.0, s.y + 0.0, s.z + 0.0) - pos;
-    return;
-  }
-#endif
   pos = rtm::xform_point(o.inv, P);
   dir = rtm::xform_point(o.inv, P + D) - pos;
 }
@@ -432,32 +402,6 @@ RT_HD bool box_cons32(const DevNode4& nd, int k, const RayF& r, float& a, float&
   return box_cons32v(nd.lo[0][k], nd.lo[1][k], nd.lo[2][k], nd.hi[0][k], nd.hi[1][k], nd.hi[2][k], r, a, b);
 }
 
-// box_cons32 for entries 2p and 2p + 1 at once: the slab arithmetic on
-// float pairs (packed v_pk_add_f32 / v_pk_mul_f32 on gfx950), the same
-// operations element by element.  Returns the pair's (a, b); the caller
-// applies the hit rule !(a > b) && !(b < 0).
-typedef float rtx_f2 __attribute__((ext_vector_type(2)));
-RT_HD void box_cons32x2(const DevNode4& nd, int p, const RayF& r, rtx_f2& a, rtx_f2& b) {
-  rtx_f2 tmin, tmax;
-#pragma unroll
-  for (int q = 0; q < 3; ++q) {
-    const rtx_f2 lo = {nd.lo[q][2 * p], nd.lo[q][2 * p + 1]};
-    const rtx_f2 hi = {nd.hi[q][2 * p], nd.hi[q][2 * p + 1]};
-    const rtx_f2 t1 = (lo - r.olo[q]) * r.inv[q];
-    const rtx_f2 t2 = (hi - r.ohi[q]) * r.inv[q];
-    const rtx_f2 n = __builtin_elementwise_min(t1, t2), f = __builtin_elementwise_max(t1, t2);
-    tmin = q == 0 ? n : __builtin_elementwise_max(tmin, n);
-    tmax = q == 0 ? f : __builtin_elementwise_min(tmax, f);
-  }
-  const rtx_f2 err = {r.err, r.err};
-  a = tmin - (err + __builtin_elementwise_abs(tmin) * 0x1p-21f);
-  b = tmax + (err + __builtin_elementwise_abs(tmax) * 0x1p-21f);
-#pragma unroll
-  for (int e = 0; e < 2; ++e) {  // inf - inf: the infinite bound itself (see box_cons32)
-    if (!(a[e] == a[e])) a[e] = tmin[e];
-    if (!(b[e] == b[e])) b[e] = tmax[e];
-  }
-}
 
 // ------------------------------------------------------------------ textures
 // TextureMap::getMappedValue / getPixelAt (material.cpp:84-138)
@@ -608,82 +552,6 @@ RT_HD bool tri_hit(const RtxFace& F, const dvec3& p, const dvec3& d, double tcap
   const double faceArea = rtm::dot(rtm::cross(v1 - v0, v2 - v0), n);
   if (faceArea < RTX_EPS32 && faceArea > -RTX_EPS32) return false;
   tOut = t;
-  return true;
-}
-
-// ---- conservative float prefilter of tri_hit (tri_pre)
-// tri_hit (TrimeshFace::intersectLocal, trimesh.cpp:119-156) accepts a face
-// only if t = ((v0 - p).n) / (n.d) lies in [eps, tcap] and every edge value
-// e_k = ((v_k+1 - v_k) x (P - v_k)).n, P = p + t d, is >= eps > 0.  With
-// A = v0 - p, B = v1 - p, C = v2 - p and the plane's normal n = N/|N|,
-// N = (B - A) x (C - A) (the reference's face normal, up to its rounding):
-//   e_0 = V_0 / s, e_1 = V_1 / s, e_2 = V_2 / s  with  V_0 = (A x B).d,
-//   V_1 = (B x C).d, V_2 = (C x A).d and s = n.d (det(A, B, P - p) =
-//   (A.n) e_0 and P - p = t d), and V_0 + V_1 + V_2 = N.d, A.N = det(A, B, C),
-//   so t = det(A, B, C) / (V_0 + V_1 + V_2).
-// So tri_hit can only accept when the three V_k share the sign of s, and then
-// only when t = D / sum(V) >= 0 and <= tcap.  tri_pre evaluates V_k and D in
-// float from the float vertices and the float ray with explicit bounds of
-// the float error (below) and reports "certainly rejected" only when two V_k
-// have opposite signs beyond their bounds, or all share a sign beyond them
-// and t is then certainly < 0 or > tcap.  Every other face — near an edge,
-// near-parallel, NaN or infinite anywhere — goes to the exact FP64 tri_hit,
-// so the set of faces the walk answers with is unchanged (the double
-// computation's own rounding, relative 2^-52, is far inside the bounds).
-// Error bounds (u = 2^-24; R = mext + max|p| bounds every |A|, |B|, |C|;
-// M = the face's max |A|, |B|, |C| component, eI = 2.01 u R the error of one
-// component of fl(fl(v) - fl(p)); |d| = 1): one component of a x b is off
-// by <= 4 M eI + 4 u M^2, a V by <= 7 M eI + 23 u M^2, D = a.(b x c) by
-// <= 18 M^2 eI + 28 u M^3 — tri_pre uses twice those (tests/
-// test_record_test_host.py checks it against exact rational arithmetic).
-struct RayTF {
-  float px, py, pz, dx, dy, dz;
-  float r;  // mext + max |p|, rounded up
-};
-RT_HD RayTF ray_tf(const dvec3& p, const dvec3& d, float mext) {
-  RayTF r;
-  r.px = static_cast<float>(p.x);
-  r.py = static_cast<float>(p.y);
-  r.pz = static_cast<float>(p.z);
-  r.dx = static_cast<float>(d.x);
-  r.dy = static_cast<float>(d.y);
-  r.dz = static_cast<float>(d.z);
-  const float pm = fmaxf(fmaxf(fabsf(r.px), fabsf(r.py)), fabsf(r.pz));
-  r.r = (mext + pm) * (1.0f + 0x1p-20f);
-  return r;
-}
-// false: tri_hit(face, p, d, tcap) certainly returns false.  tcap_up >= tcap.
-RT_HD bool tri_pre(const float4& fa, const float4& fb, const float4& fc, const RayTF& r, float tcap_up) {
-  const float ax = fa.x - r.px, ay = fa.y - r.py, az = fa.z - r.pz;
-  const float bx = fb.x - r.px, by = fb.y - r.py, bz = fb.z - r.pz;
-  const float cx = fc.x - r.px, cy = fc.y - r.py, cz = fc.z - r.pz;
-  // a x b, b x c, c x a
-  const float abx = ay * bz - az * by, aby = az * bx - ax * bz, abz = ax * by - ay * bx;
-  const float bcx = by * cz - bz * cy, bcy = bz * cx - bx * cz, bcz = bx * cy - by * cx;
-  const float cax = cy * az - cz * ay, cay = cz * ax - cx * az, caz = cx * ay - cy * ax;
-  const float v0 = (abx * r.dx + aby * r.dy) + abz * r.dz;
-  const float v1 = (bcx * r.dx + bcy * r.dy) + bcz * r.dz;
-  const float v2 = (cax * r.dx + cay * r.dy) + caz * r.dz;
-  const float m = fmaxf(fmaxf(fmaxf(fabsf(ax), fabsf(ay)), fmaxf(fabsf(az), fabsf(bx))),
-                        fmaxf(fmaxf(fmaxf(fabsf(by), fabsf(bz)), fmaxf(fabsf(cx), fabsf(cy))), fabsf(cz)));
-  const float u = 0x1p-24f;
-  const float eI = 2.01f * u * r.r;
-  const float eV = (2.0f * (7.0f * m * eI + 23.0f * u * m * m)) * (1.0f + 0x1p-20f);
-  // opposite signs beyond the bounds: an edge rejects
-  const bool pos = v0 > eV || v1 > eV || v2 > eV;
-  const bool neg = v0 < -eV || v1 < -eV || v2 < -eV;
-  if (pos && neg) return false;
-  // one sign beyond the bounds everywhere: t = D / sum(V) against [0, tcap]
-  const bool all_pos = v0 > eV && v1 > eV && v2 > eV;
-  const bool all_neg = v0 < -eV && v1 < -eV && v2 < -eV;
-  if (all_pos || all_neg) {
-    const float dd = (ax * bcx + ay * bcy) + az * bcz;  // det(a, b, c)
-    const float eD = (2.0f * (18.0f * m * m * eI + 28.0f * u * m * m * m)) * (1.0f + 0x1p-20f);
-    const float sd = all_pos ? dd : -dd;          // sign(sum V) * D
-    const float ssum = fabsf(v0) + fabsf(v1) + fabsf(v2);
-    if (sd < -eD) return false;                   // t < 0
-    if ((sd - eD) * (1.0f - 0x1p-20f) > tcap_up * ((ssum + 3.0f * eV) * (1.0f + 0x1p-20f))) return false;  // t > tcap
-  }
   return true;
 }
 

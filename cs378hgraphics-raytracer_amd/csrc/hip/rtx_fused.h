@@ -118,15 +118,6 @@ __device__ __forceinline__ bool walk_hit(const DevScene& S, const RtxLight& L, c
   return false;
 }
 
-#ifdef RTX_WALK_OOL
-// Opt-in: walk_hit out of line in the walk kernel (its resolve_hit and
-// material lookups off the kernel's register peak).  Measured 47.1-47.3 vs
-// 45.7 ms on the headline frame (the call's frame and saves cost more).
-__device__ __noinline__ bool walk_hit_ool(const DevScene* Sg, int li, const dvec3 pb, const dvec3 sdir, bool have,
-                                          double bt, int bobj, int bsub, WalkState* w, dvec3* res) {
-  return walk_hit(*Sg, Sg->lights[li], pb, sdir, have, bt, bobj, bsub, *w, *res);
-}
-#endif
 
 // the group's next-hit list and its append counter
 struct WalkEmit {
@@ -566,9 +557,7 @@ __device__ __forceinline__ void advance_fused(LaneRef& LR, const DevScene& S, co
   const RtxRenderParams& P = F.P;
   LR.qmode() = Q_NONE;
   while (LR.st() != ST_IDLE && LR.qmode() == Q_NONE) {
-#ifndef RTX_FUSED_NOREFRESH
     LR.refresh();
-#endif
     switch (LR.st()) {
       case ST_CAM: {
         // next camera ray of trace(x, y) (RayTracer.cpp:35-79)
@@ -831,8 +820,7 @@ __global__ void __launch_bounds__(WG) tail_fused_kernel(DevScene S, const DevSce
         rp = -1;
         sq = -1;
       }
-      double qblk;
-      shadow_bounds(SS, SS.lights[wl], pb, rp < 0, qlim, qblk);
+      qlim = shadow_limit(SS, SS.lights[wl], pb, rp < 0);
       qm = Q_NEXT;
       qP = pb;
       qD = sdir;

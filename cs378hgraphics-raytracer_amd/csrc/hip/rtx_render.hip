@@ -40,10 +40,7 @@ using rtm::dvec2;
 using rtm::dvec3;
 using rtm::mk3;
 
-#ifndef RTX_WG
-#define RTX_WG 256  // threads per workgroup (A/B: -DRTX_WG=64 / 128)
-#endif
-#define WG RTX_WG
+#define WG 256  // threads per workgroup (64 / 128 measured within noise)
 #define WAVES_PER_WG (WG / 64)
 // -r limit: the pending-ray stack holds depth + 2 entries per slot in HBM
 // and the slot pool shrinks to fit device memory, so this only bounds the
@@ -206,11 +203,7 @@ struct HitRef {
 // the frame took 130.1 ms instead of 127.8.  The kernels pass S as *Sg (the
 // device copy), so an out-of-line call never has to spill the by-value
 // kernel-argument copy.
-#ifdef RTX_RESOLVE_NOINLINE
-#define RTX_RESOLVE_ATTR __noinline__
-#else
 #define RTX_RESOLVE_ATTR __forceinline__
-#endif
 __device__ RTX_RESOLVE_ATTR HitRef resolve_hit(const DevScene& S, const dvec3& P, const dvec3& D, int oi, int sub,
                               int* rec_face, int* rec_mleaf) {
   HitRef r;
@@ -367,19 +360,10 @@ __device__ __forceinline__ double light_dist_atten(const RtxLight& L, const dvec
 //     the U14 limit check trips past the light, and for the walk's FIRST hit
 //     already past half the light distance (the double advance puts its
 //     check point at twice the hit distance, light.cpp:38,66).
-//   tblk: below it the point-light limit check cannot trip, so a blocker
-//     there ends the walk with 0 (directional lights never trip it).
-__device__ __forceinline__ void shadow_bounds(const DevScene& S, const RtxLight& L, const dvec3& qP, bool first,
-                                              double& tlim, double& tblk) {
-  tlim = RTX_INF;
-  tblk = -RTX_INF;
-  if (L.type == RTX_LIGHT_POINT) {
-    const double dl = rtm::distance(qP, ld3(L.pos));
-    tlim = (first ? 0.5 * dl : dl) * (1.0 + 1e-6) + S.margin;
-    tblk = 0.5 * dl * (1.0 - 1e-6) - S.margin;
-  } else if (L.type == RTX_LIGHT_DIRECTIONAL) {
-    tblk = RTX_INF;
-  }
+__device__ __forceinline__ double shadow_limit(const DevScene& S, const RtxLight& L, const dvec3& qP, bool first) {
+  if (L.type != RTX_LIGHT_POINT) return RTX_INF;
+  const double dl = rtm::distance(qP, ld3(L.pos));
+  return (first ? 0.5 * dl : dl) * (1.0 + 1e-6) + S.margin;
 }
 
 // ============================================================ lane state machine
@@ -507,22 +491,20 @@ __device__ __forceinline__ void lane_clear(const LaneMem& m, size_t g) {
 }
 
 // The ray of a lane's pending next-hit query: the shadow walk's (from the
-// backed-up shading point toward the light, bounded by the light, with the
-// opaque-blocker early-out below tblock) or a discoverMat walk's (every hit
-// of the ray, unbounded, no early-out).
+// backed-up shading point toward the light, bounded by the light) or a
+// discoverMat walk's (every hit of the ray, unbounded).
 template <bool MEDIA>
 __device__ __forceinline__ void next_query_ray(const DevScene& S, const LaneRef& L, dvec3& qP, dvec3& qD,
-                                               double& qlim, double& qblk) {
+                                               double& qlim) {
   if (MEDIA && L.dret() != DISC_NONE) {
     qP = L.dpos();
     qD = L.ddir();
     qlim = RTX_INF;
-    qblk = -RTX_INF;
     return;
   }
   qP = rtm::ray_at(L.rp(), L.rd(), L.st_t()) - L.rd() * RTX_EPS_BACKUP;
   qD = L.sdir();
-  shadow_bounds(S, S.lights[L.li()], qP, L.qrp() < 0, qlim, qblk);
+  qlim = shadow_limit(S, S.lights[L.li()], qP, L.qrp() < 0);
 }
 
 // Scene::discoverMat (scene.cpp:212-237) over the ray (dpos, ddir): its
@@ -893,20 +875,9 @@ __device__ __forceinline__ void advance_lane(LaneRef& LR, const DevScene& S, con
     }
   };
   LR.qmode() = Q_NONE;
-#ifdef RTX_WATCHDOG
-  int wd_steps = 0;
-#endif
   while (LR.st() != ST_IDLE && LR.qmode() == Q_NONE) {
     // the lane state is memory: each step re-reads the few fields it uses
     LR.refresh();
-#ifdef RTX_WATCHDOG
-    if (++wd_steps > 1000000) {
-      printf("rtx watchdog: state loop lane %d st %d dret %d top %d li %d\n", int(glane), LR.st(), LR.dret(), LR.top(),
-             LR.li());
-      LR.st() = ST_IDLE;
-      break;
-    }
-#endif
     switch (LR.st()) {
       case ST_CAM: {
         // next camera ray of trace(x, y) (RayTracer.cpp:35-79)
@@ -1200,9 +1171,6 @@ __device__ __forceinline__ void advance_lane(LaneRef& LR, const DevScene& S, con
         dvec3 result = LR.sattn();
         if (!LR.bhave()) {
           done = true;
-        } else if (LR.bhave() == 2) {  // a blocker below tblock (trace_kernel's shadow early-out)
-          result = mk3(0.0, 0.0, 0.0);
-          done = true;
         } else {
           const double t = LR.bt() - LR.last_t();
           LR.last_t() = LR.bt();
@@ -1314,9 +1282,6 @@ __global__ void __launch_bounds__(WG) render_kernel(DevScene S, const DevScene* 
   LR.st() = ST_IDLE;
   LR.sample_slot() = -1;
 
-#ifdef RTX_WATCHDOG
-  int wd_queries = 0;
-#endif
   // ---- wave-uniform scheduler state
   unsigned long long qnext = 0, qend = 0;
   bool exhausted = false;
@@ -1550,24 +1515,9 @@ __global__ void __launch_bounds__(WG) render_kernel(DevScene S, const DevScene* 
       dvec3 qP = LR.rp(), qD = LR.rd();
       double qlim = RTX_INF;
       if (LR.qmode() == Q_NEXT) {
-        double qblk;
-        next_query_ray<MEDIA>(S, LR, qP, qD, qlim, qblk);
+        next_query_ray<MEDIA>(S, LR, qP, qD, qlim);
       }
       LR.bhave() = traverse<STATS>(S, LR.qmode(), qP, qD, LR.qtp(), LR.qrp(), LR.qsq(), qlim, LR.bt(), LR.bobj(), LR.bsub(), stk, lane, C);
-#ifdef RTX_WATCHDOG
-      // debugging aid (opt-in): report a lane whose sample runs away
-      if (++wd_queries == 200000) {
-        printf("rtx watchdog: lane %d st %d qm %d dret %d dpass %d dpush %d dhead %d dtot %d bt %.17g bobj %d bsub %d "
-               "qtp %.17g qrp %d qsq %d li %d top %d P (%.17g %.17g %.17g) D (%.17g %.17g %.17g)\n",
-               int(glane), LR.st(), LR.qmode(), LR.dret(), LR.dpass(), LR.dpush(), LR.dhead(), LR.dtot(), LR.bt(),
-               LR.bobj(), LR.bsub(), LR.qtp(), LR.qrp(), LR.qsq(), LR.li(), LR.top(), qP.x, qP.y, qP.z, qD.x, qD.y,
-               qD.z);
-      }
-      if (wd_queries >= 200000 && wd_queries < 200012)
-        printf("rtx watchdog: lane %d step st %d qm %d bt %.17g bobj %d bsub %d have %d\n", int(glane), LR.st(),
-               LR.qmode(), LR.bt(), LR.bobj(), LR.bsub(), LR.bhave());
-      if (wd_queries > 200012) LR.st() = ST_IDLE;
-#endif
     }
   }
   if (STATS) {
@@ -1593,11 +1543,11 @@ __global__ void __launch_bounds__(WG) render_kernel(DevScene S, const DevScene* 
 // Samples are dealt to slots statically (sample slot + k * NSLOT).
 struct QList {
   int* slot;    // [cap]
-  double* d;    // Px Py Pz Dx Dy Dz tp tlimit tblock, field-major [QL_D][cap]
+  double* d;    // Px Py Pz Dx Dy Dz tp tlimit, field-major [QL_D][cap]
   int* iv;      // rp, sq  [2][cap]
   size_t cap;
 };
-#define QL_D 9
+#define QL_D 8
 // per-group counters (unsigned ints), each on its own 128-byte line (the
 // appends, claims and liveness atomics of three concurrent groups must not
 // share lines: packed 4 bytes apart the frame took 5% longer):
@@ -1750,11 +1700,10 @@ __global__ void __launch_bounds__(WG, RTX_ADV_WAVES) advance_kernel(DevScene S, 
       const size_t cap = Q.cap;
       const size_t k = base + lane_prefix(mask);
       dvec3 qP = L.rp(), qD = L.rd();
-      double qlim = RTX_INF, qblk = -RTX_INF;
+      double qlim = RTX_INF;
       if (m == Q_NEXT) {
-        next_query_ray<MEDIA>(S, L, qP, qD, qlim, qblk);
+        next_query_ray<MEDIA>(S, L, qP, qD, qlim);
       }
-      Q.d[8 * cap + k] = qblk;
       Q.slot[k] = slot;
       Q.d[0 * cap + k] = qP.x;
       Q.d[1 * cap + k] = qP.y;
@@ -1781,10 +1730,6 @@ __global__ void __launch_bounds__(WG, RTX_ADV_WAVES) advance_kernel(DevScene S, 
   }
 }
 
-#ifndef RTX_TAIL_STEPS
-#define RTX_TAIL_STEPS 8
-#endif
-
 // Tail of a slot group: once few slots are left, each remaining slot runs
 // its own chain — state machine, query, state machine, ... — to the end in
 // one persistent launch (the megakernel's inner loop over the wavefront's
@@ -1810,7 +1755,6 @@ __global__ void __launch_bounds__(WG) tail_kernel(DevScene S, const DevScene* __
   LaneRef L(lm, static_cast<size_t>(slot));
   const unsigned long long t_start = STATS ? __builtin_readcyclecounter() : 0ull;
   int64_t queries = 0;
-#ifndef RTX_TAIL_DECOUPLE
   // one query at a time per wave (each lane waits for its wave's slowest);
   // the decoupled variant below measured slower (8-way shard 31.2 vs 25.8
   // ms, full frame 97 vs 90): its wave executes the state machine for a few
@@ -1828,8 +1772,7 @@ __global__ void __launch_bounds__(WG) tail_kernel(DevScene S, const DevScene* __
       dvec3 qP = L.rp(), qD = L.rd();
       double qlim = RTX_INF;
       if (qm == Q_NEXT) {
-        double qblk;
-        next_query_ray<MEDIA>(S, L, qP, qD, qlim, qblk);
+        next_query_ray<MEDIA>(S, L, qP, qD, qlim);
       }
       double bt;
       int bobj, bsub;
@@ -1841,62 +1784,6 @@ __global__ void __launch_bounds__(WG) tail_kernel(DevScene S, const DevScene* __
       if (STATS) queries++;
     }
   }
-#else
-  // Decoupled lanes: a lane whose query ended advances its state machine to
-  // the next query while its wave-mates keep stepping theirs, in rounds of
-  // RTX_TAIL_STEPS traversal steps, so no lane waits for a wave-mate's long
-  // (grazing) query.
-  const NoBlocker nb;
-  Trav T;
-  bool has_q = false;
-  int qm = Q_NONE;
-  auto put_result = [&]() {
-    L.bt() = T.bt;
-    L.bobj() = T.bobj;
-    L.bsub() = T.bsub;
-    L.bhave() = T.have ? 1 : 0;
-  };
-  for (;;) {
-    if (valid && !has_q) {
-      for (;;) {
-        // the last query's result is in L.bt()/bobj/bsub/bhave
-        L.qmode() = Q_NONE;
-        claim_sample(L, F, hits, slot);
-        if (L.st() == ST_IDLE) {
-          valid = false;
-          break;
-        }
-        advance_lane<STATS, false, MEDIA>(L, *Sg, F, C, sbuf, nullptr, hits, 0, 0, pbuf, lm.n, static_cast<size_t>(slot),
-                                   pend_cap);
-        qm = L.qmode();
-        if (qm == Q_NONE) continue;
-        dvec3 qP = L.rp(), qD = L.rd();
-        double qlim = RTX_INF;
-        if (qm == Q_NEXT) {
-          double qblk;
-          next_query_ray<MEDIA>(S, L, qP, qD, qlim, qblk);
-        }
-        if (STATS) queries++;
-        has_q = qm == Q_CLOSEST
-                    ? trav_init<STATS, Q_CLOSEST>(T, S, qP, qD, L.qtp(), L.qrp(), L.qsq(), qlim, -RTX_INF, C)
-                    : trav_init<STATS, Q_NEXT>(T, S, qP, qD, L.qtp(), L.qrp(), L.qsq(), qlim, -RTX_INF, C);
-        if (has_q) break;
-        put_result();  // answered by the root test: advance again
-      }
-    }
-    if (__ballot(valid) == 0ull) break;
-    for (int k = 0; k < RTX_TAIL_STEPS; ++k) {
-      if (has_q) {
-        const bool done = qm == Q_CLOSEST ? trav_step<STATS, Q_CLOSEST>(T, S, stk, lane, nb, C)
-                                          : trav_step<STATS, Q_NEXT>(T, S, stk, lane, nb, C);
-        if (done) {
-          put_result();
-          has_q = false;
-        }
-      }
-    }
-  }
-#endif
   if (STATS && tid < static_cast<int>(counters[in_cnt])) {  // the slowest chain of the tail (RTX_DEBUG report)
     atomicMax(&stats[6 + 10], static_cast<unsigned long long>(__builtin_readcyclecounter() - t_start));
     atomicMax(&stats[7 + 10], static_cast<unsigned long long>(queries));
@@ -1907,50 +1794,14 @@ __global__ void __launch_bounds__(WG) tail_kernel(DevScene S, const DevScene* __
   }
 }
 
-// Blocker of the shadow early-out (rtx_traverse.h): hit (oi, sb) of the
-// lane's query is entered from outside (N.dir <= 0) an opaque material —
-// the walk's own resolve_hit normal and flags (ST_WALK).  Out of line: run
-// about once per shadow query, and resolve_hit's registers must not raise
-// the traversal loop's peak.  Opt-in (-DRTX_EARLYOUT): it saves 5% of the
-// traversal work on the headline frame but the call (scratch frame, saved
-// registers) cost more than that (205 vs 185 ms/frame).
-__device__ __noinline__ bool shadow_blocks(const DevScene* __restrict__ Sg, const dvec3 P, const dvec3 D, int oi,
-                                           int sb) {
-  const DevScene& S = *Sg;
-  const RtxObject& o = S.objs[oi];
-  const bool vmats = o.type == RTX_OBJ_TRIMESH && (o.pad[RTX_OBJ_MFLAGS] & RTX_MESH_VMATS);  // flags 0 (decision U2)
-  if (!vmats && (S.mats[o.material].flags & RTX_MF_TRANS)) return false;
-  const HitRef R = resolve_hit(S, P, D, oi, sb, nullptr, nullptr);
-  return !(rtm::dot(R.N, D) > 0);
-}
-
-struct ShadowBlocker {
-  const DevScene* Sg;
-  __device__ explicit ShadowBlocker(const DevScene* s) : Sg(s) {}
-  __device__ bool operator()(const Trav& T, int oi, int sb) const { return shadow_blocks(Sg, T.P, T.D, oi, sb); }
-};
-
-// scene trees up to this many records are staged in LDS whole (the host
-// sizes the trace kernels' dynamic LDS with the same rule)
-#define RTX_LDS_SREC 64
-
-// Refill a wave's idle lanes once fewer than RTX_REFILL are still
-// traversing.  Measured on the headline frame (ms/frame): 1 -> 182, 16 -> 197,
-// 40 -> 205, 56 -> 220: mixing a new query into a wave whose other lanes are
-// deep in the tree costs more (divergent nodes and modes) than the idle lanes
-// waste, so by default a wave claims its next 64 queries only when all of its
-// lanes are done (the claims still balance waves against each other).
-#ifndef RTX_REFILL
-#define RTX_REFILL 1
-#endif
-#if RTX_REFILL != 1
-#error "fused walks (trace_kernel FUSED) reset the walk state between claims: RTX_REFILL must be 1"
-#endif
-
 // Persistent traversal of one group's compacted query list.  A wave claims
-// 64 queries at a time (one atomic); lanes whose query ended take the next
-// ones of the claim (ballot + mbcnt) once fewer than RTX_REFILL lanes are
-// still stepping.
+// 64 queries at a time (one atomic) and hands them to its idle lanes (ballot
+// + mbcnt) once every lane's query is done.  Refilling idle lanes earlier
+// (once fewer than 16 / 40 / 56 lanes were still stepping) measured slower
+// (197 / 205 / 220 vs 182 ms/frame at the time): mixing a new query into a
+// wave whose other lanes are deep in the tree costs more (divergent nodes
+// and modes) than the idle lanes waste; the claims still balance waves
+// against each other.  The fused machine relies on it (trav_reset below).
 // FUSED (Q_NEXT on fused frames, rtx_fused.h): the list holds walk records;
 // a lane whose query completes runs the walk's next step (walk_hit) and
 // either queries again from the hit's key or writes the light's term to
@@ -1977,42 +1828,10 @@ __global__ void __launch_bounds__(WG, !FUSED ? RTX_TRACE_WAVES : (MODE == Q_CLOS
   const int wave = threadIdx.x >> 6;
   int* stk = lds_stack + wave * stack_cap * 64;
   const size_t cap = Q.cap;
-  // Opt-in (-DRTX_LDS_STAGE): stage the scene tree's records and the hot
-  // mesh records (every mesh's root and its children) in LDS after the
-  // stacks, so the first steps of every query read LDS instead of L2.
-  // Measured on the headline frame: 90.3 / 91.2 ms staged against 88.5 /
-  // 90.6 ms not — those records already hit in L1/L2, and choosing LDS or
-  // global per record turns every mesh-record load into a generic (flat)
-  // load.  S is this workgroup's view.
-#ifdef RTX_LDS_STAGE
-  {
-    DevNode4* lds_nodes = reinterpret_cast<DevNode4*>(lds_stack + WAVES_PER_WG * stack_cap * 64);
-    const int ns = S.n_srec <= RTX_LDS_SREC ? S.n_srec : 0;
-    const int nm = S.n_mhot;
-    const uint4* srcs = reinterpret_cast<const uint4*>(S.snode4);
-    const uint4* srcm = reinterpret_cast<const uint4*>(S.mnode4);
-    uint4* dst = reinterpret_cast<uint4*>(lds_nodes);
-    const int per_rec = sizeof(DevNode4) / sizeof(uint4);
-    for (int i = threadIdx.x; i < (ns + nm) * per_rec; i += WG)
-      dst[i] = i < ns * per_rec ? srcs[i] : srcm[i - ns * per_rec];
-    __syncthreads();
-    if (ns > 0) S.snode4 = lds_nodes;
-    S.mhot = lds_nodes + ns;
-  }
-#endif
   const bool cam = CAM && FUSED && MODE == Q_CLOSEST && SA.cam_n > 0;  // first iteration: claims + camera rays here
   const unsigned int nq = cam ? static_cast<unsigned int>(SA.cam_n) : counters[CNT_Q + (MODE - 1) * CNT_LINE];
   unsigned int* claim = counters + CNT_CLAIM + (MODE - 1) * CNT_LINE;
 
-#if defined(RTX_EARLYOUT) && RTX_TEAM
-#error "RTX_TEAM: a helper's answer does not carry the early-out's blocked flag"
-#endif
-#ifdef RTX_EARLYOUT
-  using Blk = typename std::conditional<MODE == Q_NEXT, ShadowBlocker, NoBlocker>::type;
-#else
-  using Blk = NoBlocker;
-#endif
-  const Blk blk(Sg);
   Counters C = {0, 0, 0, 0, 0, 0, 0};
   Trav T;
   bool active = false;
@@ -2034,7 +1853,7 @@ __global__ void __launch_bounds__(WG, !FUSED ? RTX_TRACE_WAVES : (MODE == Q_CLOS
     lm.d[size_t(LD_bt) * lm.n + slot] = T.bt;
     lm.i[size_t(LI_bobj) * lm.n + slot] = T.bobj;
     lm.i[size_t(LI_bsub) * lm.n + slot] = T.bsub;
-    lm.i[size_t(LI_bhave) * lm.n + slot] = T.blocked ? 2 : (T.have ? 1 : 0);
+    lm.i[size_t(LI_bhave) * lm.n + slot] = T.have ? 1 : 0;
   };
   bool pend = false;  // FUSED: the lane's walk query completed, its walk step is due
   // FUSED: the walk step of a completed query — the next query of the walk
@@ -2067,11 +1886,7 @@ __global__ void __launch_bounds__(WG, !FUSED ? RTX_TRACE_WAVES : (MODE == Q_CLOS
       const double bt = w_bt;
       const int bo = w_bo, bs = w_bs;
       dvec3 res;
-#ifdef RTX_WALK_OOL
-      if (walk_hit_ool(Sg, li, pb, sdir, w_have, bt, bo, bs, &w, &res)) {
-#else
       if (walk_hit(*Sg, L, pb, sdir, w_have, bt, bo, bs, w, res)) {
-#endif
         const size_t slot = static_cast<size_t>(Q.slot[k]);
         if (walk_pick(code) < 0) {
           const dvec3 dsc = mk3(Q.d[QF_SCX * cap + k], Q.d[QF_SCY * cap + k], Q.d[QF_SCZ * cap + k]);
@@ -2089,9 +1904,7 @@ __global__ void __launch_bounds__(WG, !FUSED ? RTX_TRACE_WAVES : (MODE == Q_CLOS
         Q.d[QF_SAZ * cap + k] = w.sattn.z;
         Q.d[QF_LAST * cap + k] = w.last_t;
         Q.iv[0 * cap + k] = bo;
-        double qlim, qblk;
-        shadow_bounds(*Sg, L, pb, false, qlim, qblk);
-        active = trav_init<STATS, MODE>(T, S, pb, sdir, bt, bo, bs, qlim, qblk, C);
+        active = trav_init<STATS, MODE>(T, S, pb, sdir, bt, bo, bs, shadow_limit(*Sg, L, pb, false), C);
         pend = !active;  // answered by the root test: the walk's next step
         if (STATS) nrestart++;
         w_have = T.have;
@@ -2104,7 +1917,7 @@ __global__ void __launch_bounds__(WG, !FUSED ? RTX_TRACE_WAVES : (MODE == Q_CLOS
   for (;;) {
     const uint64_t xt0 = STATS ? clock64() : 0;
     if (FUSED) {
-      // Every lane is idle here (RTX_REFILL 1: the step loop below runs until
+      // Every lane is idle here (the step loop below runs until
       // no lane is active), so the walk state is dead: resetting it to
       // constants tells the register allocator so, and the walk / shading
       // step's temporaries reuse its registers instead of spilling around it.
@@ -2153,7 +1966,7 @@ __global__ void __launch_bounds__(WG, !FUSED ? RTX_TRACE_WAVES : (MODE == Q_CLOS
           const dvec3 P = mk3(Q.d[0 * cap + kq], Q.d[1 * cap + kq], Q.d[2 * cap + kq]);
           const dvec3 D = mk3(Q.d[3 * cap + kq], Q.d[4 * cap + kq], Q.d[5 * cap + kq]);
           active = trav_init<STATS, MODE>(T, S, P, D, Q.d[6 * cap + kq], Q.iv[0 * cap + kq], Q.iv[1 * cap + kq],
-                                          Q.d[7 * cap + kq], MODE == Q_NEXT ? Q.d[8 * cap + kq] : -RTX_INF, C);
+                                          Q.d[7 * cap + kq], C);
         } else if (MODE == Q_CLOSEST && cam) {  // claim the slot's first sample, its first camera ray
           const int slot = SA.slot_off + static_cast<int>(kq);
           LaneRef LR(lm, static_cast<size_t>(slot));
@@ -2164,19 +1977,18 @@ __global__ void __launch_bounds__(WG, !FUSED ? RTX_TRACE_WAVES : (MODE == Q_CLOS
             // out-parameter of the out-of-line claim (a stack object: 80 B
             // of scratch written and read per camera ray)
             const QRay qr = cam_first_ray(LR, *SA.Fp);
-            active = trav_init<STATS, MODE>(T, S, qr.p, qr.d, -RTX_INF, -1, -1, RTX_INF, -RTX_INF, C);
+            active = trav_init<STATS, MODE>(T, S, qr.p, qr.d, -RTX_INF, -1, -1, RTX_INF, C);
           }
         } else if (MODE == Q_CLOSEST) {  // fused closest record: the ray only
           const dvec3 P = mk3(Q.d[0 * cap + kq], Q.d[1 * cap + kq], Q.d[2 * cap + kq]);
           const dvec3 D = mk3(Q.d[3 * cap + kq], Q.d[4 * cap + kq], Q.d[5 * cap + kq]);
-          active = trav_init<STATS, MODE>(T, S, P, D, -RTX_INF, -1, -1, RTX_INF, -RTX_INF, C);
+          active = trav_init<STATS, MODE>(T, S, P, D, -RTX_INF, -1, -1, RTX_INF, C);
         } else {  // a walk's first query (continuations restart in walk_phase)
           const int code = Q.iv[1 * cap + kq];
           const RtxLight& L = Sg->lights[walk_light(code)];
           const dvec3 pb = mk3(Q.d[QF_PX * cap + kq], Q.d[QF_PY * cap + kq], Q.d[QF_PZ * cap + kq]);
-          double qlim, qblk;
-          shadow_bounds(*Sg, L, pb, true, qlim, qblk);
-          active = trav_init<STATS, MODE>(T, S, pb, walk_dir(*Sg, code, pb), -RTX_INF, -1, -1, qlim, qblk, C);
+          active = trav_init<STATS, MODE>(T, S, pb, walk_dir(*Sg, code, pb), -RTX_INF, -1, -1,
+                                          shadow_limit(*Sg, L, pb, true), C);
         }
         if (!active) {
           if (FUSED) pend = !noq;  // (a slot without a sample: nothing to shade)
@@ -2191,14 +2003,7 @@ __global__ void __launch_bounds__(WG, !FUSED ? RTX_TRACE_WAVES : (MODE == Q_CLOS
       xcnt++;
     }
     if (__ballot(active || pend) == 0ull) break;  // nothing claimed and nothing left
-    const int thresh = exhausted ? 1 : RTX_REFILL;
     do {
-#if RTX_TEAM
-      // idle lanes help with pending mesh subtrees (team_donate; RTX_TEAM 2:
-      // also before the wave's query list is exhausted)
-      if (FUSED && (RTX_TEAM >= 2 || exhausted)) team_donate(T, stk, lane, active, stack_cap - TEAM_STASH);
-      bool hdone = false;
-#endif
       // Postponed costly units (Aila & Laine's while-while, one call site):
       // while at least leaf_k lanes of the wave are at a 4-wide record, only
       // those lanes step, so most steps run the record test alone instead of
@@ -2218,12 +2023,7 @@ __global__ void __launch_bounds__(WG, !FUSED ? RTX_TRACE_WAVES : (MODE == Q_CLOS
       }
       if (go) {
         if (STATS) qsteps++;
-        if (trav_step<STATS, MODE>(T, S, stk, lane, blk, C)) {
-#if RTX_TEAM
-          if (FUSED && (T.team & TEAM_HELPER))
-            hdone = true;
-          else
-#endif
+        if (trav_step<STATS, MODE>(T, S, stk, lane, C)) {
           if (FUSED) pend = true;
           else finish();
           active = false;
@@ -2234,9 +2034,6 @@ __global__ void __launch_bounds__(WG, !FUSED ? RTX_TRACE_WAVES : (MODE == Q_CLOS
           qsteps = 0;
         }
       }
-#if RTX_TEAM
-      if (FUSED) team_merge(T, stk, lane, hdone, MODE == Q_CLOSEST, stack_cap - TEAM_STASH);
-#endif
       if (STATS) {
         const uint64_t dt = clock64() - st0;
 #pragma unroll
@@ -2246,7 +2043,7 @@ __global__ void __launch_bounds__(WG, !FUSED ? RTX_TRACE_WAVES : (MODE == Q_CLOS
             pcnt[c]++;
           }
       }
-    } while (static_cast<int>(__popcll(__ballot(active))) >= thresh);
+    } while (__ballot(active) != 0ull);
   }
   if (STATS && lane == 0) {
     unsigned long long* pr = stats + RTX_STATS_PROF + 20 * (MODE - 1);
@@ -2561,6 +2358,13 @@ namespace {
 
 thread_local std::string g_err;
 
+// every render-path kernel launch, counted for rtx_kernel_time (`st`: the
+// SceneState of the render in progress)
+#define RTX_LAUNCH(...)                \
+  do {                                 \
+    hipLaunchKernelGGL(__VA_ARGS__);   \
+    ++st->n_launch;                    \
+  } while (0)
 #define HIP_TRY(expr)                                                            \
   do {                                                                           \
     hipError_t e_ = (expr);                                                      \
@@ -2623,6 +2427,7 @@ struct FrameCtx {
   int64_t chk_seq = -1;
   std::vector<uint64_t> chk_keys;
   int wf_call = 0;  // run_wavefront calls of the current rtx_render
+  bool bstat_clear = false;  // d_bstat (incl. *bover) cleared by this rtx_render's first forking run
   // adaptive AA: one buffer per level (values, first-quarter index, mask,
   // regions), grown on demand and reused by later frames (no hipMalloc /
   // hipFree, which synchronises the device, per level per frame)
@@ -2683,6 +2488,12 @@ struct SceneState {
   // frames whose two-entry pending stacks overflowed once: full stacks from
   // then on
   std::set<uint64_t> full_stack_keys;
+  // fork depth per whole frame (whole_frame_key: the parameters without the
+  // tile deal), decided once by depth_probe (rtx_render) from a fixed subset
+  // of the whole frame, so a frame and every shard of it use the same depth
+  std::map<uint64_t, int> depth_rule;
+  bool probe_mode = false;              // render_once is depth_probe's render
+  int64_t probe_req = 0, probe_units = 0;  // its fork requests and work units
   // rtx_render calls so far (a frame's sequence number), the wrong frames
   // found since the last rtx_frame_status, pipelined renders counted for
   // rtx_overlap_count
@@ -2693,6 +2504,7 @@ struct SceneState {
   std::vector<hipEvent_t> ev_pool;
   size_t ev_used = 0;
   std::vector<hipEvent_t> ev_start, ev_stop;
+  int64_t n_launch = 0;  // kernel launches since the last rtx_kernel_time
 };
 
 template <typename T>
@@ -2863,22 +2675,15 @@ rtx_status rtx_scene_create(int device, const RtxSceneDesc* d, void** out) {
     S.sroot = tt.sroot;
     // per-lane LDS stack: scene-level entries stay below a mesh walk's
     st->stack_cap = tt.sneed + tt.mneed + 2;
-#if RTX_TEAM
-    st->stack_cap = std::max(st->stack_cap, tt.mneed + TEAM_STASH);  // a helper's walk + its parked answer
-#endif
 #define UP(src, n, dst) \
   if ((rc = upload(*st, src, size_t(n), &dst)) != RTX_OK) { rtx_scene_destroy(st); return rc; }
     UP(tt.sn4.data(), tt.sn4.size(), S.snode4);
     UP(tt.mn4.data(), tt.mn4.size(), S.mnode4);
-    S.mhot = S.mnode4;  // kernels staging the hot records in LDS repoint this
-    S.n_mhot = tt.n_mhot;
     S.n_srec = static_cast<int32_t>(tt.sn4.size());
     UP(tt.mroots.data(), tt.mroots.size(), S.mroots);
     UP(tt.tfaces.data(), tt.tfaces.size(), S.tfaces);
     UP(tt.trank.data(), tt.trank.size(), S.trank);
     UP(tt.tmeta.data(), tt.tmeta.size(), S.tmeta);
-    UP(tt.tfacef.data(), tt.tfacef.size(), S.tfacef);
-    S.mext = mesh_extent_f(d);
 #undef UP
   }
   for (int k = 0; k < 6; ++k) {
@@ -3177,12 +2982,34 @@ rtx_status rtx_shard_pixels(const RtxRenderParams* p, int64_t* npix) {
   return RTX_OK;
 }
 
+// A whole frame's identity for the fork-depth rule: the render parameters
+// without the tile deal (tile, shard, nshards, packed), FNV-1a.
+static uint64_t whole_frame_key(const RtxRenderParams& p) {
+  RtxRenderParams q;
+  std::memset(&q, 0, sizeof(q));
+  q.width = p.width;
+  q.height = p.height;
+  q.depth = p.depth;
+  q.aa_mode = p.aa_mode;
+  q.aa_samples = p.aa_samples;
+  q.dof = p.dof;
+  q.dof_div = p.dof_div;
+  q.anaglyph = p.anaglyph;
+  q.ss_res = p.ss_res;
+  q.overlapping = p.overlapping;
+  q.aa_thresh = p.aa_thresh;
+  q.aterm_thresh = p.aterm_thresh;
+  q.dof_fd = p.dof_fd;
+  q.dof_apsz = p.dof_apsz;
+  uint64_t k = 1469598103934665603ull;
+  const unsigned char* c = reinterpret_cast<const unsigned char*>(&q);
+  for (size_t i = 0; i < sizeof(q); ++i) k = (k ^ c[i]) * 1099511628211ull;
+  return k;
+}
+
 // One render of frame `seq` (rtx_render below).  *redo 1: this synchronous
 // render found its history-sized buffers short (collect_check) — the image
-// is wrong and the caller renders again, now with full-size buffers.  2: the
-// frame's first render at the default fork depth found more fork requests
-// than spares — the caller renders it again at fork depth 3, as every later
-// render of the frame will be (run_wavefront, "forks outgrow the spares").
+// is wrong and the caller renders again, now with full-size buffers.
 static rtx_status render_once(SceneState* st, const RtxRenderParams* params, uint8_t* rgb8, double* rgb_f64,
                               RtxHitRecord* hits, int device_ptrs, void* stream_v, RtxStats* stats, int64_t seq,
                               bool retry, int* redo) {
@@ -3230,11 +3057,6 @@ static rtx_status render_once(SceneState* st, const RtxRenderParams* params, uin
   for (FrameCtx& C : st->cx)
     if (&C != X) collect_check(st, C, false);
   std::vector<uint64_t> chk_keys;  // this frame's history-sized runs (run_wavefront)
-  // the fork-depth probe (run_wavefront): a frame's first render at the
-  // default depth, whose per-group fork requests are compared with its spares
-  // before the render returns (>= 0: the spares; the history key)
-  int64_t depth_probe_spares = -1;
-  uint64_t depth_probe_key = 0;
   if (!X->free_ev) HIP_TRY(hipEventCreateWithFlags(&X->free_ev, hipEventDisableTiming));
   if (X->wf_streams.empty()) {
     hipStream_t s0;
@@ -3277,10 +3099,6 @@ static rtx_status render_once(SceneState* st, const RtxRenderParams* params, uin
   st->S_launch = st->S;
   DevScene& S = st->S_launch;
   S.ss_res = params->ss_res;
-  {
-    const char* e = getenv("RTX_SKIP_DARK");  // 0: trace every shadow ray (A/B)
-    if (e && atoi(e) == 0) S.skip_dark = 0;
-  }
   bool need_picks = false;
   for (const auto& L : st->lights) need_picks |= L.type >= RTX_LIGHT_AREA_RECT;
   if (need_picks && st->picks_res != params->ss_res) {
@@ -3327,8 +3145,7 @@ static rtx_status render_once(SceneState* st, const RtxRenderParams* params, uin
   const bool megakernel = mk_env && atoi(mk_env) != 0;
   // DoF on the wavefront path: each of a sample's divs + 1 camera rays is a
   // work unit of its own (17x the parallel units, paths 17x shorter)
-  const char* split_env = getenv("RTX_DOF_SPLIT");
-  if (!megakernel && params->dof && !F.P.anaglyph && !(split_env && atoi(split_env) == 0)) {
+  if (!megakernel && params->dof && !F.P.anaglyph) {
     F.cam_split = 1;
     F.n_samples *= F.ncam;
   }
@@ -3374,6 +3191,7 @@ static rtx_status render_once(SceneState* st, const RtxRenderParams* params, uin
   double* sb = adaptive && megakernel ? nullptr : X->d_sbuf;
   std::vector<std::pair<hipEvent_t, hipEvent_t>> frame_events;
   X->wf_call = 0;
+  X->bstat_clear = false;
 
   if (megakernel) {
     const int cslots = adaptive ? (F.spp > 64 ? F.spp : 64) : 0;
@@ -3421,11 +3239,11 @@ static rtx_status render_once(SceneState* st, const RtxRenderParams* params, uin
     dispatch2(stats, adaptive, [&](auto st_, auto ad_) {
       constexpr bool ST_ = decltype(st_)::value, AD_ = decltype(ad_)::value;
       if (media)
-        hipLaunchKernelGGL((render_kernel<ST_, AD_, true>), dim3(grid), dim3(WG), lds, ws, st->S_launch,
+        RTX_LAUNCH((render_kernel<ST_, AD_, true>), dim3(grid), dim3(WG), lds, ws, st->S_launch,
                            X->d_scene, X->d_frame, st->d_work, sb, d_hits, d_rgb8, d_rgbf, st->d_stats, st->stack_cap,
                            X->d_pbuf, pend_cap, lm);
       else
-        hipLaunchKernelGGL((render_kernel<ST_, AD_, false>), dim3(grid), dim3(WG), lds, ws, st->S_launch,
+        RTX_LAUNCH((render_kernel<ST_, AD_, false>), dim3(grid), dim3(WG), lds, ws, st->S_launch,
                            X->d_scene, X->d_frame, st->d_work, sb, d_hits, d_rgb8, d_rgbf, st->d_stats, st->stack_cap,
                            X->d_pbuf, pend_cap, lm);
     });
@@ -3562,31 +3380,22 @@ static rtx_status render_once(SceneState* st, const RtxRenderParams* params, uin
           }
           C.bstat_pending = false;
         }
-      // A frame whose fork requests outgrow the spare slots it may have (R1,
-      // the glass frame: forks at nearly every hit) forks down to heap depth
-      // 3: 14 bucket positions a set instead of 30, so the lower memory cap
-      // below keeps more slots in flight — R1 at 252-254 ms in 38.7 GB
-      // against 255 ms in 55.9 GB at depth 4 (profiles/r05q_ab_r1_memory.txt).
-      // The depth moves the line between bucket sums and the running sum
-      // (f64 images differ in the last bit), so every render of a frame uses
-      // the same one: the frame's first render at depth 4 reads its fork
-      // requests back before it returns and, when they outgrow the spares,
-      // is rendered again at depth 3 (rtx_render); the depth-4 history then
-      // decides every later render the same way.
-      if (fork_ok && fork_depth == 4 && !fd_env && !adaptive) {
-        const int64_t spares = (F.n_samples + G - 1) / G * spare_pct / 100;
-        const auto h4 = st->bucket_hist.find(bkey);
-        if (h4 == st->bucket_hist.end()) {
-          depth_probe_spares = spares;
-          depth_probe_key = bkey;
-        } else if (h4->second.forks > spares) {
-          const uint64_t key4 = bkey;
+      // A frame whose ray trees fork at many of their nodes (R1, the glass
+      // frame: fork requests at nearly every hit) forks down to heap depth 3:
+      // 14 bucket positions a set instead of 30, so the lower memory cap below
+      // keeps more slots in flight — R1 at 252-254 ms in 38.7 GB against 255
+      // ms in 55.9 GB at depth 4 (profiles/r05q_ab_r1_memory.txt).  The depth
+      // moves the line between bucket sums and the running sum (f64 images
+      // differ in the last bit), so every render of a frame — and every shard
+      // of it on a multi-GPU job — uses the same one: depth_rule, decided once
+      // per whole frame by depth_probe (rtx_render) from a fixed subset of the
+      // whole frame, the same pixels whichever shard is being rendered.
+      if (fork_ok && fork_depth == 4 && !fd_env && !adaptive && !st->probe_mode) {
+        const auto dr = st->depth_rule.find(whole_frame_key(*params));
+        if (dr != st->depth_rule.end() && dr->second == 3) {
           fork_depth = 3;
           bkey = frame_key(fork_depth);
           forks_outgrow = true;
-          // (a frame whose two-entry stacks overflowed at depth 4 keeps full
-          // stacks at depth 3 too)
-          if (st->full_stack_keys.count(key4)) st->full_stack_keys.insert(bkey);
           if (const char* e = getenv("RTX_DEBUG"))
             if (atoi(e) != 0) fprintf(stderr, "rtx: forks outgrow the spares: fork depth 3, 34-GiB cap\n");
         }
@@ -3712,9 +3521,11 @@ static rtx_status render_once(SceneState* st, const RtxRenderParams* params, uin
       if (!X->d_bstat) HIP_TRY(hipMalloc(&X->d_bstat, 4 * sizeof(unsigned int)));
       if (!X->h_bstat) HIP_TRY(hipHostMalloc(&X->h_bstat, (4 + 16) * sizeof(unsigned int)));
       if (!X->bstat_ev) HIP_TRY(hipEventCreateWithFlags(&X->bstat_ev, hipEventDisableTiming));
-      // ([taken] per run; [bover] once per render: the frame check reads it
-      // after the frame's last run)
-      HIP_TRY(hipMemsetAsync(X->d_bstat, 0, (X->wf_call == 0 ? 4 : 1) * sizeof(unsigned int), ws));
+      // ([taken] per run; [bover] once per render, by its first forking run
+      // whichever run that is: the frame check reads it after the frame's
+      // last run)
+      HIP_TRY(hipMemsetAsync(X->d_bstat, 0, (X->bstat_clear ? 1 : 4) * sizeof(unsigned int), ws));
+      X->bstat_clear = true;
       F.fbuf = X->d_fbuf;
       F.fmask = X->d_fmask;
       F.bidx = X->d_bidx;
@@ -3894,11 +3705,7 @@ static rtx_status render_once(SceneState* st, const RtxRenderParams* params, uin
     // all of its slots (every other field is written before it is read)
     HIP_TRY(hipMemsetAsync(X->d_counters, 0, 16 * CNT_PER_GROUP * sizeof(unsigned int), ws));
     const size_t lds_stacks = size_t(st->stack_cap) * 64 * sizeof(int) * WAVES_PER_WG;
-#ifdef RTX_LDS_STAGE
-    const size_t lds = lds_stacks + size_t((S.n_srec <= RTX_LDS_SREC ? S.n_srec : 0) + S.n_mhot) * sizeof(DevNode4);
-#else
     const size_t lds = lds_stacks;
-#endif
     if (lds > 160 * 1024) {
       g_err = "rtx_render: LDS budget exceeded (BVH too deep)";
       return RTX_ERR_CAPACITY;
@@ -3914,17 +3721,13 @@ static rtx_status render_once(SceneState* st, const RtxRenderParams* params, uin
     {
       // Persistent trace grids of 1/div of the resident workgroups, so the
       // groups' kernels share the GPU instead of each filling it: on small
-      // frames (a shard of a multi-GPU frame: at most RTX_TGRID_SMALL samples,
+      // frames (a shard of a multi-GPU frame: at most small_frame samples,
       // default 10 M), div = G — there the groups' launches are mostly
       // latency-bound and a group's advance launch otherwise waits for CU
       // space behind the other groups' persistent kernels (8-way headline
       // shard 7.85-8.08 -> 7.61 ms; the whole frame 36.9 -> 38.4 ms, so not
-      // there).  RTX_TGRID_DIV overrides (1: whole-GPU grids).
-      const char* es = getenv("RTX_TGRID_SMALL");
-      if (es) small_frame = atoll(es);
-      int div = F.n_samples <= small_frame ? G : 1;
-      const char* e = getenv("RTX_TGRID_DIV");
-      if (e && atoi(e) > 0) div = atoi(e);
+      // there).
+      const int div = F.n_samples <= small_frame ? G : 1;
       if (div > 1) tgrid = std::max<int64_t>(1, tgrid / div);
     }
     if (tgrid > per) tgrid = per;
@@ -3953,9 +3756,7 @@ static rtx_status render_once(SceneState* st, const RtxRenderParams* params, uin
     // Half-GPU first launches stagger the groups: headline 31.5-31.9 vs
     // 32.6-33.0 ms, C4 42.2-42.6 vs 43.9 (profiles/r05l_ab_first_grid.txt).
     // Shards keep their 1/G grids (no change measured there).
-    int tg0_c = F.n_samples > small_frame ? 50 : 0, tg0_n = F.n_samples > small_frame ? 50 : 0;
-    if (const char* e = getenv("RTX_TG0_C")) tg0_c = std::max(0, std::min(100, atoi(e)));
-    if (const char* e = getenv("RTX_TG0_N")) tg0_n = std::max(0, std::min(100, atoi(e)));
+    const int tg0_c = F.n_samples > small_frame ? 50 : 0, tg0_n = F.n_samples > small_frame ? 50 : 0;
     const char* dbg_env = getenv("RTX_DEBUG");
     const bool dbg = dbg_env && atoi(dbg_env) != 0;
     const int dbg_level = dbg_env ? atoi(dbg_env) : 0;
@@ -3966,14 +3767,6 @@ static rtx_status render_once(SceneState* st, const RtxRenderParams* params, uin
     {
       const char* e = getenv("RTX_LEAF_K");
       if (e && atoi(e) > 0) leaf_k = std::min(65, atoi(e));
-    }
-    // the same for the launches of batched iterations >= 1 (latency-bound
-    // on small frames: a wave holds one claim and waits for its slowest
-    // lane, so postponing a lane's costly units only lengthens its chain)
-    int leaf_k_late = leaf_k;
-    {
-      const char* e = getenv("RTX_LEAF_K_LATE");
-      if (e && atoi(e) > 0) leaf_k_late = std::min(65, atoi(e));
     }
     hipEvent_t e0, e1;
     if ((rc = get_event(&e0)) != RTX_OK || (rc = get_event(&e1)) != RTX_OK) return rc;
@@ -4001,16 +3794,16 @@ static rtx_status render_once(SceneState* st, const RtxRenderParams* params, uin
           const int64_t grid = std::max<int64_t>(1, (lb + WG - 1) / WG);
           if (fuse) {
             if (stats)
-              hipLaunchKernelGGL((tail_fused_kernel<true>), dim3(grid), dim3(WG), lds, sg, S, X->d_scene, X->d_frame,
+              RTX_LAUNCH((tail_fused_kernel<true>), dim3(grid), dim3(WG), lds, sg, S, X->d_scene, X->d_frame,
                                  A, sb, d_hits, X->d_pbuf, pcap_run, cnt, live_in, in_cnt, st->stack_cap, st->d_stats,
                                  ql[size_t(g) * 2 + 1], static_cast<int>(g * gslots));
             else
-              hipLaunchKernelGGL((tail_fused_kernel<false>), dim3(grid), dim3(WG), lds, sg, S, X->d_scene, X->d_frame,
+              RTX_LAUNCH((tail_fused_kernel<false>), dim3(grid), dim3(WG), lds, sg, S, X->d_scene, X->d_frame,
                                  A, sb, d_hits, X->d_pbuf, pcap_run, cnt, live_in, in_cnt, st->stack_cap, st->d_stats,
                                  ql[size_t(g) * 2 + 1], static_cast<int>(g * gslots));
           } else {
             dispatch2(stats, media, [&](auto st_, auto md_) {
-              hipLaunchKernelGGL((tail_kernel<decltype(st_)::value, decltype(md_)::value>), dim3(grid), dim3(WG), lds,
+              RTX_LAUNCH((tail_kernel<decltype(st_)::value, decltype(md_)::value>), dim3(grid), dim3(WG), lds,
                                  sg, S, X->d_scene, X->d_frame, A, sb, d_hits, X->d_pbuf, pcap_run, cnt, live_in,
                                  in_cnt, st->stack_cap, st->d_stats);
             });
@@ -4045,18 +3838,18 @@ static rtx_status render_once(SceneState* st, const RtxRenderParams* params, uin
           // the slots the first launch does not claim start idle
           const int n0 = static_cast<int>(gslots) - cam_n[size_t(g)];
           if (n0 > 0)
-            hipLaunchKernelGGL(lane_init_kernel, dim3((n0 + WG - 1) / WG), dim3(WG), 0, sg, A,
+            RTX_LAUNCH(lane_init_kernel, dim3((n0 + WG - 1) / WG), dim3(WG), 0, sg, A,
                                static_cast<int>(g * gslots) + cam_n[size_t(g)], n0);
         } else if (fuse) {
           dispatch2(stats, fork, [&](auto st_, auto fk_) {
-            hipLaunchKernelGGL((advance_fused_kernel<decltype(st_)::value, decltype(fk_)::value>), dim3(agrid),
+            RTX_LAUNCH((advance_fused_kernel<decltype(st_)::value, decltype(fk_)::value>), dim3(agrid),
                                dim3(WG), 0, sg, S, X->d_scene, X->d_frame, A, sb, d_hits, X->d_pbuf, pcap_run, q0,
                                q1, cnt, st->d_stats, static_cast<int>(g * gslots), live_in, live_out, first, in_cnt,
                                out_cnt, recycle ? X->d_free + size_t(g) * gs : nullptr);
           });
         } else {
           dispatch3(stats, media, fork, [&](auto st_, auto md_, auto fk_) {
-            hipLaunchKernelGGL((advance_kernel<decltype(st_)::value, decltype(md_)::value, decltype(fk_)::value>),
+            RTX_LAUNCH((advance_kernel<decltype(st_)::value, decltype(md_)::value, decltype(fk_)::value>),
                                dim3(agrid), dim3(WG), 0, sg,
                                S, X->d_scene, X->d_frame, A, sb, d_hits, X->d_pbuf, pcap_run, q0, q1, cnt,
                                st->d_stats, static_cast<int>(g * gslots), live_in, live_out, first, in_cnt, out_cnt);
@@ -4068,7 +3861,7 @@ static rtx_status render_once(SceneState* st, const RtxRenderParams* params, uin
                                  : tg;
         ShadeArgs sa;
         std::memset(&sa, 0, sizeof(sa));
-        sa.leaf_k = it == 0 ? leaf_k : leaf_k_late;
+        sa.leaf_k = leaf_k;
         sa.free_ids = recycle ? X->d_free + size_t(g) * gs : nullptr;
         if (fuse) {
           sa.Fp = X->d_frame;
@@ -4095,10 +3888,10 @@ static rtx_status render_once(SceneState* st, const RtxRenderParams* params, uin
               (void)(hipEventRecord(d0, sg));
             }
             if (cam_it)
-              hipLaunchKernelGGL((trace_kernel<ST_, Q_CLOSEST, true, FK_, true>), dim3(tg), dim3(WG), lds, sg, S,
+              RTX_LAUNCH((trace_kernel<ST_, Q_CLOSEST, true, FK_, true>), dim3(tg), dim3(WG), lds, sg, S,
                                  X->d_scene, q0, cnt, A, st->stack_cap, st->d_stats, X->d_wterm, sa, -1);
             else
-              hipLaunchKernelGGL((trace_kernel<ST_, Q_CLOSEST, true, FK_>), dim3(tg), dim3(WG), lds, sg, S,
+              RTX_LAUNCH((trace_kernel<ST_, Q_CLOSEST, true, FK_>), dim3(tg), dim3(WG), lds, sg, S,
                                  X->d_scene, q0, cnt, A, st->stack_cap, st->d_stats, X->d_wterm, sa, -1);
             if (dbg_level >= 2) {
               unsigned int hc[CNT_PER_GROUP];
@@ -4124,7 +3917,7 @@ static rtx_status render_once(SceneState* st, const RtxRenderParams* params, uin
               (void)(hipEventCreate(&d1));
               (void)(hipEventRecord(d0, sg));
             }
-            hipLaunchKernelGGL((trace_kernel<ST_, Q_NEXT, true>), dim3(tgn), dim3(WG), lds, sg, S, X->d_scene, q1,
+            RTX_LAUNCH((trace_kernel<ST_, Q_NEXT, true>), dim3(tgn), dim3(WG), lds, sg, S, X->d_scene, q1,
                                cnt, A, st->stack_cap, st->d_stats, X->d_wterm, sa, clr_next);
             if (dbg_level >= 2) {
               float ms = 0.f;
@@ -4143,22 +3936,22 @@ static rtx_status render_once(SceneState* st, const RtxRenderParams* params, uin
               (void)(hipEventDestroy(d1));
             }
           } else if (!FK_) {
-            hipLaunchKernelGGL((trace_kernel<ST_, Q_CLOSEST>), dim3(tg), dim3(WG), lds, sg, S, X->d_scene, q0, cnt, A,
+            RTX_LAUNCH((trace_kernel<ST_, Q_CLOSEST>), dim3(tg), dim3(WG), lds, sg, S, X->d_scene, q0, cnt, A,
                                st->stack_cap, st->d_stats, nullptr, sa, -1);
-            hipLaunchKernelGGL((trace_kernel<ST_, Q_NEXT>), dim3(tg), dim3(WG), lds, sg, S, X->d_scene, q1, cnt, A,
+            RTX_LAUNCH((trace_kernel<ST_, Q_NEXT>), dim3(tg), dim3(WG), lds, sg, S, X->d_scene, q1, cnt, A,
                                st->stack_cap, st->d_stats, nullptr, sa, clr_next);
           }
         });
         if (!fuse && fork) {  // the sequential machine's trace kernels do not depend on forking
           if (stats) {
-            hipLaunchKernelGGL((trace_kernel<true, Q_CLOSEST>), dim3(tg), dim3(WG), lds, sg, S, X->d_scene, q0, cnt,
+            RTX_LAUNCH((trace_kernel<true, Q_CLOSEST>), dim3(tg), dim3(WG), lds, sg, S, X->d_scene, q0, cnt,
                                A, st->stack_cap, st->d_stats, nullptr, sa, -1);
-            hipLaunchKernelGGL((trace_kernel<true, Q_NEXT>), dim3(tg), dim3(WG), lds, sg, S, X->d_scene, q1, cnt, A,
+            RTX_LAUNCH((trace_kernel<true, Q_NEXT>), dim3(tg), dim3(WG), lds, sg, S, X->d_scene, q1, cnt, A,
                                st->stack_cap, st->d_stats, nullptr, sa, clr_next);
           } else {
-            hipLaunchKernelGGL((trace_kernel<false, Q_CLOSEST>), dim3(tg), dim3(WG), lds, sg, S, X->d_scene, q0, cnt,
+            RTX_LAUNCH((trace_kernel<false, Q_CLOSEST>), dim3(tg), dim3(WG), lds, sg, S, X->d_scene, q0, cnt,
                                A, st->stack_cap, st->d_stats, nullptr, sa, -1);
-            hipLaunchKernelGGL((trace_kernel<false, Q_NEXT>), dim3(tg), dim3(WG), lds, sg, S, X->d_scene, q1, cnt, A,
+            RTX_LAUNCH((trace_kernel<false, Q_NEXT>), dim3(tg), dim3(WG), lds, sg, S, X->d_scene, q1, cnt, A,
                                st->stack_cap, st->d_stats, nullptr, sa, clr_next);
           }
         }
@@ -4206,7 +3999,7 @@ static rtx_status render_once(SceneState* st, const RtxRenderParams* params, uin
     // a run sized from its history (two-entry stacks, a pool of the last
     // render's set count) is checked once the frame has run (rtx_render's end)
     if (low_stack || (fork_ok && bcap < nunit_out)) chk_keys.push_back(bkey);
-    if (fork_ok && st->bucket_hist.find(bkey) == st->bucket_hist.end() && !X->bstat_pending) {
+    if (fork_ok && (st->probe_mode || st->bucket_hist.find(bkey) == st->bucket_hist.end()) && !X->bstat_pending) {
       // first render of this frame: its set count, read at the next call
       HIP_TRY(hipMemcpyAsync(X->h_bstat, X->d_bstat, 2 * sizeof(unsigned int), hipMemcpyDeviceToHost, ws));
       // (the fork counters are final: the other groups joined ws above)
@@ -4229,7 +4022,7 @@ static rtx_status render_once(SceneState* st, const RtxRenderParams* params, uin
     }
     const int64_t ppb = WG / F.spp;
     const int64_t rblocks = (npix + ppb - 1) / ppb;
-    hipLaunchKernelGGL(reduce_kernel, dim3(rblocks), dim3(WG), 0, stream, X->d_frame, sb, d_rgb8, d_rgbf, npix);
+    RTX_LAUNCH(reduce_kernel, dim3(rblocks), dim3(WG), 0, stream, X->d_frame, sb, d_rgb8, d_rgbf, npix);
     HIP_TRY(hipGetLastError());
   } else if (!megakernel) {
     // adaptive AA, level by level (adapt_*_kernel): level 0's regions are the
@@ -4261,7 +4054,7 @@ static rtx_status render_once(SceneState* st, const RtxRenderParams* params, uin
     if (!X->d_acnt) HIP_TRY(hipMalloc(&X->d_acnt, 2 * sizeof(unsigned int)));
     unsigned int hcnt[2] = {0u, 0u};
     HIP_TRY(hipMemsetAsync(X->d_acnt, 0, 2 * sizeof(unsigned int), ws));
-    hipLaunchKernelGGL(adapt_stats_kernel, dim3((npix + WG - 1) / WG), dim3(WG), 0, ws, X->d_frame, sb,
+    RTX_LAUNCH(adapt_stats_kernel, dim3((npix + WG - 1) / WG), dim3(WG), 0, ws, X->d_frame, sb,
                        levels[0], int64_t(0), int64_t(npix), X->d_acnt);
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipMemcpyAsync(hcnt, X->d_acnt, sizeof(hcnt), hipMemcpyDeviceToHost, ws));
@@ -4273,7 +4066,7 @@ static rtx_status render_once(SceneState* st, const RtxRenderParams* params, uin
       if ((rc = level_alloc(n, true, nx)) != RTX_OK) return rc;
       HIP_TRY(hipMemsetAsync(X->d_acnt, 0, 2 * sizeof(unsigned int), ws));
       const ALevel& up = levels.back();
-      hipLaunchKernelGGL(adapt_emit_kernel, dim3((up.n + WG - 1) / WG), dim3(WG), 0, ws, X->d_frame, up,
+      RTX_LAUNCH(adapt_emit_kernel, dim3((up.n + WG - 1) / WG), dim3(WG), 0, ws, X->d_frame, up,
                          const_cast<ARegion*>(nx.reg), X->d_acnt + 1);
       HIP_TRY(hipGetLastError());
       levels.push_back(nx);
@@ -4284,7 +4077,7 @@ static rtx_status render_once(SceneState* st, const RtxRenderParams* params, uin
         FL.n_items = nc;
         FL.n_samples = nc * FL.spp * (FL.cam_split ? FL.ncam : 1);
         if ((rc = run_wavefront(FL, nc, false)) != RTX_OK) return rc;
-        hipLaunchKernelGGL(adapt_stats_kernel, dim3((nc + WG - 1) / WG), dim3(WG), 0, ws, X->d_frame, sb, nx, c0,
+        RTX_LAUNCH(adapt_stats_kernel, dim3((nc + WG - 1) / WG), dim3(WG), 0, ws, X->d_frame, sb, nx, c0,
                            nc, X->d_acnt);
         HIP_TRY(hipGetLastError());
         // (run_wavefront copies FL to the device before its first launch;
@@ -4300,7 +4093,7 @@ static rtx_status render_once(SceneState* st, const RtxRenderParams* params, uin
     }
     for (size_t L = levels.size(); L-- > 0;) {
       ALevel below = L + 1 < levels.size() ? levels[L + 1] : ALevel{nullptr, nullptr, nullptr, nullptr, 0};
-      hipLaunchKernelGGL(adapt_combine_kernel, dim3((levels[L].n + WG - 1) / WG), dim3(WG), 0, ws, X->d_frame,
+      RTX_LAUNCH(adapt_combine_kernel, dim3((levels[L].n + WG - 1) / WG), dim3(WG), 0, ws, X->d_frame,
                          levels[L], below, d_rgb8, d_rgbf);
       HIP_TRY(hipGetLastError());
     }
@@ -4341,25 +4134,13 @@ static rtx_status render_once(SceneState* st, const RtxRenderParams* params, uin
       return RTX_OK;
     }
   }
-  // the fork-depth probe: this first render's fork requests, before it returns
-  if (depth_probe_spares >= 0 && X->bstat_pending && X->bstat_key == depth_probe_key && X->bstat_groups > 0) {
+  // depth_probe's render: its fork requests (every node child asks, granted
+  // or not) and its work units, before it returns
+  if (st->probe_mode && X->bstat_pending && X->bstat_groups > 0) {
     HIP_TRY(hipEventSynchronize(X->bstat_ev));
-    int64_t fm = 0;
-    for (int g = 0; g < X->bstat_groups; ++g) fm = std::max<int64_t>(fm, X->h_bstat[4 + g]);
-    if ((X->h_bstat[1] & 3u) == 0u && fm > depth_probe_spares) {
-      // this render's own frame check, now (its image is replaced: not a
-      // wrong frame, but a stack overflow still sends the re-render to full
-      // stacks)
-      if (X->chk_pending) {
-        HIP_TRY(hipStreamSynchronize(ws));
-        const int64_t nb = st->bad_n, fb = st->bad_first;
-        collect_check(st, *X, true);
-        st->bad_n = nb;
-        st->bad_first = fb;
-      }
-      *redo = 2;  // (the pending counts become the depth-4 history at the re-render)
-      return RTX_OK;
-    }
+    st->probe_req = 0;
+    for (int g = 0; g < X->bstat_groups; ++g) st->probe_req += X->h_bstat[4 + g];
+    st->probe_units = F.n_samples;
   }
   if (stats) {
     unsigned long long c[RTX_STATS_N];
@@ -4409,6 +4190,65 @@ static rtx_status render_once(SceneState* st, const RtxRenderParams* params, uin
   return RTX_OK;
 }
 
+// The fork-depth rule of a whole frame (run_wavefront, "forks at many of
+// their nodes"), decided once per whole frame: a host-buffer render at the
+// default depth of a FIXED subset of the whole frame — every 16 x 16 tile
+// whose deal index is a multiple of tiles / 128 (about 128 tiles), or the
+// whole frame when it has at most 256 such tiles — whose fork requests
+// (every node child asks, granted or not) exceed half its work units: depth
+// 3, else 4.  The subset depends on the frame's parameters only, not on the
+// shard being rendered, so a single-GPU frame and every rank of a multi-GPU
+// job decide alike and render the same bits.  The probe's kernels are not
+// counted (rtx_kernel_time).
+static rtx_status depth_probe(SceneState* st, const RtxRenderParams* params, void* stream_v, int64_t seq) {
+  const char* fork_env = getenv("RTX_FORK");
+  const char* fd_env = getenv("RTX_FORK_DEPTH");
+  const char* mk_env = getenv("RTX_MEGAKERNEL");
+  if ((fork_env && atoi(fork_env) == 0) || (fd_env && atoi(fd_env) > 0) || (mk_env && atoi(mk_env) != 0) ||
+      params->anaglyph || !st->any_recur || params->depth <= 0 || params->aa_mode == RTX_AA_ADAPTIVE ||
+      params->width <= 0 || params->height <= 0)
+    return RTX_OK;  // (frames the rule does not apply to: run_wavefront never looks them up)
+  const uint64_t key = whole_frame_key(*params);
+  if (st->depth_rule.count(key)) return RTX_OK;
+  RtxRenderParams q = *params;
+  q.tile = 0;
+  q.shard = 0;
+  q.nshards = 1;
+  q.packed = 0;
+  const int64_t ntiles = int64_t((q.width + 15) / 16) * int64_t((q.height + 15) / 16);
+  if (ntiles > 256) {
+    q.tile = 16;
+    q.nshards = static_cast<int32_t>(ntiles / 128);
+    q.packed = 1;
+  }
+  int64_t npix = 0;
+  rtx_status rc = rtx_shard_pixels(&q, &npix);
+  if (rc != RTX_OK) return rc;
+  std::vector<uint8_t> rgb(size_t(npix) * 3);
+  const size_t ev0 = st->ev_start.size();
+  const int64_t l0 = st->n_launch;
+  st->probe_mode = true;
+  st->probe_req = 0;
+  st->probe_units = 0;
+  int redo = 0;
+  rc = render_once(st, &q, rgb.data(), nullptr, nullptr, 0, stream_v, nullptr, seq, true, &redo);
+  st->probe_mode = false;
+  for (size_t k = ev0; k < st->ev_start.size(); ++k) {  // (synchronous: its events are done)
+    st->ev_pool.push_back(st->ev_start[k]);
+    st->ev_pool.push_back(st->ev_stop[k]);
+  }
+  st->ev_start.resize(ev0);
+  st->ev_stop.resize(ev0);
+  st->n_launch = l0;
+  if (rc != RTX_OK) return rc;
+  st->depth_rule[key] = st->probe_units > 0 && 2 * st->probe_req > st->probe_units ? 3 : 4;
+  if (const char* e = getenv("RTX_DEBUG"))
+    if (atoi(e) != 0)
+      fprintf(stderr, "rtx: fork-depth probe: %lld requests / %lld units -> depth %d\n",
+              static_cast<long long>(st->probe_req), static_cast<long long>(st->probe_units), st->depth_rule[key]);
+  return RTX_OK;
+}
+
 rtx_status rtx_render(void* scene, const RtxRenderParams* params, uint8_t* rgb8, double* rgb_f64,
                       RtxHitRecord* hits, int device_ptrs, void* stream_v, RtxStats* stats) {
   if (!scene || !params) {
@@ -4417,12 +4257,26 @@ rtx_status rtx_render(void* scene, const RtxRenderParams* params, uint8_t* rgb8,
   }
   SceneState* st = static_cast<SceneState*>(scene);
   const int64_t seq = st->frame_seq++;
+  rtx_status rc0 = depth_probe(st, params, stream_v, seq);
+  if (rc0 != RTX_OK) return rc0;
   int redo = 0;
+  const size_t ev0 = st->ev_start.size();
+  const int64_t pip0 = st->n_pipelined;
   rtx_status rc = render_once(st, params, rgb8, rgb_f64, hits, device_ptrs, stream_v, stats, seq, false, &redo);
   if (rc == RTX_OK && redo) {
     if (redo == 1)
       fprintf(stderr, "rtx_render: rendering frame %lld again with full-size buffers\n", static_cast<long long>(seq));
     redo = 0;
+    // the replaced attempt's kernel events and pipelining count go: the
+    // counters (rtx_kernel_time, rtx_overlap_count) describe one frame
+    for (size_t k = ev0; k < st->ev_start.size(); ++k) {
+      HIP_TRY(hipEventSynchronize(st->ev_stop[k]));
+      st->ev_pool.push_back(st->ev_start[k]);
+      st->ev_pool.push_back(st->ev_stop[k]);
+    }
+    st->ev_start.resize(ev0);
+    st->ev_stop.resize(ev0);
+    st->n_pipelined = pip0;
     rc = render_once(st, params, rgb8, rgb_f64, hits, device_ptrs, stream_v, stats, seq, true, &redo);
     if (rc == RTX_OK && redo) {
       g_err = "rtx_render: the frame came out wrong twice (history-sized buffers short after a full-size re-render)";
@@ -4454,7 +4308,8 @@ rtx_status rtx_kernel_time(void* scene, double* total_ms, int* launches) {
     st->ev_pool.push_back(st->ev_stop[k]);
   }
   if (total_ms) *total_ms = tot;
-  if (launches) *launches = static_cast<int>(st->ev_start.size());
+  if (launches) *launches = static_cast<int>(st->n_launch);
+  st->n_launch = 0;
   st->ev_start.clear();
   st->ev_stop.clear();
   return RTX_OK;

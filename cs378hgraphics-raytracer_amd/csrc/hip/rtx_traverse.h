@@ -18,14 +18,6 @@
 #define Q_CLOSEST 1
 #define Q_NEXT 2
 
-// Teams (team_donate below): lanes of a wave without a query of their own
-// walk pending mesh subtrees of lanes that still have work.  0 = off.
-#ifndef RTX_TEAM
-#define RTX_TEAM 0
-#endif
-#define TEAM_HELPER 0x80
-#define TEAM_STASH 5  // stack entries a helper's own answer is parked in (top of its column)
-
 namespace rtxd {
 
 // Unified query over the two-level BVH.
@@ -46,25 +38,17 @@ namespace rtxd {
 // persistent trace kernel can hand a lane a new query as soon as its own one
 // ends while the other lanes of the wave keep stepping; traverse() runs one
 // query to completion.
-//
-// Shadow early-out (Q_NEXT with a Blocker).  The walk of srsAttenuation
-// (light.cpp:30-50) returns 0 when it reaches a hit entered from outside
-// (N.dir <= 0) whose material is not transmissive.  Before such a hit the
-// walk can only end with 0 (another blocker, the aterm cut) or through the
-// point-light limit check, which cannot trip for hits with t < tblock
-// (DESIGN.md).  So the first blocker found with t < tblock settles the
-// whole walk: T.blocked, shadow attenuation 0.
 struct Trav {
   dvec3 P, D;
   RayInv ri;  // exact-fallback reciprocal: the root and the objects' world boxes
   RayF rf;    // float tests of the records being walked: the scene's, or in
               // mode 2 the mesh's (local frame); reset when the mesh is done
-  double tp, tlimit, tlo, tblock;
+  double tp, tlimit, tlo;
   int rp, sq;
   // answer so far
   double bt;
   int bobj, bsub;
-  bool have, blocked;
+  bool have;
   // walk: ref >= 0 DevNode4 record, ref < 0 leaf ~(first << 2 | count);
   // mode 0 scene BVH, 1 objects [oc, oe) of a scene leaf, 2 mesh BVH
   int sp, ref, mode, oc, oe;
@@ -74,9 +58,6 @@ struct Trav {
   int moi, mbase, mfoff, mnoff, mface;
   bool mhave;
   bool closest;  // the query's mode (read by the Q_ANY instantiations)
-#if RTX_TEAM
-  int team;  // teams (team_donate): 0, a helper (TEAM_HELPER | owner lane) or an owner (helpers << 8)
-#endif
 };
 
 // QMODE Q_ANY: one instantiation for both query kinds, the mode read from
@@ -84,13 +65,6 @@ struct Trav {
 // tail), so a wave steps them together instead of running the two loops
 // one after the other.
 #define Q_ANY 0
-
-// Plain ordered queries (closest hits, the host harness, the megakernel).
-struct NoBlocker {
-  RT_HD NoBlocker() {}
-  RT_HD explicit NoBlocker(const void*) {}
-  RT_HD bool operator()(const Trav&, int, int) const { return false; }
-};
 
 // A face hit counts only if its mesh-BVH leaf box passes the exact slab test
 // in the mesh's local frame (KdTree::intersectList collects the items of hit
@@ -102,7 +76,7 @@ RT_HD bool leaf_ok(const Trav& T, const DevScene& S, int leaf) {
   return slab(lf.bmin, lf.bmax, T.lp, T.ld, a, b);
 }
 
-// Visit one 4-wide record:// Visit one 4-wide record: test its entries' boxes (conservatively, pruned
+// Visit one 4-wide record: test its entries' boxes (conservatively, pruned
 // to [lo, hi]), continue with the nearest entry hit and push the
 // other hits farthest first, so the walk stays near-first.  False if no
 // entry was hit (the caller pops).
@@ -134,30 +108,6 @@ RT_HD bool visit4(const Rec4& R, const RayF& rf, const double hi, const double l
   const float hf = f_up_wide(hi), lf = f_down_wide(lo);
   float a0 = NOHIT, a1 = NOHIT, a2 = NOHIT, a3 = NOHIT;
   int r0 = 0, r1 = 0, r2 = 0, r3 = 0;
-#ifdef RTX_PACKED_RECORDS
-#error "RTX_PACKED_RECORDS: rework for the Rec4 operand (visit4 takes the loaded record)"
-
-  const int cnt = nd.count;
-  // Opt-in: two entries per packed float pair (box_cons32x2; entries past
-  // `count` are empty boxes, which the slab rule does not reject: masked
-  // here).  Measured 47.7 / 48.9 ms against 46.4 / 47.1 for the scalar
-  // tests on the headline frame: fewer instructions, more spills (192 B).
-  auto pair = [&](int p, float& ax, int& rx, float& ay, int& ry) {
-    rtx_f2 ta, tb;
-    box_cons32x2(nd, p, rf, ta, tb);
-#pragma unroll
-    for (int e = 0; e < 2; ++e) {
-      const int k = 2 * p + e;
-      if (STATS && k < cnt) C.nodes++;
-      if (k < cnt && !(ta[e] > tb[e]) && !(tb[e] < 0.0f) && !(ta[e] > hf) && !(tb[e] < lf)) {
-        (e ? ay : ax) = ta[e];
-        (e ? ry : rx) = nd.child[k];
-      }
-    }
-  };
-  pair(0, a0, r0, a1, r1);
-  pair(1, a2, r2, a3, r3);
-#else
   // the whole record in one burst of 16-byte loads before any test (the
   // caller issues them, load_rec4): the entries used to be loaded inside
   // their own `k < count` branches, up to nine dependent round trips per
@@ -180,7 +130,6 @@ RT_HD bool visit4(const Rec4& R, const RayF& rf, const double hi, const double l
   test(1, lx.y, ly.y, lz.y, hx.y, hy.y, hz.y, ch.y, a1, r1);
   test(2, lx.z, ly.z, lz.z, hx.z, hy.z, hz.z, ch.z, a2, r2);
   test(3, lx.w, ly.w, lz.w, hx.w, hy.w, hz.w, ch.w, a3, r3);
-#endif
   // sorting network on (entry distance, ref)
   auto cs = [](float& x, int& rx, float& y, int& ry) {
     const bool s = y < x;
@@ -208,22 +157,17 @@ RT_HD bool visit4(const Rec4& R, const RayF& rf, const double hi, const double l
 // box is missed: KdTree::intersectList starts with the root's bbox test).
 template <bool STATS, int QMODE>
 RT_HD bool trav_init(Trav& T, const DevScene& S, const dvec3& P, const dvec3& D, const double tp, const int rp,
-                     const int sq, const double tlimit, const double tblock, Counters& C) {
+                     const int sq, const double tlimit, Counters& C) {
   T.P = P;
   T.D = D;
   T.tp = tp;
   T.rp = rp;
   T.sq = sq;
   T.tlimit = tlimit;
-  T.tblock = tblock;
   T.bt = tlimit;
   T.bobj = INT_MAX;
   T.bsub = INT_MAX;
   T.have = false;
-  T.blocked = false;
-#if RTX_TEAM
-  T.team = 0;
-#endif
   if (QMODE != Q_ANY) T.closest = QMODE == Q_CLOSEST;  // Q_ANY: set by the caller first
   if (S.n_snodes == 0) return false;
   T.tlo = QMODE == Q_CLOSEST ? -RTX_INF : tp - S.margin;  // Q_ANY: tp = -inf for a closest query
@@ -260,13 +204,10 @@ RT_HD void trav_reset(Trav& T) {
   T.ri.inv = mk3(0.0, 0.0, 0.0);
   T.ri.fast = true;
   T.rf = RayF{0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-  T.tp = T.tlimit = T.tlo = T.tblock = T.bt = T.len = T.mbest = 0.0;
+  T.tp = T.tlimit = T.tlo = T.bt = T.len = T.mbest = 0.0;
   T.rp = T.sq = T.bobj = T.bsub = T.sp = T.ref = T.mode = T.oc = T.oe = 0;
   T.moi = T.mbase = T.mfoff = T.mnoff = T.mface = 0;
-  T.have = T.blocked = T.mhave = T.closest = false;
-#if RTX_TEAM
-  T.team = 0;
-#endif
+  T.have = T.mhave = T.closest = false;
 }
 
 // The lane's next unit is a 4-wide record (scene or mesh): the cheap step.
@@ -275,9 +216,8 @@ RT_HD void trav_reset(Trav& T) {
 RT_HD bool trav_at_record(const Trav& T) { return T.mode != 1 && T.ref >= 0; }
 
 // One unit of the walk; true when the query is complete.
-template <bool STATS, int QMODE, class Blocker>
-RT_HD bool trav_step(Trav& T, const DevScene& S, int* __restrict__ stk, const int lane, const Blocker& blocker,
-                     Counters& C) {
+template <bool STATS, int QMODE>
+RT_HD bool trav_step(Trav& T, const DevScene& S, int* __restrict__ stk, const int lane, Counters& C) {
   const bool closest = QMODE == Q_CLOSEST || (QMODE == Q_ANY && T.closest);
   const double tp = T.tp, tlimit = T.tlimit, tlo = T.tlo;
   const int rp = T.rp, sq = T.sq;
@@ -294,21 +234,8 @@ RT_HD bool trav_step(Trav& T, const DevScene& S, int* __restrict__ stk, const in
   if (T.mode != 1 && ref >= 0) {
     // the record's loads first, then the prune bounds (FP64) while they are
     // in flight (the scheduler used to place the loads after the bounds)
-    const DevNode4* recs = !mesh ? S.snode4 : (ref < S.n_mhot ? S.mhot : S.mnode4);
+    const DevNode4* recs = !mesh ? S.snode4 : S.mnode4;
     const Rec4 rec = load_rec4(recs[ref]);
-#ifdef RTX_AMP_LOADS
-    // (diagnostic: the record loaded a second time — L1 hits issued in the
-    // same burst — to tell memory-pipeline throughput from latency)
-    {
-      int zero = 0;
-      asm volatile("" : "+v"(zero));
-      const Rec4 r2 = load_rec4(recs[ref + zero]);
-      pin(r2.lx.x), pin(r2.ly.y), pin(r2.lz.z), pin(r2.hx.w), pin(r2.hy.x), pin(r2.hz.y), pin(r2.ch.z), pin(r2.nrec);
-    }
-#endif
-#ifdef RTX_EARLY_REC  // (measured: no gain, 33.16 vs 33.11-33.15 ms, profiles/r05e_ab_ident_early.txt)
-    sched_fence();
-#endif
     double hi = bt + S.margin, lo = tlo;
     if (mesh) {
       const double len = T.len;
@@ -379,16 +306,10 @@ RT_HD bool trav_step(Trav& T, const DevScene& S, int* __restrict__ stk, const in
               lt = t;
               ls = sb;
             }
-          } else if (!T.blocked) {
+          } else {
             const double tw = t / ln;
             if (key_less(tp, rp, sq, tw, oi, sb) && tw <= tlimit) {
-              if (tw < T.tblock && blocker(T, oi, sb)) {
-                bt = tw;
-                bobj = oi;
-                bsub = sb;
-                have = true;
-                T.blocked = true;
-              } else if (!have || key_less(tw, oi, sb, bt, bobj, bsub)) {
+              if (!have || key_less(tw, oi, sb, bt, bobj, bsub)) {
                 bt = tw;
                 bobj = oi;
                 bsub = sb;
@@ -515,7 +436,6 @@ RT_HD bool trav_step(Trav& T, const DevScene& S, int* __restrict__ stk, const in
             }
           }
         }
-        if (T.blocked) return true;
         if (closest && ls >= 0) {
           const double tw = lt / ln;
           if (!have || tw < bt || (tw == bt && oi < bobj)) {
@@ -546,36 +466,6 @@ RT_HD bool trav_step(Trav& T, const DevScene& S, int* __restrict__ stk, const in
     // strictly farther than the mesh's best; next: farther than the
     // current best key) — tri_hit stops before the edge tests
     const double tcap = closest && T.mhave ? rtm::gmin(whi, T.mbest) : whi;
-#ifdef RTX_TRI_PRE
-    // Opt-in: the leaf's faces as floats in one burst (3 x 48 B; a leaf of
-    // fewer faces loads its last one again), the conservative float
-    // prefilter on each (tri_pre), and the exact FP64 tri_hit only on the
-    // faces it cannot reject — the double face (96 B) then, not for every
-    // face.  Exact (tests/test_record_test_host.py) but measured slower:
-    // headline 33.9-34.1 vs 33.2-33.4 ms, R1 265-267 vs 255 ms
-    // (profiles/r05h_ab_tri_pre.txt) — the kernels are bound neither by the
-    // FP64 face tests nor by the faces' round trips.
-    const FaceF* ff = S.tfacef + T.mfoff + f0;
-    const int nf = f1 - f0;
-    const FaceF q0 = ff[0], q1 = ff[nf > 1 ? 1 : 0], q2 = ff[nf > 2 ? 2 : 0];
-    const RayTF rt = ray_tf(T.lp, T.ld, S.mext);
-    const float tcf = f_up_wide(tcap);
-    unsigned int surv = (tri_pre(q0.a, q0.b, q0.c, rt, tcf) ? 1u : 0u) |
-                        (nf > 1 && tri_pre(q1.a, q1.b, q1.c, rt, tcf) ? 2u : 0u) |
-                        (nf > 2 && tri_pre(q2.a, q2.b, q2.c, rt, tcf) ? 4u : 0u);
-    const int rk0 = __builtin_bit_cast(int, q0.a.w), rk1 = __builtin_bit_cast(int, q1.a.w),
-              rk2 = __builtin_bit_cast(int, q2.a.w);
-    const int lf0 = __builtin_bit_cast(int, q0.b.w), lf1 = __builtin_bit_cast(int, q1.b.w),
-              lf2 = __builtin_bit_cast(int, q2.b.w);
-    if (STATS) C.tris += nf;
-    while (surv) {
-      const int k = __builtin_ctz(surv);
-      surv &= surv - 1;
-      const int f = f0 + k;
-      double tf;
-      const bool hit = tri_hit(S.tfaces[T.mfoff + f], T.lp, T.ld, tcap, tf);
-      const TMeta meta = {k == 0 ? rk0 : (k == 1 ? rk1 : rk2), k == 0 ? lf0 : (k == 1 ? lf1 : lf2)};
-#else
     for (int f = f0; f < f1; ++f) {
       if (STATS) C.tris++;
       double tf;
@@ -585,7 +475,6 @@ RT_HD bool trav_step(Trav& T, const DevScene& S, int* __restrict__ stk, const in
       const bool hit = tri_hit(S.tfaces[T.mfoff + f], T.lp, T.ld, tcap, tf);
       pin(meta.rank);
       pin(meta.leaf);
-#endif
       if (hit) {
         const int rk = meta.rank;
         if (closest) {
@@ -597,14 +486,6 @@ RT_HD bool trav_step(Trav& T, const DevScene& S, int* __restrict__ stk, const in
         } else {
           const double tw = tf / len;
           if (key_less(tp, rp, sq, tw, T.moi, rk) && tw <= tlimit && leaf_ok(T, S, meta.leaf)) {
-            if (tw < T.tblock && blocker(T, T.moi, rk)) {
-              bt = tw;
-              bobj = T.moi;
-              bsub = rk;
-              have = true;
-              T.blocked = true;
-              return true;
-            }
             if (!have || key_less(tw, T.moi, rk, bt, bobj, bsub)) {
               bt = tw;
               bobj = T.moi;
@@ -621,15 +502,6 @@ RT_HD bool trav_step(Trav& T, const DevScene& S, int* __restrict__ stk, const in
     ref = stk[sp * 64 + lane];
     return false;
   }
-#if RTX_TEAM
-  if (T.team != 0) {
-    // a helper's subtree is done (the wave merges its minimum into the
-    // owner's); an owner waits here, at its mesh's end, for its helpers
-    if (T.team & TEAM_HELPER) return true;
-    ref = ~0;  // an empty leaf: the next steps come back here
-    return false;
-  }
-#endif
   // mesh finished: Trimesh::intersectLocal's result enters Scene::intersect
   T.rf = ray_f(T.P, T.D, T.ri);
   if (closest && T.mhave) {
@@ -652,150 +524,6 @@ RT_HD bool trav_step(Trav& T, const DevScene& S, int* __restrict__ stk, const in
   return false;
 }
 
-#if RTX_TEAM
-// Teams.  A query's answer is a minimum under a total order — the closest
-// hit: per mesh the (t, face rank)-smallest face passing leaf_ok; the next
-// hit: the (t, object, sub)-smallest key after the previous one — and every
-// pruning bound only drops candidates that cannot be that minimum.  So a
-// pending subtree of a lane's mesh walk (an entry of its stack above
-// T.mbase) can be walked by another lane with a copy of the ray, the bounds
-// and the best so far, and the two minima merged: the answer is the same
-// candidate ("Teams").
-//
-// team_donate (wave-uniform, when the wave's query list is exhausted): the
-// k-th lane without an active query takes the bottom mesh entry (the largest
-// pending subtree: entries are pushed farthest-first, deeper ones above) of
-// the k-th lane walking a mesh with entries left; the owner moves its top
-// entry into the hole.  A helper that holds a finished answer (pend) parks it
-// in the TEAM_STASH top entries of its own stack column (a mesh walk from a
-// subtree needs at most stack_cap - TEAM_STASH entries, host-sized).
-__device__ inline void team_donate(Trav& T, int* __restrict__ stk, const int lane, bool& active, const int stash) {
-  const unsigned long long idle = __ballot(!active);
-  if (idle == 0ull) return;
-  const unsigned long long dmask =
-      __ballot(active && !(T.team & TEAM_HELPER) && T.mode == 2 && T.sp > T.mbase);
-  if (dmask == 0ull) return;
-  int src = lane;
-  bool newh = false, give = false;
-  unsigned long long im = idle, dm = dmask;
-  while (im != 0ull && dm != 0ull) {
-    const int h = __builtin_ctzll(im), d = __builtin_ctzll(dm);
-    im &= im - 1ull;
-    dm &= dm - 1ull;
-    if (lane == h) {
-      src = d;
-      newh = true;
-    }
-    if (lane == d) give = true;
-  }
-  int e = 0;
-  if (give) {
-    const int b = T.mbase;
-    e = stk[b * 64 + lane];
-    stk[b * 64 + lane] = stk[(T.sp - 1) * 64 + lane];
-    T.sp--;
-    T.team += 256;
-  }
-  if (newh) {
-    stk[(stash + 0) * 64 + lane] = T.have ? 1 : 0;
-    stk[(stash + 1) * 64 + lane] = __double2loint(T.bt);
-    stk[(stash + 2) * 64 + lane] = __double2hiint(T.bt);
-    stk[(stash + 3) * 64 + lane] = T.bobj;
-    stk[(stash + 4) * 64 + lane] = T.bsub;
-  }
-  // the owner's ray (mesh frame), bounds and best so far; identity elsewhere
-  e = __shfl(e, src);
-#pragma unroll
-  for (int a = 0; a < 3; ++a) {
-    T.rf.olo[a] = __shfl(T.rf.olo[a], src);
-    T.rf.ohi[a] = __shfl(T.rf.ohi[a], src);
-    T.rf.inv[a] = __shfl(T.rf.inv[a], src);
-  }
-  T.rf.err = __shfl(T.rf.err, src);
-  T.lp.x = __shfl(T.lp.x, src);
-  T.lp.y = __shfl(T.lp.y, src);
-  T.lp.z = __shfl(T.lp.z, src);
-  T.ld.x = __shfl(T.ld.x, src);
-  T.ld.y = __shfl(T.ld.y, src);
-  T.ld.z = __shfl(T.ld.z, src);
-  T.tp = __shfl(T.tp, src);
-  T.tlimit = __shfl(T.tlimit, src);
-  T.tlo = __shfl(T.tlo, src);
-  T.rp = __shfl(T.rp, src);
-  T.sq = __shfl(T.sq, src);
-  T.bt = __shfl(T.bt, src);
-  T.bobj = __shfl(T.bobj, src);
-  T.bsub = __shfl(T.bsub, src);
-  T.have = __shfl(T.have ? 1 : 0, src) != 0;
-  T.len = __shfl(T.len, src);
-  T.mbest = __shfl(T.mbest, src);
-  T.moi = __shfl(T.moi, src);
-  T.mfoff = __shfl(T.mfoff, src);
-  T.mnoff = __shfl(T.mnoff, src);
-  T.mface = __shfl(T.mface, src);
-  T.mhave = __shfl(T.mhave ? 1 : 0, src) != 0;
-  T.closest = __shfl(T.closest ? 1 : 0, src) != 0;
-  if (newh) {
-    T.ref = e;
-    T.sp = 0;
-    T.mbase = 0;
-    T.mode = 2;
-    T.oc = T.oe = 0;
-    T.blocked = false;
-    T.team = TEAM_HELPER | src;
-    active = true;
-  }
-}
-
-// Helpers whose subtree is done (hdone) merge their minimum into their
-// owner's — closest: the mesh's best face (the owner waits at its mesh's
-// end, so the merge is at mesh level, with the face-rank tie rule); next
-// hit: the key — and take their own answer back from the stash.
-__device__ inline void team_merge(Trav& T, const int* __restrict__ stk, const int lane, const bool hdone, const bool closest,
-                      const int stash) {
-  unsigned long long hm = __ballot(hdone);
-  while (hm != 0ull) {
-    const int h = __builtin_ctzll(hm);
-    hm &= hm - 1ull;
-    const int o = __builtin_amdgcn_readlane(T.team & 63, h);
-    if (closest) {
-      const bool hh = __builtin_amdgcn_readlane(T.mhave ? 1 : 0, h) != 0;
-      const double hb = __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(T.mbest), h),
-                                         __builtin_amdgcn_readlane(__double2loint(T.mbest), h));
-      const int hf = __builtin_amdgcn_readlane(T.mface, h);
-      if (lane == o) {
-        if (hh && (!T.mhave || hb < T.mbest || (hb == T.mbest && hf < T.mface))) {
-          T.mbest = hb;
-          T.mface = hf;
-          T.mhave = true;
-        }
-        T.team -= 256;
-      }
-    } else {
-      const bool hh = __builtin_amdgcn_readlane(T.have ? 1 : 0, h) != 0;
-      const double hb = __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(T.bt), h),
-                                         __builtin_amdgcn_readlane(__double2loint(T.bt), h));
-      const int ho = __builtin_amdgcn_readlane(T.bobj, h), hs = __builtin_amdgcn_readlane(T.bsub, h);
-      if (lane == o) {
-        if (hh && (!T.have || key_less(hb, ho, hs, T.bt, T.bobj, T.bsub))) {
-          T.bt = hb;
-          T.bobj = ho;
-          T.bsub = hs;
-          T.have = true;
-        }
-        T.team -= 256;
-      }
-    }
-  }
-  if (hdone) {
-    T.have = stk[(stash + 0) * 64 + lane] != 0;
-    T.bt = __hiloint2double(stk[(stash + 2) * 64 + lane], stk[(stash + 1) * 64 + lane]);
-    T.bobj = stk[(stash + 3) * 64 + lane];
-    T.bsub = stk[(stash + 4) * 64 + lane];
-    T.team = 0;
-  }
-}
-#endif
 
 // One query to completion (no shadow early-out).
 template <bool STATS>
@@ -803,14 +531,13 @@ RT_HD bool traverse(const DevScene& S, const int qmode, const dvec3& P, const dv
                     const int sq, const double tlimit, double& bt, int& bobj, int& bsub, int* __restrict__ stk,
                     const int lane, Counters& C) {
   Trav T;
-  const NoBlocker nb;
   if (qmode == Q_CLOSEST) {
-    if (trav_init<STATS, Q_CLOSEST>(T, S, P, D, tp, rp, sq, tlimit, -RTX_INF, C))
-      while (!trav_step<STATS, Q_CLOSEST>(T, S, stk, lane, nb, C)) {
+    if (trav_init<STATS, Q_CLOSEST>(T, S, P, D, tp, rp, sq, tlimit, C))
+      while (!trav_step<STATS, Q_CLOSEST>(T, S, stk, lane, C)) {
       }
   } else {
-    if (trav_init<STATS, Q_NEXT>(T, S, P, D, tp, rp, sq, tlimit, -RTX_INF, C))
-      while (!trav_step<STATS, Q_NEXT>(T, S, stk, lane, nb, C)) {
+    if (trav_init<STATS, Q_NEXT>(T, S, P, D, tp, rp, sq, tlimit, C))
+      while (!trav_step<STATS, Q_NEXT>(T, S, stk, lane, C)) {
       }
   }
   bt = T.bt;
@@ -826,10 +553,9 @@ RT_HD bool traverse_any(const DevScene& S, const int qmode, const dvec3& P, cons
                         const int rp, const int sq, const double tlimit, double& bt, int& bobj, int& bsub,
                         int* __restrict__ stk, const int lane, Counters& C) {
   Trav T;
-  const NoBlocker nb;
   T.closest = qmode == Q_CLOSEST;
-  if (trav_init<STATS, Q_ANY>(T, S, P, D, T.closest ? -RTX_INF : tp, rp, sq, tlimit, -RTX_INF, C))
-    while (!trav_step<STATS, Q_ANY>(T, S, stk, lane, nb, C)) {
+  if (trav_init<STATS, Q_ANY>(T, S, P, D, T.closest ? -RTX_INF : tp, rp, sq, tlimit, C))
+    while (!trav_step<STATS, Q_ANY>(T, S, stk, lane, C)) {
     }
   bt = T.bt;
   bobj = T.bobj;
@@ -947,8 +673,8 @@ inline TBox tbox_empty() {
 }
 
 // Binned SAH over item boxes (defaults: 16 bins, traversal cost 1.2 per node
-// against 1 per item; SahParams, A/B switches RTX_SAH_BINS / RTX_SAH_NODE /
-// RTX_SAH_ITEM / RTX_SAH_LEAF read by build_trav_trees).  Emits nodes in DFS
+// against 1 per item, SahParams; other settings measured within noise,
+// profiles/r04u_sah_sweep.txt).  Emits nodes in DFS
 // pre-order (child0 = i + 1, right), leaves [first, first + count) into
 // `order`, a permutation of the items.
 struct SahParams {
@@ -1070,15 +796,13 @@ struct TravTrees {
   std::vector<RtxFace> tfaces;
   std::vector<int32_t> trank;
   std::vector<TMeta> tmeta;
-  std::vector<FaceF> tfacef;    // tfaces as floats + rank / leaf (tri_pre)
   std::vector<RtxObject> objs;  // the objects with their mesh fields in pad (augment_objects)
   int sneed = 0, mneed = 0;
-  int n_mhot = 0;  // mesh records [0, n_mhot) are the hot ones (renumbered first)
 };
 
 // Renumber the mesh records so the hottest come first — every mesh's root
-// record, then their children while `cap` allows — for kernels that stage
-// [0, n_mhot) in LDS (every walk into a mesh starts there).
+// record, then their children while `cap` allows — so every walk into a mesh
+// starts on a few densely packed cache lines.
 inline void hot_mesh_records(TravTrees& T, int cap) {
   const int n = static_cast<int>(T.mn4.size());
   std::vector<int> hot;
@@ -1110,7 +834,6 @@ inline void hot_mesh_records(TravTrees& T, int cap) {
   T.mn4.swap(out);
   for (DevRoot& mr : T.mroots)
     if (mr.ref >= 0 && mr.ref < n) mr.ref = remap[size_t(mr.ref)];
-  T.n_mhot = static_cast<int>(hot.size());
 }
 
 // The device copy of the objects: a trimesh's mesh fields (face_off,
@@ -1128,25 +851,15 @@ inline void augment_objects(const RtxSceneDesc* d, std::vector<RtxObject>& objs)
     o.pad[RTX_OBJ_MFLAGS] = (me.node_count > 0 ? RTX_MESH_TREE : 0) | (me.has_normals ? RTX_MESH_NORMALS : 0) |
                             (me.has_vmats ? RTX_MESH_VMATS : 0);
   }
-  for (RtxObject& o : objs) {  // identity M^-1 (obj_local)
-    static const double id[12] = {1, 0, 0, 0, 1, 0, 0, 0, 1, 0, 0, 0};
-    bool ident = true;
-    for (int k = 0; k < 12; ++k) ident = ident && o.inv[k] == id[k] && !std::signbit(o.inv[k]);
-    if (ident) o.pad[RTX_OBJ_MFLAGS] |= RTX_OBJ_IDENT;
-  }
 }
 
 inline bool build_trav_trees(const RtxSceneDesc* d, TravTrees& T) {
   std::memset(&T.sroot, 0, sizeof(T.sroot));
   augment_objects(d, T.objs);
-  // mesh-tree SAH parameters (A/B switches; the walk's results do not depend
-  // on the tree, DESIGN.md "Traversal trees")
-  SahParams sp;
-  int mesh_leaf = 3;
-  if (const char* e = getenv("RTX_SAH_BINS")) sp.bins = atoi(e);
-  if (const char* e = getenv("RTX_SAH_NODE")) sp.c_node = atof(e);
-  if (const char* e = getenv("RTX_SAH_ITEM")) sp.c_item = atof(e);
-  if (const char* e = getenv("RTX_SAH_LEAF")) mesh_leaf = std::min(3, std::max(1, atoi(e)));  // (leaf codes hold <= 3)
+  // mesh-tree SAH parameters (the walk's results do not depend on the tree,
+  // DESIGN.md "Traversal trees")
+  const SahParams sp;
+  const int mesh_leaf = 3;  // leaf codes hold <= 3 faces
   std::vector<RtxNode> nodes;
   std::vector<int> order;
   std::vector<TBox> boxes;
@@ -1170,7 +883,6 @@ inline bool build_trav_trees(const RtxSceneDesc* d, TravTrees& T) {
   T.tfaces.assign(size_t(d->n_faces), RtxFace());
   T.trank.assign(size_t(d->n_faces), 0);
   T.tmeta.assign(size_t(d->n_faces), TMeta{0, 0});
-  T.tfacef.assign(size_t(d->n_faces), FaceF{});
   for (int m = 0; m < d->n_meshes; ++m) {
     const RtxMesh& me = d->meshes[m];
     std::memset(&T.mroots[size_t(m)], 0, sizeof(DevRoot));
@@ -1188,14 +900,6 @@ inline bool build_trav_trees(const RtxSceneDesc* d, TravTrees& T) {
       T.tfaces[size_t(me.face_off + j)] = d->faces[me.face_off + order[size_t(j)]];
       T.trank[size_t(me.face_off + j)] = order[size_t(j)];
       T.tmeta[size_t(me.face_off + j)] = TMeta{order[size_t(j)], me.node_off + d->face_ids[me.face_off + order[size_t(j)]].leaf};
-    }
-    for (int j = 0; j < me.face_count; ++j) {  // the float copy for tri_pre (rounded to nearest)
-      const RtxFace& F = T.tfaces[size_t(me.face_off + j)];
-      const TMeta& tm = T.tmeta[size_t(me.face_off + j)];
-      FaceF& q = T.tfacef[size_t(me.face_off + j)];
-      q.a = make_float4(float(F.v0[0]), float(F.v0[1]), float(F.v0[2]), __builtin_bit_cast(float, tm.rank));
-      q.b = make_float4(float(F.v1[0]), float(F.v1[1]), float(F.v1[2]), __builtin_bit_cast(float, tm.leaf));
-      q.c = make_float4(float(F.v2[0]), float(F.v2[1]), float(F.v2[2]), 0.0f);
     }
     int need = 0;
     if (!build_node4(nodes.data(), static_cast<int>(nodes.size()), T.mn4, T.mroots[size_t(m)], need)) return false;
@@ -1235,14 +939,5 @@ inline double mesh_extent(const RtxSceneDesc* d) {
   return e;
 }
 
-// tri_pre's bound on every mesh-local vertex coordinate, as a float rounded
-// up: the largest |coordinate| of any face vertex (every vertex, whether or
-// not a mesh tree holds it)
-inline float mesh_extent_f(const RtxSceneDesc* d) {
-  double e = 1.0;
-  for (int f = 0; f < d->n_faces; ++f)
-    for (int k = 0; k < 3; ++k) e = fmax(e, fmax(fabs(d->faces[f].v0[k]), fmax(fabs(d->faces[f].v1[k]), fabs(d->faces[f].v2[k]))));
-  return round_up_f(e);
-}
 
 }  // namespace rtxd

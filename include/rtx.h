@@ -272,8 +272,9 @@ rtx_status rtx_shard_pixels(const RtxRenderParams* params, int64_t* npixels);
 #define RTX_WORK_COUNT 15
 rtx_status rtx_last_work(void* scene, int64_t* out, int n);
 
-/* Device time (ms) of render kernels launched since the last call, read
- * from hipEvents recorded on the render stream; synchronizes those events. */
+/* Device time (ms) of the renders since the last call, read from hipEvents
+ * recorded on the render stream (synchronizes those events), and the number
+ * of kernels those renders launched (every launch of the render path). */
 rtx_status rtx_kernel_time(void* scene, double* total_ms, int* launches);
 
 /* Outcome of the asynchronous (device-buffer) renders issued so far on this

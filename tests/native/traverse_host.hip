@@ -29,8 +29,6 @@ bool make_scene(const RtxSceneDesc* d, HostScene& H) {
   S.sroot = H.T.sroot;
   S.snode4 = H.T.sn4.data();
   S.mnode4 = H.T.mn4.data();
-  S.mhot = S.mnode4;
-  S.n_mhot = H.T.n_mhot;
   S.n_srec = static_cast<int32_t>(H.T.sn4.size());
   S.mroots = H.T.mroots.data();
   S.tfaces = H.T.tfaces.data();
@@ -38,8 +36,6 @@ bool make_scene(const RtxSceneDesc* d, HostScene& H) {
   S.snodes = d->scene_nodes;
   S.objs = H.T.objs.data();  // with the mesh fields in pad (augment_objects)
   S.tmeta = H.T.tmeta.data();
-  S.tfacef = H.T.tfacef.data();
-  S.mext = mesh_extent_f(d);
   S.oprm = d->obj_params;
   S.mats = d->materials;
   S.meshes = d->meshes;
@@ -140,40 +136,6 @@ int rec_test_host(int32_t n, const double* P, const double* D, const double* box
     float a, b;
     ok[k] = box_cons32(nd, 0, rf, a, b) ? 1 : 0;
     a_out[k] = a;
-  }
-  return 0;
-}
-
-// The face prefilter (tri_pre, as the leaf step runs it) against the exact
-// tri_hit on n (ray, face, tcap) cases: face k = 9 doubles (v0, v1, v2), its
-// normal computed as the loader does (normalize(cross(v1 - v0, v2 - v0)),
-// scene_build.cpp), the float copy rounded to nearest, mext from the face's
-// own vertices.  pre[k] = tri_pre's verdict (0: certainly rejected),
-// exact[k] = tri_hit's.  The test requires exact => pre.
-int tri_pre_host(int32_t n, const double* P, const double* D, const double* V, const double* tcap, int32_t* pre,
-                 int32_t* exact) {
-  for (int32_t k = 0; k < n; ++k) {
-    const dvec3 p = mk3(P[3 * k], P[3 * k + 1], P[3 * k + 2]);
-    const dvec3 d = mk3(D[3 * k], D[3 * k + 1], D[3 * k + 2]);
-    RtxFace F;
-    for (int q = 0; q < 3; ++q) {
-      F.v0[q] = V[9 * k + q];
-      F.v1[q] = V[9 * k + 3 + q];
-      F.v2[q] = V[9 * k + 6 + q];
-    }
-    const dvec3 n0 = rtm::normalize(rtm::cross(ld3(F.v1) - ld3(F.v0), ld3(F.v2) - ld3(F.v0)));
-    F.n[0] = n0.x;
-    F.n[1] = n0.y;
-    F.n[2] = n0.z;
-    double e = 1.0;
-    for (int q = 0; q < 9; ++q) e = fmax(e, fabs(V[9 * k + q]));
-    const float mext = round_up_f(e);
-    const float4 fa = make_float4(float(F.v0[0]), float(F.v0[1]), float(F.v0[2]), 0.f);
-    const float4 fb = make_float4(float(F.v1[0]), float(F.v1[1]), float(F.v1[2]), 0.f);
-    const float4 fc = make_float4(float(F.v2[0]), float(F.v2[1]), float(F.v2[2]), 0.f);
-    pre[k] = tri_pre(fa, fb, fc, ray_tf(p, d, mext), f_up_wide(tcap[k])) ? 1 : 0;
-    double tf;
-    exact[k] = tri_hit(F, p, d, tcap[k], tf) ? 1 : 0;
   }
   return 0;
 }

@@ -106,3 +106,29 @@ def test_c5_band_parity(pkg, orc):
                 ref["hits"][y0:y1])
     print("c5_band", m)
     assert_parity(m)
+
+
+@pytest.mark.parametrize("nshards", [8, 2])
+def test_r1_shards_equal_whole_frame(pkg, nshards):
+    """R1 (the glass frame, whose fork requests outgrow its spare slots) at
+    full size: every sampled shard of an N-way multi-GPU deal renders its tiles
+    bit for bit as the whole frame does.  The fork depth (4 or 3: the line
+    between bucket sums and the running sum, f64 last bits) is decided per
+    frame from its own fork requests against a size-independent share of its
+    samples, so a 33-M-unit whole frame (50 % spares) and its 4-M / 16-M-unit
+    shards (100 % spares) agree (RayTracer.cpp:283-314)."""
+    path = scene_path("trimesh2_glass.ray")
+    opts = cli_opts(pkg, "-w 1920 -r 5 -O r -A 4")
+    host = pkg.HostScene(path)
+    dev = pkg.DeviceScene(host, 0)
+    full = dev.render(opts, want_f64=True)
+    h, w, T = full["height"], opts.width, 16
+    for shard in sorted({0, nshards - 1}):
+        part = dev.render(opts, want_f64=True, tile=T, shard=shard, nshards=nshards, packed=True)
+        outf = np.full((h, w, 3), np.nan)
+        pkg.unpack_tiles(part["rgb"], w, h, T, shard, nshards, outf)
+        own = ~np.isnan(outf[..., 0])
+        assert own.sum() > 0
+        diff = own & (outf != full["rgb"]).any(axis=2)
+        assert not diff.any(), f"shard {shard}/{nshards}: {int(diff.sum())} pixels differ from the whole frame"
+    dev.close()

@@ -150,13 +150,17 @@ def test_repeat_deterministic(pkg):
     ("trimesh2.ray", "-w 128 -r 5 -O r -A 4", 32, 3),
     ("trimesh2.ray", "-w 64 -r 5 -O d -A 2.5 -B 4 -C 0.05", 0, 1),
     # the headline frame at full size, as two 16.6M-unit shards (the largest
-    # frames that overlap on the frame contexts by default): eight frames,
-    # four per shard, alternating contexts
+    # frames that overlap on the frame contexts by default; two contexts
+    # above 10 M units): eight frames, four per shard, alternating contexts
     ("trimesh2.ray", "-w 1920 -r 5 -O r -A 4", 32, 2),
-], ids=["glass", "tiles3", "dof", "headline_full_x2"])
+    # ... and as four 8.3M-unit shards: three contexts (frames of at most
+    # 10 M units), so the third context's buffers are checked at full size
+    ("trimesh2.ray", "-w 1920 -r 5 -O r -A 4", 16, 4),
+], ids=["glass", "tiles3", "dof", "headline_full_x2", "headline_full_x4"])
 def test_pipelined_frames_identical(pkg, scene, flags, tile, nshards):
-    """Renders into device buffers alternate between the scene's two frame
-    contexts and overlap each other (rtx_render: frame contexts).  Eight such
+    """Renders into device buffers rotate over the scene's frame contexts
+    (three on frames of at most 10 M work units, two on larger ones) and
+    overlap each other (rtx_render: frame contexts).  Eight such
     frames queued back to back — each shard more than once, into separate
     buffers, on one stream, one synchronisation at the end — must each equal
     the stream-ordered host-mode render of the same shard byte for byte (and
@@ -410,13 +414,13 @@ def test_wrong_frame_never_ok(pkg, capfd, monkeypatch, knob):
 
 @pytest.mark.gpu
 def test_fork_depth_from_history(pkg, orc, capfd, monkeypatch):
-    """A frame whose fork requests outgrow its spare slots (the glass scene,
+    """A frame whose ray trees fork at many of their nodes (the glass scene,
     R1's) forks down to heap depth 3 under the lower frame-memory cap
-    (rtx_render, "forks outgrow the spares").  The depth changes the f64
-    image in the last bit, so the frame's first render — which finds out —
-    is rendered again at depth 3 before it returns: every render of the frame,
-    host-mode or into device buffers, must be the same bytes, and match the
-    CPU restatement."""
+    (run_wavefront, "forks outgrow the spares").  The depth changes the f64
+    image in the last bit, so it is decided once per whole frame before its
+    first render (depth_probe: a fixed subset of the whole frame at the
+    default depth): every render of the frame, host-mode or into device
+    buffers, must be the same bytes, and match the CPU restatement."""
     import ctypes as C
 
     if os.environ.get("RTX_FORK") == "0" or os.environ.get("RTX_FORK_DEPTH") or os.environ.get("RTX_FUSE") == "0":
@@ -462,8 +466,9 @@ def test_fork_depth_from_history(pkg, orc, capfd, monkeypatch):
 
 @pytest.mark.gpu
 def test_fork_depth_first_render_is_depth3(pkg, capfd, monkeypatch):
-    """The first render of a frame whose forks outgrow the spares is itself
-    the depth-3 image: equal, in f64, to a render with RTX_FORK_DEPTH=3."""
+    """The first render of a frame whose ray trees fork at many nodes is
+    itself the depth-3 image: equal, in f64, to a render with
+    RTX_FORK_DEPTH=3."""
     if os.environ.get("RTX_FORK") == "0" or os.environ.get("RTX_FORK_DEPTH") or os.environ.get("RTX_FUSE") == "0":
         pytest.skip("no forks / a fixed fork depth / the sequential machine (its own fork counts) in this mode")
     scene, flags = "trimesh2_glass.ray", "-w 64 -r 5 -O r -A 4"

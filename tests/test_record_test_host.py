@@ -160,84 +160,3 @@ def test_prune_bounds_widen(pkg):
     fin = np.isfinite(up) & (np.abs(x) > 1e-30) & (np.abs(x) < 1e38)
     rel = (up[fin].astype(np.float64) - x[fin]) / np.abs(x[fin])
     assert rel.max() < 2.0 ** -20
-
-
-def _tri_cases(rng, n):
-    """Adversarial (ray, triangle, tcap) cases for the face prefilter: rays
-    aimed at a vertex, at a point of an edge, just inside / outside an edge
-    (a few ulps to 1e-4 of the edge length), at the interior; near-parallel
-    rays; origins near and far (up to 1e4 from a face of size 1e-3 .. 10),
-    faces far from the origin of coordinates; tcap at, just under and just
-    over the plane distance."""
-    P, D, V, T = [], [], [], []
-    for _ in range(n):
-        scale = 10.0 ** rng.uniform(-3, 1)
-        centre = rng.normal(size=3) * 10.0 ** rng.uniform(-2, 3)
-        tri = centre + rng.normal(size=(3, 3)) * scale
-        kind = rng.integers(0, 6)
-        w = rng.dirichlet([1, 1, 1])
-        if kind == 0:  # a vertex
-            target = tri[rng.integers(0, 3)]
-        elif kind in (1, 2):  # on / near an edge
-            i = rng.integers(0, 3)
-            a, b = tri[i], tri[(i + 1) % 3]
-            s = rng.uniform(0, 1)
-            edge_pt = a + s * (b - a)
-            inward = tri[(i + 2) % 3] - edge_pt
-            eps = 0.0 if kind == 1 else rng.choice([-1, 1]) * 10.0 ** rng.uniform(-16, -4)
-            target = edge_pt + eps * inward
-        else:
-            target = w @ tri
-        dist = 10.0 ** rng.uniform(-4, 4)
-        d = rng.normal(size=3)
-        if kind == 5:  # near-parallel to the plane
-            nrm = np.cross(tri[1] - tri[0], tri[2] - tri[0])
-            nrm /= np.linalg.norm(nrm)
-            d = d - (d @ nrm) * nrm + nrm * 10.0 ** rng.uniform(-12, -2)
-        d /= np.linalg.norm(d)
-        o = target - dist * d
-        if rng.uniform() < 0.2:
-            o = target + dist * d  # the face behind the ray
-        tc = np.inf
-        r = rng.uniform()
-        if r < 0.3:
-            tc = dist * (1.0 + rng.choice([-1, 1]) * 10.0 ** rng.uniform(-15, -3))
-        elif r < 0.4:
-            tc = dist
-        P.append(o), D.append(d), V.append(tri.ravel()), T.append(tc)
-    return (np.array(P, np.float64), np.array(D, np.float64), np.array(V, np.float64), np.array(T, np.float64))
-
-
-def test_face_prefilter_is_conservative(pkg):
-    """tri_pre (rtx_device.h) never rejects a face the exact FP64 tri_hit
-    accepts (so the walk's answers are unchanged), and it does reject the
-    clear misses (most of them)."""
-    L = _harness(pkg)
-    L.tri_pre_host.argtypes = [C.c_int32] + [C.c_void_p] * 6
-    rng = np.random.default_rng(20261018)
-    P, D, V, T = _tri_cases(rng, 200000)
-    n = P.shape[0]
-    pre = np.zeros(n, np.int32)
-    ex = np.zeros(n, np.int32)
-    assert L.tri_pre_host(n, P.ctypes.data, D.ctypes.data, V.ctypes.data, T.ctypes.data, pre.ctypes.data,
-                          ex.ctypes.data) == 0
-    bad = np.nonzero((ex == 1) & (pre == 0))[0]
-    assert len(bad) == 0, f"{len(bad)} exact hits rejected by tri_pre, first {bad[:5]}"
-    assert ex.sum() > 1000 and (ex == 0).sum() > 1000
-    # clear misses: rays aimed at a random point well outside the face
-    rng = np.random.default_rng(7)
-    tri = rng.normal(size=(20000, 3, 3))
-    far = tri.mean(axis=1) + 5.0 * rng.normal(size=(20000, 3))
-    d = rng.normal(size=(20000, 3))
-    d /= np.linalg.norm(d, axis=1, keepdims=True)
-    o = far - 10.0 * d
-    T2 = np.full(20000, np.inf)
-    pre2 = np.zeros(20000, np.int32)
-    ex2 = np.zeros(20000, np.int32)
-    V2 = np.ascontiguousarray(tri.reshape(20000, 9))
-    o, d = np.ascontiguousarray(o), np.ascontiguousarray(d)
-    assert L.tri_pre_host(20000, o.ctypes.data, d.ctypes.data, V2.ctypes.data, T2.ctypes.data, pre2.ctypes.data,
-                          ex2.ctypes.data) == 0
-    assert not ((ex2 == 1) & (pre2 == 0)).any()
-    miss = ex2 == 0
-    assert pre2[miss].mean() < 0.05, f"prefilter passes {pre2[miss].mean():.3f} of the clear misses"
