@@ -17,27 +17,11 @@
 #include <math.h>
 #include <stdint.h>
 
-#if defined(__HIPCC__)
-#include <hip/hip_runtime.h>
-#define RT_HD __host__ __device__ __forceinline__
-#else
-#define RT_HD inline
-#endif
+#include "rt_types.h"
 
 namespace rtm {
 
-struct dvec2 {
-  double x, y;
-};
-
-struct dvec3 {
-  double x, y, z;
-  RT_HD double operator[](int i) const { return i == 0 ? x : (i == 1 ? y : z); }
-};
-
-RT_HD dvec3 mk3(double x, double y, double z) { dvec3 r; r.x = x; r.y = y; r.z = z; return r; }
 RT_HD dvec3 splat3(double s) { return mk3(s, s, s); }
-RT_HD dvec2 mk2(double x, double y) { dvec2 r; r.x = x; r.y = y; return r; }
 
 RT_HD double get(const dvec3& v, int i) { return i == 0 ? v.x : (i == 1 ? v.y : v.z); }
 RT_HD void set(dvec3& v, int i, double s) {

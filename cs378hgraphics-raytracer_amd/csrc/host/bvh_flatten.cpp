@@ -25,6 +25,7 @@
 #include "../../../include/rtx_host.h"
 #include "raw_records.h"
 #include "scene_model.h"
+#include "../common/rt_math.h"
 
 namespace rtxh {
 namespace {

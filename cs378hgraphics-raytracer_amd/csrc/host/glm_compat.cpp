@@ -10,6 +10,7 @@
 #include <cmath>
 
 #include "scene_model.h"
+#include "../common/rt_math.h"
 
 namespace rtxh {
 

@@ -22,6 +22,7 @@
 #include <sstream>
 
 #include "scene_model.h"
+#include "../common/rt_math.h"
 
 namespace rtxh {
 

@@ -20,6 +20,7 @@
 #include <fstream>
 
 #include "scene_model.h"
+#include "../common/rt_math.h"
 
 namespace rtxh {
 

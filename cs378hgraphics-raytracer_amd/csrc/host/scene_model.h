@@ -14,7 +14,7 @@
 #include <string>
 #include <vector>
 
-#include "../common/rt_math.h"
+#include "../common/rt_types.h"
 
 namespace rtxh {
 

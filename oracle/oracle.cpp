@@ -23,6 +23,7 @@
 
 #include "../cs378hgraphics-raytracer_amd/csrc/host/raw_records.h"
 #include "../cs378hgraphics-raytracer_amd/csrc/host/scene_model.h"
+#include "glm_restated.h"  // the oracle's own glm 0.9.8.4 arithmetic (never rt_math.h)
 
 // the checker's own .ray loader (parse_restated.cpp; the product's parser is
 // not linked)
@@ -33,6 +34,7 @@ bool oracle_load_cubemap(const std::string& file, rtxh::Texture faces[6], std::s
 using rtm::dvec2;
 using rtm::dvec3;
 using rtm::mk3;
+using namespace glmr;  // vector operators and glm functions (glm_restated.h)
 
 namespace orc {
 
@@ -277,15 +279,10 @@ struct Geom {
   virtual bool intersectLocal(Ray& r, Isect& i) const = 0;
   virtual void intersectLocalList(Ray& r, std::vector<Isect>& iv) const = 0;
 
-  // operator*(dmat4x4, dvec3) (scene.h:57-62): glm mat4 * dvec4(v, 1),
-  // (m0 x + m1 y) + (m2 z + m3 w) per row
-  dvec3 globalToLocal(const dvec3& v) const {
-    const double* m = tf->inverse.m;
-    double o[3];
-    for (int r = 0; r < 3; ++r) o[r] = (m[0 * 4 + r] * v.x + m[1 * 4 + r] * v.y) + (m[2 * 4 + r] * v.z + m[3 * 4 + r] * 1.0);
-    return mk3(o[0], o[1], o[2]);
-  }
-  dvec3 localToGlobalNormal(const dvec3& v) const { return rtm::normalize(rtm::mat3_mul(tf->normi.m, v)); }
+  // operator*(dmat4x4, dvec3) (scene.h:57-62): glm mat4 * dvec4(v, 1)
+  // (glmr::mat4_mul_point, tmat4x4 * tvec4's column form)
+  dvec3 globalToLocal(const dvec3& v) const { return glmr::mat4_mul_point(tf->inverse.m, v); }
+  dvec3 localToGlobalNormal(const dvec3& v) const { return glmr::normalize(glmr::mat3_mul(tf->normi.m, v)); }
 
   bool intersect(Ray& r, Isect& i) const {  // scene.cpp:13-38
     tl.objects++;
@@ -293,8 +290,8 @@ struct Geom {
     if (!(bounds.intersect(r, tmin, tmax))) return false;
     dvec3 pos = globalToLocal(r.p);
     dvec3 dir = globalToLocal(r.p + r.d) - pos;
-    double length = rtm::length(dir);
-    dir = rtm::normalize(dir);
+    double length = glmr::length(dir);
+    dir = glmr::normalize(dir);
     dvec3 Wpos = r.p, Wdir = r.d;
     r.p = pos;
     r.d = dir;
@@ -316,8 +313,8 @@ struct Geom {
     if (!(bounds.intersect(r, tmin, tmax))) return buf;
     dvec3 pos = globalToLocal(r.p);
     dvec3 dir = globalToLocal(r.p + r.d) - pos;
-    double length = rtm::length(dir);
-    dir = rtm::normalize(dir);
+    double length = glmr::length(dir);
+    dir = glmr::normalize(dir);
     dvec3 Wpos = r.p, Wdir = r.d;
     r.p = pos;
     r.d = dir;
@@ -336,10 +333,10 @@ const rtxh::Material& Isect::getMaterial() const { return material ? *material :
 
 struct Sphere : Geom {
   bool intersectLocal(Ray& r, Isect& i) const override {  // Sphere.cpp:9-40
-    r.d = rtm::normalize(r.d);
+    r.d = glmr::normalize(r.d);
     dvec3 v = -r.p;
-    double b = rtm::dot(v, r.d);
-    double discriminant = b * b - rtm::dot(v, v) + 1;
+    double b = glmr::dot(v, r.d);
+    double discriminant = b * b - glmr::dot(v, v) + 1;
     if (discriminant < 0.0) return false;
     discriminant = sqrt(discriminant);
     double t2 = b + discriminant;
@@ -348,18 +345,18 @@ struct Sphere : Geom {
     double t1 = b - discriminant;
     if (t1 > RAY_EPSILON) {
       i.t = t1;
-      i.N = rtm::normalize(r.at(t1));
+      i.N = glmr::normalize(r.at(t1));
     } else {
       i.t = t2;
-      i.N = rtm::normalize(r.at(t2));
+      i.N = glmr::normalize(r.at(t2));
     }
     return true;
   }
   void intersectLocalList(Ray& r, std::vector<Isect>& iv) const override {  // Sphere.cpp:42-72
-    r.d = rtm::normalize(r.d);
+    r.d = glmr::normalize(r.d);
     dvec3 v = -r.p;
-    double b = rtm::dot(v, r.d);
-    double discriminant = b * b - rtm::dot(v, v) + 1;
+    double b = glmr::dot(v, r.d);
+    double discriminant = b * b - glmr::dot(v, v) + 1;
     if (discriminant < 0.0) return;
     discriminant = sqrt(discriminant);
     double t1 = b - discriminant;
@@ -368,14 +365,14 @@ struct Sphere : Geom {
       Isect i;
       i.obj = this;
       i.t = t1;
-      i.N = rtm::normalize(r.at(t1));
+      i.N = glmr::normalize(r.at(t1));
       iv.push_back(i);
     }
     if (t2 > RAY_EPSILON) {
       Isect i;
       i.obj = this;
       i.t = t2;
-      i.N = rtm::normalize(r.at(t2));
+      i.N = glmr::normalize(r.at(t2));
       iv.push_back(i);
     }
   }
@@ -384,7 +381,7 @@ struct Sphere : Geom {
 struct Box : Geom {
   dvec3 computeNormal(int bestIndex, const Isect& i) const {  // Box.cpp:99-108
     dvec3 b_norm = mk(*material, rtxh::P_BUMP, i);
-    if (rtm::length(b_norm) > 0.0001) return rtm::normalize(b_norm - mk3(0.5, 0.5, 0.5));
+    if (glmr::length(b_norm) > 0.0001) return glmr::normalize(b_norm - mk3(0.5, 0.5, 0.5));
     if (bestIndex < 3) return mk3(-double(bestIndex == 0), -double(bestIndex == 1), -double(bestIndex == 2));
     return mk3(double(bestIndex == 3), double(bestIndex == 4), double(bestIndex == 5));
   }
@@ -462,7 +459,7 @@ struct Cylinder : Geom {
       double z = P[2];
       if (z >= 0.0 && z <= 1.0) {
         i.t = t1;
-        i.N = rtm::normalize(mk3(P[0], P[1], 0.0));
+        i.N = glmr::normalize(mk3(P[0], P[1], 0.0));
         return true;
       }
     }
@@ -471,8 +468,8 @@ struct Cylinder : Geom {
     if (z >= 0.0 && z <= 1.0) {
       i.t = t2;
       dvec3 normal = mk3(P[0], P[1], 0.0);
-      if (!capped && rtm::dot(normal, r.d) > 0) normal = -normal;
-      i.N = rtm::normalize(normal);
+      if (!capped && glmr::dot(normal, r.d) > 0) normal = -normal;
+      i.N = glmr::normalize(normal);
       return true;
     }
     return false;
@@ -538,7 +535,7 @@ struct Cylinder : Geom {
         Isect i;
         i.obj = this;
         i.t = t1;
-        i.N = rtm::normalize(mk3(P[0], P[1], 0.0));
+        i.N = glmr::normalize(mk3(P[0], P[1], 0.0));
         iv.push_back(i);
       }
     }
@@ -550,8 +547,8 @@ struct Cylinder : Geom {
         i.obj = this;
         i.t = t2;
         dvec3 normal = mk3(P[0], P[1], 0.0);
-        if (!capped && rtm::dot(normal, r.d) > 0) normal = -normal;
-        i.N = rtm::normalize(normal);
+        if (!capped && glmr::dot(normal, r.d) > 0) normal = -normal;
+        i.N = glmr::normalize(normal);
         iv.push_back(i);
       }
     }
@@ -654,7 +651,7 @@ struct Cone : Geom {
       theRoot = farRoot;
       normal = bodyNormal(r, theRoot);
     }
-    if (!capped && rtm::dot(normal, r.d) > 0) normal = -normal;
+    if (!capped && glmr::dot(normal, r.d) > 0) normal = -normal;
     const double pz = r.p[2], dz = r.d[2];
     const double t1 = (-pz) / dz, t2 = (height - pz) / dz;
     if (capped) {
@@ -672,18 +669,18 @@ struct Cone : Geom {
     if (theRoot <= RAY_EPSILON) return false;
     i.obj = this;
     i.t = theRoot;
-    i.N = rtm::normalize(normal);
+    i.N = glmr::normalize(normal);
     return true;
   }
   void intersectLocalList(Ray& r, std::vector<Isect>& iv) const override {  // Cone.cpp:108-210
     double nearRoot, farRoot;
     if (!roots(r, nearRoot, farRoot)) return;
     auto push = [&](double t, dvec3 n, bool body) {
-      if (body && !capped && rtm::dot(n, r.d) > 0) n = -n;
+      if (body && !capped && glmr::dot(n, r.d) > 0) n = -n;
       Isect i;
       i.obj = this;
       i.t = t;
-      i.N = rtm::normalize(n);
+      i.N = glmr::normalize(n);
       iv.push_back(i);
     };
     if (isGoodRoot(r.at(nearRoot)) && nearRoot > RAY_EPSILON) push(nearRoot, bodyNormal(r, nearRoot), true);
@@ -716,19 +713,19 @@ struct Trimesh : Geom {
     const auto& ids = M.faces[f];
     const dvec3 verts[3] = {M.verts[ids[0]], M.verts[ids[1]], M.verts[ids[2]]};
     const dvec3 normal = M.face_normals[f];
-    double t = rtm::dot(normal, r.d);
+    double t = glmr::dot(normal, r.d);
     if (t < RAY_EPSILON / 32 && t > -RAY_EPSILON / 32) return false;  // ZCHK
-    t = rtm::dot(verts[0] - r.p, normal) / t;
+    t = glmr::dot(verts[0] - r.p, normal) / t;
     if (t < RAY_EPSILON / 32) return false;  // BTTC
     dvec3 p_isect = r.at(t);
     for (int k = 0; k < 3; k++) {
       dvec3 prime = verts[k];
       dvec3 edgev = verts[(k + 1) % 3];
-      if (rtm::dot(rtm::cross(edgev - prime, p_isect - prime), normal) < RAY_EPSILON / 32) return false;
+      if (glmr::dot(glmr::cross(edgev - prime, p_isect - prime), normal) < RAY_EPSILON / 32) return false;
     }
-    double faceArea = rtm::dot(rtm::cross(verts[1] - verts[0], verts[2] - verts[0]), normal);
-    double baryU = rtm::dot(rtm::cross(verts[1] - p_isect, verts[2] - p_isect), normal);
-    double baryV = rtm::dot(rtm::cross(verts[2] - p_isect, verts[0] - p_isect), normal);
+    double faceArea = glmr::dot(glmr::cross(verts[1] - verts[0], verts[2] - verts[0]), normal);
+    double baryU = glmr::dot(glmr::cross(verts[1] - p_isect, verts[2] - p_isect), normal);
+    double baryV = glmr::dot(glmr::cross(verts[2] - p_isect, verts[0] - p_isect), normal);
     if (faceArea < RAY_EPSILON / 32 && faceArea > -RAY_EPSILON / 32) return false;
     dvec3 bary = mk3(baryU / faceArea, baryV / faceArea, 0);
     bary.z = 1 - bary.x - bary.y;
@@ -761,7 +758,7 @@ struct Trimesh : Geom {
     if (M.normals.size() != 0) {
       const dvec3 n0 = M.normals[ids[0]], n1 = M.normals[ids[1]], n2 = M.normals[ids[2]];
       const double mm[9] = {n0.x, n0.y, n0.z, n1.x, n1.y, n1.z, n2.x, n2.y, n2.z};
-      i.N = rtm::normalize(rtm::mat3_mul(mm, bary));
+      i.N = glmr::normalize(glmr::mat3_mul(mm, bary));
     } else {
       i.N = normal;
     }
@@ -816,12 +813,12 @@ struct DirectionalLight : Light {  // light.cpp:56-59
 
 struct PointLight : Light {  // light.cpp:61-73
   double distanceAttenuation(const dvec3& P) const override {
-    double d = rtm::distance(L->pos, P);
-    return rtm::gclamp(1.0 / (double(L->c) + double(L->l) * d + double(L->q) * d * d), 0.0, 1.0);
+    double d = glmr::distance(L->pos, P);
+    return glmr::clamp(1.0 / (double(L->c) + double(L->l) * d + double(L->q) * d * d), 0.0, 1.0);
   }
-  dvec3 getDirection(const dvec3& P) const override { return rtm::normalize(L->pos - P); }
+  dvec3 getDirection(const dvec3& P) const override { return glmr::normalize(L->pos - P); }
   bool sattnLimitCheck(const Ray& r, const Isect& i) const override {
-    return rtm::dot(L->pos - r.at(i.t), r.d) <= 0;
+    return glmr::dot(L->pos - r.at(i.t), r.d) <= 0;
   }
 };
 
@@ -850,14 +847,14 @@ struct AreaLight : PointLight {  // light.cpp:76-104
     dvec3 pb = p - r.d * EPS_BACKUP;
     for (int i = 0; i < tl_ss_res; i++) {
       dvec3 lpos = pick(i);
-      if (validImpact(r, pb, lpos)) sattn += srsAttenuation(pb, rtm::normalize(lpos - pb));
+      if (validImpact(r, pb, lpos)) sattn += srsAttenuation(pb, glmr::normalize(lpos - pb));
     }
     sattn *= (1.0 / (tl_ss_res - 1));
     return sattn;
   }
   bool sattnLimitCheck(const Ray& r, const Isect& i) const override {
     dvec3 imp = impact(r);
-    return rtm::dot(imp - r.at(i.t), r.d) <= 0;
+    return glmr::dot(imp - r.at(i.t), r.d) <= 0;
   }
 };
 
@@ -869,8 +866,8 @@ struct AreaLightRect : AreaLight {  // light.cpp:100-110
     return mk3(L->u.x * a + L->v.x * b, L->u.y * a + L->v.y * b, L->u.z * a + L->v.z * b);
   }
   dvec3 impact(const Ray& r) const override {
-    double t = rtm::dot(L->orient, r.d);
-    t = rtm::dot(L->pos - r.p, L->orient) / t;
+    double t = glmr::dot(L->orient, r.d);
+    t = glmr::dot(L->pos - r.p, L->orient) / t;
     return r.at(t);
   }
 };
@@ -887,27 +884,27 @@ struct AreaLightCirc : AreaLight {  // light.cpp:112-141
     if (ab.x < ab.y && ab.x < ab.z) u = mk3(0.0, -ori.z, ori.y);
     else if (ab.y < ab.z) u = mk3(-ori.z, 0.0, ori.x);
     else u = mk3(-ori.y, ori.x, 0.0);
-    u = rtm::normalize(u);
-    dvec3 v = rtm::cross(ori, u);
+    u = glmr::normalize(u);
+    dvec3 v = glmr::cross(ori, u);
     return x * u + y * v + L->pos;
   }
   dvec3 impact(const Ray& r) const override {
-    double t = rtm::dot(L->orient, r.d);
-    t = rtm::dot(L->pos - r.p, L->orient) / t;
+    double t = glmr::dot(L->orient, r.d);
+    t = glmr::dot(L->pos - r.p, L->orient) / t;
     dvec3 colpos = r.at(t);
-    if (rtm::dot(colpos - L->pos, colpos - L->pos) < (L->radius * L->radius)) return r.at(t);
+    if (glmr::dot(colpos - L->pos, colpos - L->pos) < (L->radius * L->radius)) return r.at(t);
     return mk3(0.0, 0.0, 0.0);
   }
 };
 
 struct SpotLight : AreaLightCirc {  // light.cpp:143-149
   bool validImpact(const Ray&, const dvec3& p) const override {
-    return (rtm::dot(getDirection(p), L->orient) <= 0) &&
-           (rtm::dot(rtm::normalize(p - (L->pos - L->offset * L->orient)), L->orient) > std::cos(PI / 4));
+    return (glmr::dot(getDirection(p), L->orient) <= 0) &&
+           (glmr::dot(glmr::normalize(p - (L->pos - L->offset * L->orient)), L->orient) > std::cos(PI / 4));
   }
   bool validImpact(const Ray&, const dvec3& p, const dvec3& lp) const override {
-    return (rtm::dot(getDirection(p), L->orient) <= 0) &&
-           (rtm::dot(rtm::normalize(p - lp), L->orient) > std::cos(PI / 4));
+    return (glmr::dot(getDirection(p), L->orient) <= 0) &&
+           (glmr::dot(glmr::normalize(p - lp), L->orient) > std::cos(PI / 4));
   }
 };
 
@@ -988,7 +985,7 @@ struct Scene {
     std::sort(iv.begin(), iv.end(), [](const Isect& a, const Isect& b) { return a.t < b.t; });
     std::vector<Isect> obj_stk;
     for (const Isect& iv_it : iv) {
-      const bool leaving = rtm::dot(iv_it.N, r.d) > 0;
+      const bool leaving = glmr::dot(iv_it.N, r.d) > 0;
       if (leaving) {
         obj_stk.push_back(iv_it);
       } else {
@@ -1037,7 +1034,7 @@ dvec3 Light::srsAttenuation(const dvec3& pos, const dvec3& dir) const {
     last_t = iv_it.t;
     iv_it.t = t;
     const rtxh::Material& m_in = iv_it.getMaterial();
-    const bool is_inside = rtm::dot(iv_it.N, r2l.d) > 0;
+    const bool is_inside = glmr::dot(iv_it.N, r2l.d) > 0;
     r2l.p = r2l.at(iv_it.t);
     rtxh::Material m_disc;
     if (tl_overlapping) m_disc = tl_scene->discoverMat(r2l);  // light.cpp:39
@@ -1047,8 +1044,8 @@ dvec3 Light::srsAttenuation(const dvec3& pos, const dvec3& dir) const {
     if (sattnLimitCheck(r2l, iv_it)) return sattn;
     if (!next_m.trans) return mk3(0.0, 0.0, 0.0);
     const double th = tl_scene->aterm_thresh;
-    if (th > 0.0 && rtm::dot(sattn, sattn) < th * th) return mk3(0.0, 0.0, 0.0);
-    sattn *= rtm::pow3(mk(curr_m, rtxh::P_KT, iv_it), iv_it.t);
+    if (th > 0.0 && glmr::dot(sattn, sattn) < th * th) return mk3(0.0, 0.0, 0.0);
+    sattn *= glmr::pow(mk(curr_m, rtxh::P_KT, iv_it), glmr::vec3(iv_it.t));
   }
   return sattn;
 }
@@ -1067,11 +1064,11 @@ dvec3 shade(const rtxh::Material& m, const Scene* scene, const Ray& r, const Ise
   for (size_t l_idx = 0; l_idx < scene->lights.size(); ++l_idx) {
     const Light& L = *scene->lights[l_idx];
     const dvec3 l_i = L.getDirection(isect_p);
-    const dvec3 l_r = (l_i - 2 * (rtm::dot(l_i, surf_n)) * surf_n);
-    double dot = rtm::dot(l_i, surf_n);
+    const dvec3 l_r = (l_i - 2 * (glmr::dot(l_i, surf_n)) * surf_n);
+    double dot = glmr::dot(l_i, surf_n);
     if (trans) dot = std::fabs(dot);
-    const dvec3 d_comp = kd * rtm::gmax(0.0, dot);
-    const dvec3 s_comp = ks * rtm::pow3(rtm::splat3(rtm::gmax(0.0, rtm::dot(l_r, v))), sh);
+    const dvec3 d_comp = kd * glmr::max(0.0, dot);
+    const dvec3 s_comp = ks * glmr::pow(glmr::vec3(glmr::max(0.0, glmr::dot(l_r, v))), glmr::vec3(sh));
     const double dattn = L.distanceAttenuation(isect_p);
     const dvec3 sattn = L.shadowAttenuation(r, isect_p);
     i_out += dattn * sattn * L.getColor() * (d_comp + s_comp);
@@ -1125,16 +1122,16 @@ struct Tracer {
       const rtxh::Material& m_in = i.getMaterial();
       t = i.t;
       colorC = shade(m_in, scene, r, i);
-      if (thresh > 0.0 && rtm::dot(colorC, colorC) < thresh) return colorC;
+      if (thresh > 0.0 && glmr::dot(colorC, colorC) < thresh) return colorC;
       if (m_in.recur && depth > 0) {
         rtxh::Material m_disc;  // RayTracer.cpp:128
         if (P.overlapping) m_disc = scene->discoverMat(Ray(r.at(i.t - RAY_EPSILON), r.d));
         const rtxh::Material& m_out = P.overlapping ? m_disc : g_air;
-        bool leaving = rtm::dot(i.N, r.d) >= 0;
+        bool leaving = glmr::dot(i.N, r.d) >= 0;
         const rtxh::Material& curr_m = leaving ? m_in : m_out;
         const rtxh::Material& next_m = leaving ? m_out : m_in;
         dvec3 normal = (leaving ? -1.0 : 1.0) * i.N;
-        double c = -1 * rtm::dot(normal, r.d);
+        double c = -1 * glmr::dot(normal, r.d);
         double eta = next_m.trans ? mindex(curr_m, i) / mindex(next_m, i) : 0;
         double radicand = 1 - eta * eta * (1 - c * c);
         bool tir = next_m.trans && radicand < 0;
@@ -1145,8 +1142,7 @@ struct Tracer {
           Ray reflRay(reflStart, reflDir);
           tl.secondary++;
           dvec3 reflCol = traceRay(reflRay, thresh, depth, reflT) * mk(m_in, rtxh::P_KR, i);
-          reflCol *= rtm::gmax3(rtm::gmin3(rtm::pow3(mk(curr_m, rtxh::P_KT, i), reflT), rtm::splat3(1.0)),
-                                rtm::splat3(0.0));
+          reflCol *= glmr::max(glmr::min(glmr::pow(mk(curr_m, rtxh::P_KT, i), glmr::vec3(reflT)), 1.0), 0.0);
           colorC += reflCol;
         }
         if (next_m.trans && !tir) {
@@ -1154,7 +1150,7 @@ struct Tracer {
           Ray transRay(r.at(i.t + RAY_EPSILON), eta * r.d + (eta * c - sqrt(radicand)) * normal);
           tl.secondary++;
           dvec3 transCol = traceRay(transRay, thresh, depth, transT);
-          transCol *= rtm::pow3(mk(next_m, rtxh::P_KT, i), transT);
+          transCol *= glmr::pow(mk(next_m, rtxh::P_KT, i), glmr::vec3(transT));
           colorC += transCol;
         }
       }
@@ -1169,17 +1165,17 @@ struct Tracer {
     const dvec3 eye = anaglyph_eye ? cam.eye + mk3(0.25, 0.0, 0.0) : cam.eye;  // ANAGLYPH_DELTA
     x -= 0.5;
     y -= 0.5;
-    dvec3 dir = rtm::normalize(cam.look + x * cam.u + y * cam.v);  // camera.cpp:21-31
+    dvec3 dir = glmr::normalize(cam.look + x * cam.u + y * cam.v);  // camera.cpp:21-31
     Ray r(eye, dir);
     double dummy = 0.0;
     tl.camera++;
     dvec3 ret = traceRay(r, P.aterm_thresh, P.depth, dummy);
     if (P.dof) {
-      double fd = rtm::gmax(P.dof_fd, 1.0);
+      double fd = glmr::max(P.dof_fd, 1.0);
       dvec3 fp_n = -r.d;
       dvec3 fp_pt = r.at(fd);
-      double t = rtm::dot(fp_n, r.d);
-      t = rtm::dot(fp_pt - r.p, fp_n) / t;
+      double t = glmr::dot(fp_n, r.d);
+      t = glmr::dot(fp_pt - r.p, fp_n) / t;
       dvec3 dest = r.at(t);
       double sz = P.dof_apsz / 2;
       int divs = P.dof_div;
@@ -1189,13 +1185,13 @@ struct Tracer {
         offsetAngle = offsetAngle / divs + (k - 1) * baseAngle;
         dvec3 offVec = (std::cos(offsetAngle) * cam.v + std::sin(offsetAngle) * cam.u) * sz;
         r.p = eye + offVec;
-        r.d = rtm::normalize(dest - r.p);
+        r.d = glmr::normalize(dest - r.p);
         tl.camera++;
         ret += traceRay(r, P.aterm_thresh, P.depth, dummy);
       }
       ret *= (1.0 / (divs + 1.0));
     }
-    ret = rtm::gclamp3(ret, 0.0, 1.0);
+    ret = glmr::clamp(ret, 0.0, 1.0);
     return ret;
   }
 
@@ -1242,7 +1238,7 @@ struct Tracer {
       sd += rtm::mk3(std::pow(a.x, 2.0), std::pow(a.y, 2.0), std::pow(a.z, 2.0));
     }
     sd *= (1.0 / (samples * samples - 1));
-    if (rtm::length(sd) > P.aa_thresh) {
+    if (glmr::length(sd) > P.aa_thresh) {
       mu = mk3(0.0, 0.0, 0.0);
       for (int a = 0; a < 2; a++)
         for (int b = 0; b < 2; b++) {
@@ -1507,9 +1503,9 @@ int oracle_render(const char* ray_path, const char* cubemap_file, const RtxRende
           // RayTracer::setPixel (RayTracer.cpp:388-394)
           if (rgb8) {
             uint8_t* pixel = rgb8 + pix * 3;
-            pixel[0] = rtm::to_byte(col.x);
-            pixel[1] = rtm::to_byte(col.y);
-            pixel[2] = rtm::to_byte(col.z);
+            pixel[0] = glmr::set_pixel_byte(col.x);
+            pixel[1] = glmr::set_pixel_byte(col.y);
+            pixel[2] = glmr::set_pixel_byte(col.z);
           }
           if (rgb_f64) {
             rgb_f64[pix * 3 + 0] = col.x;
