@@ -464,6 +464,8 @@ struct ShadeArgs {
   int leaf_k;      // object / leaf units wait while >= leaf_k lanes are at a
                    // record (trace_kernel; 65: never)
   const int* free_ids;  // the group's free fork slots (advance_fused_kernel pushes them)
+  int* ovf;        // the group's stack overflow columns (StackShort), one per thread of the launch
+  int lds_k;       // StackShort: stack entries per lane in LDS
 };
 
 // Camera ray k of the sample at (sx, sy), eye pass `pass` (trace(),

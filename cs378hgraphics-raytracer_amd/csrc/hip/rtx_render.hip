@@ -1818,7 +1818,13 @@ __global__ void __launch_bounds__(WG) tail_kernel(DevScene S, const DevScene* __
 // CAM: the first iteration's instantiation (claims + first camera rays,
 // SA.cam_n > 0); the others carry none of that code, so the later
 // iterations' closest-hit launches keep their own register budget.
-template <bool STATS, int MODE, bool FUSED = false, bool FORK = false, bool CAM = false>
+// LDS (trace_lds_bytes): per wave, the stack — [stack_cap][64] entries, or
+// with SHORT [RTX_LDS_STACK][64] and the deeper entries in the group's
+// overflow columns (StackShort) — then [RTX_COLD_FIELDS][64] doubles of the
+// traversal's cold state (ColdLDS: the world ray and its reciprocal, 19
+// VGPRs the persistent walk state no longer holds; spills of the fused
+// kernels 48 / 64 B -> 0 / 16 B, headline 31.8-32.0 -> 30.6-31.2 ms).
+template <bool STATS, int MODE, bool FUSED = false, bool FORK = false, bool CAM = false, bool SHORT = false>
 __global__ void __launch_bounds__(WG, !FUSED ? RTX_TRACE_WAVES : (MODE == Q_CLOSEST ? RTX_SHADE_WAVES : RTX_WALK_WAVES))
     trace_kernel(DevScene S, const DevScene* __restrict__ Sg, QList Q, unsigned int* __restrict__ counters,
                  LaneMem lm, int stack_cap, unsigned long long* __restrict__ stats, double* __restrict__ wterm,
@@ -1826,14 +1832,22 @@ __global__ void __launch_bounds__(WG, !FUSED ? RTX_TRACE_WAVES : (MODE == Q_CLOS
   extern __shared__ int lds_stack[];
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
-  int* stk = lds_stack + wave * stack_cap * 64;
+  const int scap = SHORT ? SA.lds_k : stack_cap;  // stack entries per lane in LDS
+  using Stk = typename std::conditional<SHORT, StackShort, StackLDS>::type;
+  Stk stk;
+  if constexpr (SHORT)
+    stk = StackShort{lds_stack + wave * scap * 64 + lane, lds_stack, SA.ovf + blockIdx.x * WG,
+                     static_cast<int>(gridDim.x) * WG, scap};
+  else
+    stk = StackLDS{lds_stack + wave * stack_cap * 64 + lane};
   const size_t cap = Q.cap;
   const bool cam = CAM && FUSED && MODE == Q_CLOSEST && SA.cam_n > 0;  // first iteration: claims + camera rays here
   const unsigned int nq = cam ? static_cast<unsigned int>(SA.cam_n) : counters[CNT_Q + (MODE - 1) * CNT_LINE];
   unsigned int* claim = counters + CNT_CLAIM + (MODE - 1) * CNT_LINE;
 
   Counters C = {0, 0, 0, 0, 0, 0, 0};
-  Trav T;
+  TravT<ColdLDS> T;
+  T.cold.c = reinterpret_cast<double*>(lds_stack + WAVES_PER_WG * scap * 64) + wave * RTX_COLD_FIELDS * 64 + lane;
   bool active = false;
   size_t kq = 0;
   // wave-uniform claim state: [qnext, qend) of the list
@@ -2023,7 +2037,7 @@ __global__ void __launch_bounds__(WG, !FUSED ? RTX_TRACE_WAVES : (MODE == Q_CLOS
       }
       if (go) {
         if (STATS) qsteps++;
-        if (trav_step<STATS, MODE>(T, S, stk, lane, C)) {
+        if (trav_step<STATS, MODE>(T, S, stk, C)) {
           if (FUSED) pend = true;
           else finish();
           active = false;
@@ -2413,6 +2427,8 @@ struct FrameCtx {
   size_t bidx_bytes = 0;
   int* d_free = nullptr;  // per slot group: its free fork slots (fork_claim / advance_fused_kernel)
   size_t free_bytes = 0;
+  int* d_ovf = nullptr;  // per slot group: the trace kernels' stack overflow columns (StackShort)
+  size_t ovf_bytes = 0;
   unsigned int* d_bstat = nullptr;
   unsigned int* h_bstat = nullptr;  // pinned: [taken, refused, -, -, fork requests of group g at 4 + g]
   hipEvent_t bstat_ev = nullptr;
@@ -2822,6 +2838,7 @@ rtx_status rtx_scene_destroy(void* scene) {
     if (X.d_acnt) (void)hipFree(X.d_acnt);
     if (X.d_bidx) (void)hipFree(X.d_bidx);
     if (X.d_free) (void)hipFree(X.d_free);
+    if (X.d_ovf) (void)hipFree(X.d_ovf);
     if (X.d_bstat) (void)hipFree(X.d_bstat);
     if (X.h_bstat) (void)hipHostFree(X.h_bstat);
     if (X.bstat_ev) (void)hipEventDestroy(X.bstat_ev);
@@ -3704,16 +3721,37 @@ static rtx_status render_once(SceneState* st, const RtxRenderParams* params, uin
     // deferred colour: set by the group's first advance_kernel, which visits
     // all of its slots (every other field is written before it is read)
     HIP_TRY(hipMemsetAsync(X->d_counters, 0, 16 * CNT_PER_GROUP * sizeof(unsigned int), ws));
+    // LDS per workgroup: the tail kernels' whole stacks (cold state in
+    // registers); the trace kernels' stacks and cold state (trace_kernel) —
+    // whole stacks unless those would cost the trace kernels a resident
+    // workgroup (RTX_TRACE_WAVES per SIMD: 3 of 160 KB), else SHORT stacks
+    // (the 1M-face dragon: 41 entries)
     const size_t lds_stacks = size_t(st->stack_cap) * 64 * sizeof(int) * WAVES_PER_WG;
     const size_t lds = lds_stacks;
-    if (lds > 160 * 1024) {
+    const size_t lds_cold = size_t(RTX_COLD_FIELDS) * 64 * sizeof(double) * WAVES_PER_WG;
+    const size_t lds_full = lds_stacks + lds_cold;
+    int lds_k = RTX_LDS_STACK;
+    bool short_stack = st->stack_cap > lds_k && lds_full * RTX_TRACE_WAVES > size_t(160) * 1024;
+    // (test knob: short stacks of K entries on every frame, so the overflow
+    // columns are exercised — tests/test_gpu_parity.py)
+    if (const char* e = getenv("RTX_TEST_LDS_STACK"))
+      if (atoi(e) > 0) {
+        lds_k = std::min(atoi(e), 64);
+        short_stack = st->stack_cap > lds_k;
+      }
+    const size_t lds_tr = short_stack ? size_t(lds_k) * 64 * sizeof(int) * WAVES_PER_WG + lds_cold : lds_full;
+    const int ovf_entries = short_stack ? st->stack_cap - lds_k : 0;
+    if (lds > 160 * 1024 || lds_tr > 160 * 1024) {
       g_err = "rtx_render: LDS budget exceeded (BVH too deep)";
       return RTX_ERR_CAPACITY;
     }
-    const void* tfn = stats ? reinterpret_cast<const void*>(trace_kernel<true, Q_CLOSEST>)
-                            : reinterpret_cast<const void*>(trace_kernel<false, Q_CLOSEST>);
+    const void* tfn =
+        stats ? (short_stack ? reinterpret_cast<const void*>(trace_kernel<true, Q_CLOSEST, false, false, false, true>)
+                             : reinterpret_cast<const void*>(trace_kernel<true, Q_CLOSEST>))
+              : (short_stack ? reinterpret_cast<const void*>(trace_kernel<false, Q_CLOSEST, false, false, false, true>)
+                             : reinterpret_cast<const void*>(trace_kernel<false, Q_CLOSEST>));
     int per_cu = 0;
-    HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, tfn, WG, lds));
+    HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, tfn, WG, lds_tr));
     if (per_cu < 1) per_cu = 1;
     int64_t tgrid = static_cast<int64_t>(st->n_cu) * per_cu;
     const int64_t tgrid_full = std::min<int64_t>(per, tgrid);
@@ -3738,16 +3776,31 @@ static rtx_status render_once(SceneState* st, const RtxRenderParams* params, uin
     if (fuse) {
       int pc = 0, pn = 0;
       HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(
-          &pc, reinterpret_cast<const void*>(trace_kernel<false, Q_CLOSEST, true, true>), WG, lds));
+          &pc,
+          short_stack ? reinterpret_cast<const void*>(trace_kernel<false, Q_CLOSEST, true, true, false, true>)
+                      : reinterpret_cast<const void*>(trace_kernel<false, Q_CLOSEST, true, true>),
+          WG, lds_tr));
       HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(
-          &pn, reinterpret_cast<const void*>(trace_kernel<false, Q_NEXT, true>), WG, lds));
+          &pn,
+          short_stack ? reinterpret_cast<const void*>(trace_kernel<false, Q_NEXT, true, false, false, true>)
+                      : reinterpret_cast<const void*>(trace_kernel<false, Q_NEXT, true>),
+          WG, lds_tr));
       tgrid_c = std::min<int64_t>(per, std::max<int64_t>(1, tgrid * std::max(1, pc) / per_cu));
       tgrid_n = std::min<int64_t>(per, std::max<int64_t>(1, tgrid * std::max(1, pn) / per_cu));
       tfull_c = std::min<int64_t>(per, std::max<int64_t>(1, tgrid_full * std::max(1, pc) / per_cu));
       tfull_n = std::min<int64_t>(per, std::max<int64_t>(1, tgrid_full * std::max(1, pn) / per_cu));
     }
+    // stack overflow columns (StackShort): per group, one column of
+    // ovf_entries per thread of its largest trace launch
+    const int64_t ovf_threads =
+        std::max<int64_t>(std::max<int64_t>(std::max<int64_t>(tgrid, tgrid_c), std::max<int64_t>(tgrid_n, tfull_c)),
+                          tfull_n) * WG;
+    if (ovf_entries > 0 &&
+        (rc = ensure(reinterpret_cast<void**>(&X->d_ovf), &X->ovf_bytes,
+                     size_t(G) * size_t(ovf_entries) * size_t(ovf_threads) * sizeof(int))) != RTX_OK)
+      return rc;
     // The first iteration's closest-hit / walk grids as a percentage of the
-    // whole GPU's residency (RTX_TG0_C / RTX_TG0_N; 0 = the grids above).
+    // whole GPU's residency (tg0_c / tg0_n; 0 = the grids above).
     // On whole frames (div 1) the groups' first launches otherwise each take
     // the whole GPU in turn: group 0's camera rays first, then its walks
     // beside the others' camera rays, and its advance launch starved of CUs
@@ -3863,6 +3916,12 @@ static rtx_status render_once(SceneState* st, const RtxRenderParams* params, uin
         std::memset(&sa, 0, sizeof(sa));
         sa.leaf_k = leaf_k;
         sa.free_ids = recycle ? X->d_free + size_t(g) * gs : nullptr;
+        sa.ovf = ovf_entries > 0 ? X->d_ovf + size_t(g) * size_t(ovf_entries) * size_t(ovf_threads) : nullptr;
+        sa.lds_k = lds_k;
+        if (short_stack && std::max(tg, tgn) * WG > ovf_threads) {
+          g_err = "rtx_render: internal error: a trace launch exceeds its stack overflow columns";
+          return RTX_ERR_INVALID;
+        }
         if (fuse) {
           sa.Fp = X->d_frame;
           sa.hits = d_hits;
@@ -3874,8 +3933,8 @@ static rtx_status render_once(SceneState* st, const RtxRenderParams* params, uin
           sa.out_cnt = out_cnt;
           sa.cam_n = cam_it ? cam_n[size_t(g)] : 0;
         }
-        dispatch2(stats, fork, [&](auto st_, auto fk_) {
-          constexpr bool ST_ = decltype(st_)::value, FK_ = decltype(fk_)::value;
+        dispatch3(stats, fork, short_stack, [&](auto st_, auto fk_, auto sh_) {
+          constexpr bool ST_ = decltype(st_)::value, FK_ = decltype(fk_)::value, SH_ = decltype(sh_)::value;
           if (fuse) {
             // (inside the dispatch lambda: no HIP_TRY returns here; debug only)
             hipEvent_t d0 = nullptr, d1 = nullptr;
@@ -3888,10 +3947,10 @@ static rtx_status render_once(SceneState* st, const RtxRenderParams* params, uin
               (void)(hipEventRecord(d0, sg));
             }
             if (cam_it)
-              RTX_LAUNCH((trace_kernel<ST_, Q_CLOSEST, true, FK_, true>), dim3(tg), dim3(WG), lds, sg, S,
+              RTX_LAUNCH((trace_kernel<ST_, Q_CLOSEST, true, FK_, true, SH_>), dim3(tg), dim3(WG), lds_tr, sg, S,
                                  X->d_scene, q0, cnt, A, st->stack_cap, st->d_stats, X->d_wterm, sa, -1);
             else
-              RTX_LAUNCH((trace_kernel<ST_, Q_CLOSEST, true, FK_>), dim3(tg), dim3(WG), lds, sg, S,
+              RTX_LAUNCH((trace_kernel<ST_, Q_CLOSEST, true, FK_, false, SH_>), dim3(tg), dim3(WG), lds_tr, sg, S,
                                  X->d_scene, q0, cnt, A, st->stack_cap, st->d_stats, X->d_wterm, sa, -1);
             if (dbg_level >= 2) {
               unsigned int hc[CNT_PER_GROUP];
@@ -3917,7 +3976,7 @@ static rtx_status render_once(SceneState* st, const RtxRenderParams* params, uin
               (void)(hipEventCreate(&d1));
               (void)(hipEventRecord(d0, sg));
             }
-            RTX_LAUNCH((trace_kernel<ST_, Q_NEXT, true>), dim3(tgn), dim3(WG), lds, sg, S, X->d_scene, q1,
+            RTX_LAUNCH((trace_kernel<ST_, Q_NEXT, true, false, false, SH_>), dim3(tgn), dim3(WG), lds_tr, sg, S, X->d_scene, q1,
                                cnt, A, st->stack_cap, st->d_stats, X->d_wterm, sa, clr_next);
             if (dbg_level >= 2) {
               float ms = 0.f;
@@ -3936,24 +3995,20 @@ static rtx_status render_once(SceneState* st, const RtxRenderParams* params, uin
               (void)(hipEventDestroy(d1));
             }
           } else if (!FK_) {
-            RTX_LAUNCH((trace_kernel<ST_, Q_CLOSEST>), dim3(tg), dim3(WG), lds, sg, S, X->d_scene, q0, cnt, A,
+            RTX_LAUNCH((trace_kernel<ST_, Q_CLOSEST, false, false, false, SH_>), dim3(tg), dim3(WG), lds_tr, sg, S, X->d_scene, q0, cnt, A,
                                st->stack_cap, st->d_stats, nullptr, sa, -1);
-            RTX_LAUNCH((trace_kernel<ST_, Q_NEXT>), dim3(tg), dim3(WG), lds, sg, S, X->d_scene, q1, cnt, A,
+            RTX_LAUNCH((trace_kernel<ST_, Q_NEXT, false, false, false, SH_>), dim3(tg), dim3(WG), lds_tr, sg, S, X->d_scene, q1, cnt, A,
                                st->stack_cap, st->d_stats, nullptr, sa, clr_next);
           }
         });
         if (!fuse && fork) {  // the sequential machine's trace kernels do not depend on forking
-          if (stats) {
-            RTX_LAUNCH((trace_kernel<true, Q_CLOSEST>), dim3(tg), dim3(WG), lds, sg, S, X->d_scene, q0, cnt,
-                               A, st->stack_cap, st->d_stats, nullptr, sa, -1);
-            RTX_LAUNCH((trace_kernel<true, Q_NEXT>), dim3(tg), dim3(WG), lds, sg, S, X->d_scene, q1, cnt, A,
-                               st->stack_cap, st->d_stats, nullptr, sa, clr_next);
-          } else {
-            RTX_LAUNCH((trace_kernel<false, Q_CLOSEST>), dim3(tg), dim3(WG), lds, sg, S, X->d_scene, q0, cnt,
-                               A, st->stack_cap, st->d_stats, nullptr, sa, -1);
-            RTX_LAUNCH((trace_kernel<false, Q_NEXT>), dim3(tg), dim3(WG), lds, sg, S, X->d_scene, q1, cnt, A,
-                               st->stack_cap, st->d_stats, nullptr, sa, clr_next);
-          }
+          dispatch2(stats, short_stack, [&](auto st_, auto sh_) {
+            constexpr bool ST_ = decltype(st_)::value, SH_ = decltype(sh_)::value;
+            RTX_LAUNCH((trace_kernel<ST_, Q_CLOSEST, false, false, false, SH_>), dim3(tg), dim3(WG), lds_tr, sg, S,
+                       X->d_scene, q0, cnt, A, st->stack_cap, st->d_stats, nullptr, sa, -1);
+            RTX_LAUNCH((trace_kernel<ST_, Q_NEXT, false, false, false, SH_>), dim3(tg), dim3(WG), lds_tr, sg, S,
+                       X->d_scene, q1, cnt, A, st->stack_cap, st->d_stats, nullptr, sa, clr_next);
+          });
         }
         HIP_TRY(hipGetLastError());
         if (it % check_every == check_every - 1) {

@@ -38,9 +38,77 @@ namespace rtxd {
 // persistent trace kernel can hand a lane a new query as soon as its own one
 // ends while the other lanes of the wave keep stepping; traverse() runs one
 // query to completion.
-struct Trav {
+//
+// Cold state.  The world ray (P, D) and its exact-fallback reciprocal (ri)
+// are read only by the object steps (the world-box test, the transform into
+// a mesh's frame) and when a mesh walk ends (the scene's float ray again) —
+// not by the record steps that are most of the walk.  ColdRegs keeps them in
+// registers; ColdLDS keeps them in a per-wave LDS block beside the stacks
+// (field-major, [field][64 lanes], 8-byte accesses: conflict-free), which
+// takes 19 VGPRs off the persistent traversal state of the trace kernels.
+struct ColdRegs {
   dvec3 P, D;
-  RayInv ri;  // exact-fallback reciprocal: the root and the objects' world boxes
+  RayInv ri;
+  dvec3 lp, ld;  // the mesh-local ray of a mesh walk
+  RT_HD dvec3 getLP() const { return lp; }
+  RT_HD dvec3 getLD() const { return ld; }
+  RT_HD void setL(const dvec3& p, const dvec3& d) {
+    lp = p;
+    ld = d;
+  }
+  RT_HD dvec3 getP() const { return P; }
+  RT_HD dvec3 getD() const { return D; }
+  RT_HD RayInv getRI() const { return ri; }
+  RT_HD void set(const dvec3& p, const dvec3& d, const RayInv& r) {
+    P = p;
+    D = d;
+    ri = r;
+  }
+  RT_HD void reset() {
+    P = D = lp = ld = mk3(0.0, 0.0, 0.0);
+    ri.inv = mk3(0.0, 0.0, 0.0);
+    ri.fast = true;
+  }
+};
+#define RTX_COLD_FIELDS 10  // doubles per lane in a ColdLDS block (P, D, 1/D, fast)
+// (The mesh-local ray lp, ld — read by every leaf step — stays in registers:
+// in LDS as well it measured no faster, 31.33 vs 31.32 ms with the short
+// stack, and its 3 KB per wave do not fit beside a whole stack.)
+struct ColdLDS {
+  double* c;  // the lane's column of its wave's block: field k at c[k * 64]
+  dvec3 lp, ld;
+  RT_HD dvec3 getLP() const { return lp; }
+  RT_HD dvec3 getLD() const { return ld; }
+  RT_HD void setL(const dvec3& p, const dvec3& d) {
+    lp = p;
+    ld = d;
+  }
+  RT_HD dvec3 getP() const { return mk3(c[0 * 64], c[1 * 64], c[2 * 64]); }
+  RT_HD dvec3 getD() const { return mk3(c[3 * 64], c[4 * 64], c[5 * 64]); }
+  RT_HD RayInv getRI() const {
+    RayInv r;
+    r.inv = mk3(c[6 * 64], c[7 * 64], c[8 * 64]);
+    r.fast = c[9 * 64] != 0.0;
+    return r;
+  }
+  RT_HD void set(const dvec3& p, const dvec3& d, const RayInv& r) {
+    c[0 * 64] = p.x;
+    c[1 * 64] = p.y;
+    c[2 * 64] = p.z;
+    c[3 * 64] = d.x;
+    c[4 * 64] = d.y;
+    c[5 * 64] = d.z;
+    c[6 * 64] = r.inv.x;
+    c[7 * 64] = r.inv.y;
+    c[8 * 64] = r.inv.z;
+    c[9 * 64] = r.fast ? 1.0 : 0.0;
+  }
+  RT_HD void reset() { lp = ld = mk3(0.0, 0.0, 0.0); }
+};
+
+template <class Cold>
+struct TravT {
+  Cold cold;  // P, D, ri: the world ray and its exact-fallback reciprocal
   RayF rf;    // float tests of the records being walked: the scene's, or in
               // mode 2 the mesh's (local frame); reset when the mesh is done
   double tp, tlimit, tlo;
@@ -52,13 +120,13 @@ struct Trav {
   // walk: ref >= 0 DevNode4 record, ref < 0 leaf ~(first << 2 | count);
   // mode 0 scene BVH, 1 objects [oc, oe) of a scene leaf, 2 mesh BVH
   int sp, ref, mode, oc, oe;
-  // mesh context (local frame of object moi)
-  dvec3 lp, ld;
+  // mesh context (local frame of object moi; its ray in cold)
   double len, mbest;
   int moi, mbase, mfoff, mnoff, mface;
   bool mhave;
   bool closest;  // the query's mode (read by the Q_ANY instantiations)
 };
+using Trav = TravT<ColdRegs>;
 
 // QMODE Q_ANY: one instantiation for both query kinds, the mode read from
 // the Trav — for kernels whose lanes mix closest and next-hit queries (the
@@ -70,11 +138,57 @@ struct Trav {
 // in the mesh's local frame (KdTree::intersectList collects the items of hit
 // leaves, kdTree.h:100-117): the walk's internal tests are conservative.
 // `leaf`: the face's reference leaf node (TMeta.leaf, a global mnodes index).
-RT_HD bool leaf_ok(const Trav& T, const DevScene& S, int leaf) {
+RT_HD bool leaf_ok(const dvec3& lp, const dvec3& ld, const DevScene& S, int leaf) {
   const RtxNode& lf = S.mnodes[leaf];
   double a, b;
-  return slab(lf.bmin, lf.bmax, T.lp, T.ld, a, b);
+  return slab(lf.bmin, lf.bmax, lp, ld, a, b);
 }
+
+// The walk's stack of pending entries (records or leaves), per lane.
+// StackLDS: the whole stack in LDS, entry i of the lane at s[i * 64] (one
+// column per lane of its wave's [entry][64] block: conflict-free).
+// StackShort (the trace kernels of scenes whose whole stacks and cold state
+// do not fit in LDS at 3 workgroups per CU, e.g. the 1M-face dragon): the
+// first k entries in LDS (RTX_LDS_STACK; a test knob lowers it), the rest in
+// a per-thread overflow column in HBM — walks rarely go that deep (the headline scene's deepest of
+// 360 k sampled queries held 10 entries, the dragon's 13; the trees' worst
+// cases are 31 / 41).  Where the whole stack fits it is faster (its put / get
+// need no branch: headline 30.6-31.2 vs 31.3-31.4 ms).
+#define RTX_LDS_STACK 16
+struct StackLDS {
+  int* s;
+  RT_HD bool lds_only(int) const { return true; }
+  RT_HD void put(int i, int v) const { s[i * 64] = v; }
+  RT_HD void put_lds(int i, int v) const { s[i * 64] = v; }
+  RT_HD int get(int i) const { return s[i * 64]; }
+};
+struct StackShort {
+  int* s;       // the lane's LDS column (entry i at s[i * 64])
+  int* sb;      // the workgroup's LDS stack block: s - sb = wave * k * 64 + lane
+  int* ob;      // the workgroup's overflow columns (thread t's at ob[t])
+  int ostride;  // threads of the launch
+  int k;        // entries in LDS
+  // the thread's overflow column, from its LDS column (no register of its
+  // own for the rare deep walk)
+  RT_HD int* col() const {
+    const int q = static_cast<int>(s - sb);
+    return ob + ((q / (k * 64)) * 64 + (q & 63));
+  }
+  // entries [0, n) all in LDS
+  RT_HD bool lds_only(int n) const { return n <= k; }
+  RT_HD void put(int i, int v) const {
+    if (i < k) s[i * 64] = v;
+    else col()[size_t(i - k) * ostride] = v;
+  }
+  RT_HD void put_lds(int i, int v) const { s[i * 64] = v; }
+  // (the LDS read is unconditional, clamped; only an overflowed entry is
+  // read again from HBM)
+  RT_HD int get(int i) const {
+    int v = s[(i < k ? i : k - 1) * 64];
+    if (i >= k) v = col()[size_t(i - k) * ostride];
+    return v;
+  }
+};
 
 // Visit one 4-wide record: test its entries' boxes (conservatively, pruned
 // to [lo, hi]), continue with the nearest entry hit and push the
@@ -100,9 +214,9 @@ RT_HD Rec4 load_rec4(const DevNode4& nd) {
   return r;
 }
 
-template <bool STATS>
-RT_HD bool visit4(const Rec4& R, const RayF& rf, const double hi, const double lo, int* __restrict__ stk,
-                  const int lane, int& sp, int& ref, Counters& C) {
+template <bool STATS, class STK>
+RT_HD bool visit4(const Rec4& R, const RayF& rf, const double hi, const double lo, const STK& stk, int& sp,
+                  int& ref, Counters& C) {
   const float NOHIT = __builtin_inff();
   // prune bounds widened to floats (hi up, lo down): pruning stays safe
   const float hf = f_up_wide(hi), lf = f_down_wide(lo);
@@ -146,20 +260,24 @@ RT_HD bool visit4(const Rec4& R, const RayF& rf, const double hi, const double l
   cs(a1, r1, a3, r3);
   cs(a1, r1, a2, r2);
   if (!(a0 < NOHIT)) return false;
-  if (a3 < NOHIT) stk[(sp++) * 64 + lane] = r3;
-  if (a2 < NOHIT) stk[(sp++) * 64 + lane] = r2;
-  if (a1 < NOHIT) stk[(sp++) * 64 + lane] = r1;
+  if (stk.lds_only(sp + 3)) {  // (every push of a shallow walk: LDS stores only)
+    if (a3 < NOHIT) stk.put_lds(sp++, r3);
+    if (a2 < NOHIT) stk.put_lds(sp++, r2);
+    if (a1 < NOHIT) stk.put_lds(sp++, r1);
+  } else {
+    if (a3 < NOHIT) stk.put(sp++, r3);
+    if (a2 < NOHIT) stk.put(sp++, r2);
+    if (a1 < NOHIT) stk.put(sp++, r1);
+  }
   ref = r0;
   return true;
 }
 
 // Start a query; false if it is already complete (empty scene or the root
 // box is missed: KdTree::intersectList starts with the root's bbox test).
-template <bool STATS, int QMODE>
-RT_HD bool trav_init(Trav& T, const DevScene& S, const dvec3& P, const dvec3& D, const double tp, const int rp,
+template <bool STATS, int QMODE, class TR>
+RT_HD bool trav_init(TR& T, const DevScene& S, const dvec3& P, const dvec3& D, const double tp, const int rp,
                      const int sq, const double tlimit, Counters& C) {
-  T.P = P;
-  T.D = D;
   T.tp = tp;
   T.rp = rp;
   T.sq = sq;
@@ -171,21 +289,20 @@ RT_HD bool trav_init(Trav& T, const DevScene& S, const dvec3& P, const dvec3& D,
   if (QMODE != Q_ANY) T.closest = QMODE == Q_CLOSEST;  // Q_ANY: set by the caller first
   if (S.n_snodes == 0) return false;
   T.tlo = QMODE == Q_CLOSEST ? -RTX_INF : tp - S.margin;  // Q_ANY: tp = -inf for a closest query
-  T.ri = ray_inv(D);
-  T.rf = ray_f(P, D, T.ri);
+  const RayInv ri = ray_inv(D);
+  T.cold.set(P, D, ri);
+  T.rf = ray_f(P, D, ri);
   if (STATS) {
     C.nodes++;
     C.queries++;
   }
   double a, b;
-  if (!box_test(S.sroot.lo, S.sroot.hi, P, D, T.ri, a, b) || a > T.bt + S.margin || b < T.tlo) return false;
+  if (!box_test(S.sroot.lo, S.sroot.hi, P, D, ri, a, b) || a > T.bt + S.margin || b < T.tlo) return false;
   T.sp = 0;
   T.ref = S.sroot.ref;
   T.mode = 0;
   T.oc = 0;
   T.oe = 0;
-  T.lp = mk3(0, 0, 0);
-  T.ld = mk3(0, 0, 0);
   T.len = 1.0;
   T.mbest = RTX_INF;
   T.moi = 0;
@@ -199,10 +316,9 @@ RT_HD bool trav_init(Trav& T, const DevScene& S, const dvec3& P, const dvec3& D,
 
 // Every field a constant (a walk no lane continues): lets the compiler see
 // the walk's registers as free between queries.
-RT_HD void trav_reset(Trav& T) {
-  T.P = T.D = T.lp = T.ld = mk3(0.0, 0.0, 0.0);
-  T.ri.inv = mk3(0.0, 0.0, 0.0);
-  T.ri.fast = true;
+template <class TR>
+RT_HD void trav_reset(TR& T) {
+  T.cold.reset();
   T.rf = RayF{0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   T.tp = T.tlimit = T.tlo = T.bt = T.len = T.mbest = 0.0;
   T.rp = T.sq = T.bobj = T.bsub = T.sp = T.ref = T.mode = T.oc = T.oe = 0;
@@ -213,11 +329,12 @@ RT_HD void trav_reset(Trav& T) {
 // The lane's next unit is a 4-wide record (scene or mesh): the cheap step.
 // Objects (mode 1: world-box test, transform to the mesh frame) and mesh
 // leaves (exact face tests) are the costly ones.
-RT_HD bool trav_at_record(const Trav& T) { return T.mode != 1 && T.ref >= 0; }
+template <class TR>
+RT_HD bool trav_at_record(const TR& T) { return T.mode != 1 && T.ref >= 0; }
 
 // One unit of the walk; true when the query is complete.
-template <bool STATS, int QMODE>
-RT_HD bool trav_step(Trav& T, const DevScene& S, int* __restrict__ stk, const int lane, Counters& C) {
+template <bool STATS, int QMODE, class TR, class STK>
+RT_HD bool trav_step(TR& T, const DevScene& S, const STK& stk, Counters& C) {
   const bool closest = QMODE == Q_CLOSEST || (QMODE == Q_ANY && T.closest);
   const double tp = T.tp, tlimit = T.tlimit, tlo = T.tlo;
   const int rp = T.rp, sq = T.sq;
@@ -243,11 +360,11 @@ RT_HD bool trav_step(Trav& T, const DevScene& S, int* __restrict__ stk, const in
       if (closest && T.mhave) hi = rtm::gmin(hi, T.mbest + S.lmargin);
       lo = closest ? -RTX_INF : tlo * len * (1.0 - 1e-12) - S.lmargin;
     }
-    if (visit4<STATS>(rec, T.rf, hi, lo, stk, lane, sp, ref, C)) return false;
+    if (visit4<STATS>(rec, T.rf, hi, lo, stk, sp, ref, C)) return false;
     if (!mesh) {
       if (sp == 0) return true;
       --sp;
-      ref = stk[sp * 64 + lane];
+      ref = stk.get(sp);
       return false;
     }
   }
@@ -264,9 +381,10 @@ RT_HD bool trav_step(Trav& T, const DevScene& S, int* __restrict__ stk, const in
     if (STATS) C.objects++;
     double a, b;
     // Geometry::intersect's world-box test (scene.cpp:15) + prune
-    if (box_test(o.wmin, o.wmax, T.P, T.D, T.ri, a, b) && !(a > bt + S.margin) && !(b < tlo)) {
+    const dvec3 wP = T.cold.getP(), wD = T.cold.getD();
+    if (box_test(o.wmin, o.wmax, wP, wD, T.cold.getRI(), a, b) && !(a > bt + S.margin) && !(b < tlo)) {
       dvec3 pos, dir;
-      obj_local(o, T.P, T.D, pos, dir);
+      obj_local(o, wP, wD, pos, dir);
       const double ln = rtm::length(dir);
       dir = rtm::normalize(dir);
       if (o.type == RTX_OBJ_TRIMESH) {
@@ -278,8 +396,7 @@ RT_HD bool trav_step(Trav& T, const DevScene& S, int* __restrict__ stk, const in
           const double whi = (bt + S.margin) * ln * (1.0 + 1e-12);
           const double lo = closest ? -RTX_INF : tlo * ln * (1.0 - 1e-12) - S.lmargin;
           if (box_test(mr.lo, mr.hi, pos, dir, mri, ma, mb) && !(ma > whi) && !(mb < lo)) {
-            T.lp = pos;
-            T.ld = dir;
+            T.cold.setL(pos, dir);
             T.rf = ray_f(pos, dir, mri);
             T.len = ln;
             T.moi = oi;
@@ -450,7 +567,7 @@ RT_HD bool trav_step(Trav& T, const DevScene& S, int* __restrict__ stk, const in
     if (T.oc == T.oe) {
       if (sp == 0) return true;
       --sp;
-      ref = stk[sp * 64 + lane];
+      ref = stk.get(sp);
       T.mode = 0;
     }
     return false;
@@ -466,26 +583,27 @@ RT_HD bool trav_step(Trav& T, const DevScene& S, int* __restrict__ stk, const in
     // strictly farther than the mesh's best; next: farther than the
     // current best key) — tri_hit stops before the edge tests
     const double tcap = closest && T.mhave ? rtm::gmin(whi, T.mbest) : whi;
+    const dvec3 lp = T.cold.getLP(), ld = T.cold.getLD();
     for (int f = f0; f < f1; ++f) {
       if (STATS) C.tris++;
       double tf;
       // the face's reference rank (ties, answer) and leaf, issued before the
       // face's own loads so they arrive in the same burst
       const TMeta meta = S.tmeta[T.mfoff + f];
-      const bool hit = tri_hit(S.tfaces[T.mfoff + f], T.lp, T.ld, tcap, tf);
+      const bool hit = tri_hit(S.tfaces[T.mfoff + f], lp, ld, tcap, tf);
       pin(meta.rank);
       pin(meta.leaf);
       if (hit) {
         const int rk = meta.rank;
         if (closest) {
-          if ((!T.mhave || tf < T.mbest || (tf == T.mbest && rk < T.mface)) && leaf_ok(T, S, meta.leaf)) {
+          if ((!T.mhave || tf < T.mbest || (tf == T.mbest && rk < T.mface)) && leaf_ok(lp, ld, S, meta.leaf)) {
             T.mbest = tf;
             T.mface = rk;
             T.mhave = true;
           }
         } else {
           const double tw = tf / len;
-          if (key_less(tp, rp, sq, tw, T.moi, rk) && tw <= tlimit && leaf_ok(T, S, meta.leaf)) {
+          if (key_less(tp, rp, sq, tw, T.moi, rk) && tw <= tlimit && leaf_ok(lp, ld, S, meta.leaf)) {
             if (!have || key_less(tw, T.moi, rk, bt, bobj, bsub)) {
               bt = tw;
               bobj = T.moi;
@@ -499,11 +617,11 @@ RT_HD bool trav_step(Trav& T, const DevScene& S, int* __restrict__ stk, const in
   }
   if (sp > T.mbase) {
     --sp;
-    ref = stk[sp * 64 + lane];
+    ref = stk.get(sp);
     return false;
   }
   // mesh finished: Trimesh::intersectLocal's result enters Scene::intersect
-  T.rf = ray_f(T.P, T.D, T.ri);
+  T.rf = ray_f(T.cold.getP(), T.cold.getD(), T.cold.getRI());
   if (closest && T.mhave) {
     const double tw = T.mbest / len;
     if (!have || tw < bt || (tw == bt && T.moi < bobj)) {
@@ -519,7 +637,7 @@ RT_HD bool trav_step(Trav& T, const DevScene& S, int* __restrict__ stk, const in
   }
   if (sp == 0) return true;
   --sp;
-  ref = stk[sp * 64 + lane];
+  ref = stk.get(sp);
   T.mode = 0;
   return false;
 }
@@ -533,11 +651,11 @@ RT_HD bool traverse(const DevScene& S, const int qmode, const dvec3& P, const dv
   Trav T;
   if (qmode == Q_CLOSEST) {
     if (trav_init<STATS, Q_CLOSEST>(T, S, P, D, tp, rp, sq, tlimit, C))
-      while (!trav_step<STATS, Q_CLOSEST>(T, S, stk, lane, C)) {
+      while (!trav_step<STATS, Q_CLOSEST>(T, S, StackLDS{stk + lane}, C)) {
       }
   } else {
     if (trav_init<STATS, Q_NEXT>(T, S, P, D, tp, rp, sq, tlimit, C))
-      while (!trav_step<STATS, Q_NEXT>(T, S, stk, lane, C)) {
+      while (!trav_step<STATS, Q_NEXT>(T, S, StackLDS{stk + lane}, C)) {
       }
   }
   bt = T.bt;
@@ -555,7 +673,7 @@ RT_HD bool traverse_any(const DevScene& S, const int qmode, const dvec3& P, cons
   Trav T;
   T.closest = qmode == Q_CLOSEST;
   if (trav_init<STATS, Q_ANY>(T, S, P, D, T.closest ? -RTX_INF : tp, rp, sq, tlimit, C))
-    while (!trav_step<STATS, Q_ANY>(T, S, stk, lane, C)) {
+    while (!trav_step<STATS, Q_ANY>(T, S, StackLDS{stk + lane}, C)) {
     }
   bt = T.bt;
   bobj = T.bobj;

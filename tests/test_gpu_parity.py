@@ -477,3 +477,36 @@ def test_fork_depth_first_render_is_depth3(pkg, capfd, monkeypatch):
     monkeypatch.setenv("RTX_FORK_DEPTH", "3")
     b = pkg.DeviceScene(pkg.HostScene(scene_path(scene)), 0).render(opts, want_f64=True)
     assert np.array_equal(a["rgb"], b["rgb"])
+
+
+@pytest.mark.parametrize("scene,flags,tile,nshards", [
+    ("trimesh2.ray", "-w 96 -r 5 -O r -A 4", 0, 1),
+    ("trimesh2_glass.ray", "-w 96 -r 5 -O r -A 2", 0, 1),
+    ("trimesh2.ray", "-w 64 -r 5 -O d -A 2.5 -B 4 -C 0.05", 0, 1),
+    ("hitchcock.ray", "-w 100 -r 2 -O r -A 2", 32, 3),
+    ("spheres_overlap.ray", "-w 64 -r 5 -O r -A 2", 0, 1),
+], ids=["trimesh2", "glass", "dof", "hitchcock_x3", "spheres"])
+def test_short_stack_overflow_identical(pkg, orc, monkeypatch, scene, flags, tile, nshards):
+    """The trace kernels' short stacks (StackShort: the first k entries in
+    LDS, deeper ones in per-thread overflow columns in HBM — what a scene
+    with a deep mesh tree, the 1M-face dragon, runs on) give the same walk
+    as whole LDS stacks: with k = 2 (RTX_TEST_LDS_STACK) most walks spill
+    into the overflow columns, and every frame must equal the default
+    render bit for bit (the traversal's answers do not depend on where its
+    pending entries live, kdTree.h:100-117) and the CPU restatement."""
+    if os.environ.get("RTX_MEGAKERNEL") not in (None, "", "0"):
+        pytest.skip("the megakernel has no trace kernels")
+    path = scene_path(scene)
+    opts = pkg.RenderOptions.from_cli(flags.split())
+    dev = pkg.DeviceScene(pkg.HostScene(path), 0)
+    kw = dict(tile=tile, shard=nshards - 1, nshards=nshards, packed=nshards > 1) if nshards > 1 else {}
+    want = dev.render(opts, want_f64=True, **kw)
+    monkeypatch.setenv("RTX_TEST_LDS_STACK", "2")
+    dev2 = pkg.DeviceScene(pkg.HostScene(path), 0)
+    for _ in range(2):  # (the first render and one sized from its history)
+        got = dev2.render(opts, want_f64=True, **kw)
+        assert np.array_equal(got["rgb8"], want["rgb8"])
+        assert np.array_equal(got["rgb"], want["rgb"])
+    if nshards == 1:
+        ref = orc.render(pkg, path, opts, want_hits=False)
+        assert np.abs(got["rgb"] - ref["rgb"]).max() <= 1e-4
