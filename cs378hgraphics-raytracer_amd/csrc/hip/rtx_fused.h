@@ -515,15 +515,15 @@ __device__ __forceinline__ void cam_start(LaneRef& LR, const FrameParams& F, Rtx
 // its first camera ray straight away — what advance_fused (claim, ST_CAM,
 // ST_POP) would have done, without the pending-stack entry and the query
 // record round trip.  False: the slot has no sample (left idle).
-// (out of line, and only in the first iteration's instantiation of the
-// closest-hit kernel, trace_kernel<..., CAM = true>: inlined there its
-// registers add to the traversal's peak, and the backend fails on the
-// inlined STATS instantiation, "Subtarget requires even aligned vector
+// (only in the first iteration's instantiation of the closest-hit kernel,
+// trace_kernel<..., CAM = true>; inlined there since the cold traversal state
+// moved to LDS, out of line — cam_first_claim — in the instantiations the
+// backend fails on inlined, "Subtarget requires even aligned vector
 // registers")
-// (arguments by value: a reference would put the caller's LaneRef and
-// counters in scratch for the call)
-__device__ __noinline__ bool cam_first_claim(const LaneMem lm, int slot, const FrameParams& F,
-                                             RtxHitRecord* __restrict__ hits) {
+// (the out-of-line version takes its arguments by value: a reference would
+// put the caller's LaneRef and counters in scratch for the call)
+__device__ __forceinline__ bool cam_first_claim_inl(const LaneMem lm, int slot, const FrameParams& F,
+                                                   RtxHitRecord* __restrict__ hits) {
   LaneRef LR(lm, static_cast<size_t>(slot));
   lane_init(LR);
   claim_sample(LR, F, hits, slot);
@@ -537,6 +537,10 @@ __device__ __noinline__ bool cam_first_claim(const LaneMem lm, int slot, const F
   LR.qmode() = Q_CLOSEST;
   LR.st() = ST_HIT;
   return true;
+}
+__device__ __noinline__ bool cam_first_claim(const LaneMem lm, int slot, const FrameParams& F,
+                                             RtxHitRecord* __restrict__ hits) {
+  return cam_first_claim_inl(lm, slot, F, hits);
 }
 // its ray again at shading time (the walk's registers are reused meanwhile)
 __device__ __forceinline__ QRay cam_first_ray(const LaneRef& LR, const FrameParams& F) {

@@ -1984,7 +1984,12 @@ __global__ void __launch_bounds__(WG, !FUSED ? RTX_TRACE_WAVES : (MODE == Q_CLOS
         } else if (MODE == Q_CLOSEST && cam) {  // claim the slot's first sample, its first camera ray
           const int slot = SA.slot_off + static_cast<int>(kq);
           LaneRef LR(lm, static_cast<size_t>(slot));
-          noq = !cam_first_claim(lm, slot, *SA.Fp, SA.hits);
+          // inlined (scratch 60-76 -> 16 B, headline -0.8 %); out of line in
+          // the counting and short-stack instantiations, on which the backend
+          // stops ("Subtarget requires even aligned vector registers": a
+          // 64-bit scratch reload into an odd register pair)
+          noq = STATS || SHORT ? !cam_first_claim(lm, slot, *SA.Fp, SA.hits)
+                               : !cam_first_claim_inl(lm, slot, *SA.Fp, SA.hits);
           if (!noq) {
             if (STATS) C.camera++;
             // the ray from the claim's (sx, sy), here rather than through an
