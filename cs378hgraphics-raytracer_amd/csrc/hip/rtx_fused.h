@@ -150,6 +150,7 @@ __device__ __forceinline__ void emit_walk(const WalkEmit& E, bool on, int slot, 
     k = base + lane_prefix(m);
   }
   const size_t cap = E.q.cap;
+  k = RTX_CHK(CHK_QREC, k, cap);
   double* d = E.q.d;
   d[QF_PX * cap + k] = pb.x;
   d[QF_PY * cap + k] = pb.y;
@@ -579,7 +580,8 @@ __device__ __forceinline__ void advance_fused(LaneRef& LR, const DevScene& S, co
             break;
           }
           if (F.cam_split) {  // one camera ray of a DoF sample: its own sum (reduce_kernel scales, clamps)
-            const int64_t u = static_cast<int64_t>(LR.sample_slot()) * F.ncam + (LR.cam_end() - 1);
+            const int64_t u = RTX_CHK(CHK_SAMPLE, static_cast<int64_t>(LR.sample_slot()) * F.ncam + (LR.cam_end() - 1),
+                                      F.chk_samples * F.ncam);
             sbuf[u * 3 + 0] = LR.acc().x;
             sbuf[u * 3 + 1] = LR.acc().y;
             sbuf[u * 3 + 2] = LR.acc().z;
@@ -710,8 +712,8 @@ __global__ void __launch_bounds__(WG, STATS ? 1 : RTX_FUSED_ADV_WAVES)
     base = __shfl(base, 0);
     if (qm == Q_CLOSEST) {
       const size_t cap = q0.cap, n = lm.n;
-      const size_t k = base + lane_prefix(mask);
-      const double* b = pbuf + static_cast<size_t>(L.top()) * 13 * n + slot;
+      const size_t k = RTX_CHK(CHK_QREC, base + lane_prefix(mask), cap);
+      const double* b = pbuf + static_cast<size_t>(RTX_CHK(CHK_PEND, L.top(), pend_cap)) * 13 * n + slot;
       q0.slot[k] = slot;
       q0.d[0 * cap + k] = b[0 * n];
       q0.d[1 * cap + k] = b[1 * n];
@@ -728,7 +730,7 @@ __global__ void __launch_bounds__(WG, STATS ? 1 : RTX_FUSED_ADV_WAVES)
     unsigned int base = 0;
     if (lane == 0) base = atomicAdd(&counters[out_cnt], static_cast<unsigned int>(__popcll(alive)));
     base = __shfl(base, 0);
-    if (live) live_out[base + lane_prefix(alive)] = slot;
+    if (live) live_out[RTX_CHK(CHK_LIVE, base + lane_prefix(alive), F.chk_live)] = slot;
   }
   if (FORK && free_ids) {
     // a fork slot whose sub-tree ended here goes on the group's free list
@@ -740,7 +742,7 @@ __global__ void __launch_bounds__(WG, STATS ? 1 : RTX_FUSED_ADV_WAVES)
       unsigned int base = 0;
       if (lane == 0) base = atomicAdd(&counters[CNT_FREE], static_cast<unsigned int>(__popcll(fm)));
       base = __shfl(base, 0);
-      if (freed) free_ids[base + lane_prefix(fm)] = slot;
+      if (freed) free_ids[RTX_CHK(CHK_FREE, base + lane_prefix(fm), F.chk_live)] = slot;
     }
   }
   if (STATS) {

@@ -132,7 +132,41 @@ struct FrameParams {
   // level's are aregs[0 .. n_samples / spp) (adapt_stats_kernel)
   int adapt;
   const ARegion* aregs;
+  // bounds of the frame's device buffers (the bounds-check build's RTX_CHK,
+  // DESIGN.md §5): bucket owners (bidx / fmask), wterm units, sample-buffer
+  // entries, per-group live-list entries
+  int64_t chk_units, chk_samples;
+  int chk_wunits, chk_live;
 };
+
+// ---- bounds-check build (-DRTX_BOUNDS_CHECK, tools/build_variants.sh): every
+// slot, query-record, live-list, bucket, pick, wterm and stack index the
+// wavefront kernels compute is checked against its buffer's extent; the
+// first violation (site, index, bound) and a count go to rtx_chk_state and
+// the access is redirected to index 0 instead of faulting; rtx_render (host
+// buffers) and rtx_frame_status (device buffers) report a violation as
+// RTX_ERR_INVALID.  Without the flag RTX_CHK(site, i, n) is i.
+#ifdef RTX_BOUNDS_CHECK
+__device__ unsigned long long rtx_chk_state[3];  // count, first (site << 48 | index), its bound
+__device__ __noinline__ long long rtx_chk_fail(int site, long long i, long long n) {
+  const unsigned long long c = atomicAdd(&rtx_chk_state[0], 1ull);
+  if (c == 0ull) {
+    rtx_chk_state[1] = (static_cast<unsigned long long>(site) << 48) | (static_cast<unsigned long long>(i) & 0xffffffffffffull);
+    rtx_chk_state[2] = static_cast<unsigned long long>(n);
+  }
+  return 0;
+}
+#define RTX_CHK(site, i, n) \
+  ((static_cast<long long>(i) >= 0 && static_cast<long long>(i) < static_cast<long long>(n)) ? (i) \
+                                                                                            : static_cast<std::remove_reference_t<decltype(i)>>(rtx_chk_fail(site, static_cast<long long>(i), static_cast<long long>(n))))
+constexpr bool kBoundsCheck = true;
+#else
+#define RTX_CHK(site, i, n) (i)
+constexpr bool kBoundsCheck = false;
+#endif
+// sites
+enum { CHK_SLOT = 1, CHK_QREC, CHK_LIVE, CHK_FREE, CHK_BUNIT, CHK_BSET, CHK_BPOS, CHK_PEND, CHK_STACK, CHK_LIGHT,
+       CHK_PICK, CHK_WUNIT, CHK_SAMPLE };
 
 // Tile deal: deal index d = shard + k * nshards is tile row d / tiles_x,
 // column (d % tiles_x + row) % tiles_x — row-major with each row rotated by
@@ -466,7 +500,8 @@ struct LaneRef {
 #undef M_I
 #undef M_D
 #undef M_V
-  __device__ __forceinline__ LaneRef(const LaneMem& mm, size_t gg) : m(mm), g(static_cast<unsigned int>(gg)) {}
+  __device__ __forceinline__ LaneRef(const LaneMem& mm, size_t gg)
+      : m(mm), g(static_cast<unsigned int>(RTX_CHK(CHK_SLOT, gg, mm.n))) {}
   // Compiler barrier + opaque lane index: the state is memory, re-read per
   // step, and every field address is recomputed from (uniform base, g) where
   // it is used.  Without the opaque g, LLVM hoists the 43 per-lane 64-bit
@@ -660,6 +695,7 @@ struct ForkCtx {
   int* live_out;
   unsigned int* live_cnt;
   const int* free_ids;
+  int live_cap;  // entries of the group's live and free lists (the bounds check)
 };
 
 // lanes of the wave below the calling lane in `mask` (mbcnt)
@@ -699,7 +735,7 @@ __device__ __forceinline__ int fork_claim(const ForkCtx* fk, bool want) {
   fbase = __shfl(fbase, leader);
   if (!want) return -1;
   const int r = static_cast<int>(lane_prefix(m));
-  if (r < avail) return fk->free_ids[old - 1 - r];
+  if (r < avail) return fk->free_ids[RTX_CHK(CHK_FREE, old - 1 - r, fk->live_cap)];
   const unsigned int idx = static_cast<unsigned int>(fbase + (r - avail));
   return idx < fk->spare_n ? fk->spare_base + static_cast<int>(idx) : -1;
 }
@@ -713,7 +749,7 @@ __device__ __forceinline__ void fork_join(const ForkCtx* fk, int T) {
   if (static_cast<int>(threadIdx.x & 63) == leader)
     base = atomicAdd(fk->live_cnt, static_cast<unsigned int>(__popcll(m)));
   base = __shfl(base, leader);
-  if (T >= 0) fk->live_out[base + lane_prefix(m)] = T;
+  if (T >= 0) fk->live_out[RTX_CHK(CHK_LIVE, base + lane_prefix(m), fk->live_cap)] = T;
 }
 
 // pending-ray entry field 12: bucket (the ray's heap position if it is a
@@ -727,12 +763,14 @@ __device__ __forceinline__ double pend_code(int pos, int depth, int kind) {
 // one lane at a time, in that lane's ray order; the fmask bit says whether
 // the bucket already holds a sum)
 __device__ __forceinline__ void bucket_add(const FrameParams& F, int s, int b, const dvec3& c) {
+  s = RTX_CHK(CHK_BUNIT, s, F.chk_units);
+  b = RTX_CHK(CHK_BPOS, b - 2, F.fork_npos) + 2;
   const int set = F.bidx[s];
   if (set < 0) {  // (never: the root takes the set before its children exist)
     atomicOr(F.bover, 2u);
     return;
   }
-  double* f = F.fbuf + (static_cast<int64_t>(set) * F.fork_npos + (b - 2)) * 3;
+  double* f = F.fbuf + (static_cast<int64_t>(RTX_CHK(CHK_BSET, set, F.bcap)) * F.fork_npos + (b - 2)) * 3;
   const unsigned int bit = 1u << (b - 2);
   const unsigned int old = atomicOr(&F.fmask[s], bit);
   if (old & bit) {
@@ -760,6 +798,7 @@ __device__ __forceinline__ void bucket_alloc(const FrameParams& F, int s, bool w
   if (static_cast<int>(threadIdx.x & 63) == leader) base = atomicAdd(F.bcnt, static_cast<unsigned int>(__popcll(m)));
   base = __shfl(base, leader);
   if (!want) return;
+  s = RTX_CHK(CHK_BUNIT, s, F.chk_units);
   const unsigned int idx = base + lane_prefix(m);
   if (idx < static_cast<unsigned int>(F.bcap)) {
     F.bidx[s] = static_cast<int>(idx);
@@ -895,6 +934,7 @@ __device__ __forceinline__ void advance_lane(LaneRef& LR, const DevScene& S, con
             // sum; reduce_kernel adds the sample's rays in order, scales and
             // clamps
             const int64_t u = static_cast<int64_t>(LR.sample_slot()) * F.ncam + (LR.cam_end() - 1);
+            (void)RTX_CHK(CHK_SAMPLE, u, F.chk_samples * F.ncam);
             sbuf[u * 3 + 0] = LR.acc().x;
             sbuf[u * 3 + 1] = LR.acc().y;
             sbuf[u * 3 + 2] = LR.acc().z;
@@ -1629,9 +1669,10 @@ __device__ __forceinline__ void claim_sample(LaneRef& L, const FrameParams& F, R
       L.sx() = double(pi) / (double(P.width) * ssx);  // tracePixel (RayTracer.cpp:87-88)
       L.sy() = double(pj) / (double(P.height) * ssy);
     }
-    L.sample_slot() = static_cast<int>(oidx * F.spp + smp);
+    L.sample_slot() = static_cast<int>(RTX_CHK(CHK_SAMPLE, oidx * F.spp + smp, F.chk_samples));
     // the buckets' owner: the sample, or with the DoF split its camera ray
     L.bunit() = F.cam_split ? L.sample_slot() * F.ncam + cam0 : L.sample_slot();
+    if (F.fork_on) L.bunit() = RTX_CHK(CHK_BUNIT, L.bunit(), F.chk_units);
     if (F.fork_on) {  // no bucket written yet (forks come later), no set taken
       F.fmask[L.bunit()] = 0u;
       F.bidx[L.bunit()] = -1;
@@ -1672,7 +1713,7 @@ __global__ void __launch_bounds__(WG, RTX_ADV_WAVES) advance_kernel(DevScene S, 
   // first iteration, which only starts camera rays)
   const ForkCtx fk = {counters + CNT_FORK, slot_off + F.wf_gsamp,
                       first ? 0u : static_cast<unsigned int>(F.wf_gs - F.wf_gsamp), live_out, counters + out_cnt,
-                      nullptr};
+                      nullptr, F.chk_live};
   if (valid && (L.st() != ST_IDLE || slot_unit(F, slot, L.kdone()) >= 0)) {
     // the previous iteration's query result is already in L.bt()/bobj/bsub/bhave
     L.qmode() = Q_NONE;
@@ -1723,7 +1764,7 @@ __global__ void __launch_bounds__(WG, RTX_ADV_WAVES) advance_kernel(DevScene S, 
     unsigned int base = 0;
     if (lane == 0) base = atomicAdd(&counters[out_cnt], static_cast<unsigned int>(__popcll(alive)));
     base = __shfl(base, 0);
-    if (live) live_out[base + lane_prefix(alive)] = slot;
+    if (live) live_out[RTX_CHK(CHK_LIVE, base + lane_prefix(alive), F.chk_live)] = slot;
   }
   if (STATS) {
     stats_add(C, stats, lane);
@@ -1884,6 +1925,10 @@ __global__ void __launch_bounds__(WG, !FUSED ? RTX_TRACE_WAVES : (MODE == Q_CLOS
       size_t k = kq;
       asm volatile("" : "+v"(k));
       const int code = Q.iv[1 * cap + k];
+      (void)RTX_CHK(CHK_LIGHT, walk_light(code), Sg->n_lights);
+      (void)RTX_CHK(CHK_PICK, walk_pick(code) + 1, Sg->ss_res + 1);
+      (void)RTX_CHK(CHK_WUNIT, SA.Fp->lunit[walk_light(code)] + (walk_pick(code) < 0 ? 0 : 2 + walk_pick(code)),
+              SA.Fp->chk_wunits);
       const RtxLight& L = Sg->lights[walk_light(code)];
       const dvec3 pb = mk3(Q.d[QF_PX * cap + k], Q.d[QF_PY * cap + k], Q.d[QF_PZ * cap + k]);
       const dvec3 sdir = walk_dir(*Sg, code, pb);  // as the emitter computed it
@@ -1944,7 +1989,7 @@ __global__ void __launch_bounds__(WG, !FUSED ? RTX_TRACE_WAVES : (MODE == Q_CLOS
       } else if (pend) {
         const FrameParams& F = *SA.Fp;
         const ForkCtx fk = {counters + CNT_FORK, SA.slot_off + F.wf_gsamp, static_cast<unsigned int>(F.wf_gs - F.wf_gsamp),
-                            SA.live_out, counters + SA.out_cnt, SA.free_ids};
+                            SA.live_out, counters + SA.out_cnt, SA.free_ids, F.chk_live};
         const WalkEmit we = {SA.qn, counters + CNT_Q + CNT_LINE, -1, 0};
         LaneRef LR(lm, static_cast<size_t>(cam ? SA.slot_off + static_cast<int>(kq) : Q.slot[kq]));
         const QRay qr = cam ? cam_first_ray(LR, F) : qray_at(LR, SA.pbuf, lm.n);
@@ -1974,7 +2019,7 @@ __global__ void __launch_bounds__(WG, !FUSED ? RTX_TRACE_WAVES : (MODE == Q_CLOS
       const unsigned int nidle = __popcll(idle);
       const unsigned int take = avail < nidle ? avail : nidle;
       if (!active && !pend && rank < take) {
-        kq = static_cast<size_t>(qnext) + rank;
+        kq = RTX_CHK(CHK_QREC, static_cast<size_t>(qnext) + rank, cap);
         bool noq = false;
         if (!FUSED) {
           const dvec3 P = mk3(Q.d[0 * cap + kq], Q.d[1 * cap + kq], Q.d[2 * cap + kq]);
@@ -1985,11 +2030,11 @@ __global__ void __launch_bounds__(WG, !FUSED ? RTX_TRACE_WAVES : (MODE == Q_CLOS
           const int slot = SA.slot_off + static_cast<int>(kq);
           LaneRef LR(lm, static_cast<size_t>(slot));
           // inlined (scratch 60-76 -> 16 B, headline -0.8 %); out of line in
-          // the counting and short-stack instantiations, on which the backend
+          // the counting, short-stack and bounds-check instantiations, on which the backend
           // stops ("Subtarget requires even aligned vector registers": a
           // 64-bit scratch reload into an odd register pair)
-          noq = STATS || SHORT ? !cam_first_claim(lm, slot, *SA.Fp, SA.hits)
-                               : !cam_first_claim_inl(lm, slot, *SA.Fp, SA.hits);
+          noq = STATS || SHORT || kBoundsCheck ? !cam_first_claim(lm, slot, *SA.Fp, SA.hits)
+                                               : !cam_first_claim_inl(lm, slot, *SA.Fp, SA.hits);
           if (!noq) {
             if (STATS) C.camera++;
             // the ray from the claim's (sx, sy), here rather than through an
@@ -2042,7 +2087,9 @@ __global__ void __launch_bounds__(WG, !FUSED ? RTX_TRACE_WAVES : (MODE == Q_CLOS
       }
       if (go) {
         if (STATS) qsteps++;
-        if (trav_step<STATS, MODE>(T, S, stk, C)) {
+        const bool qdone = trav_step<STATS, MODE>(T, S, stk, C);
+        (void)RTX_CHK(CHK_STACK, T.sp, stack_cap + 1);  // (sp <= stack_cap: the LDS or overflow columns held every push)
+        if (qdone) {
           if (FUSED) pend = true;
           else finish();
           active = false;
@@ -2794,10 +2841,35 @@ static bool collect_check(SceneState* st, FrameCtx& X, bool wait) {
   return true;
 }
 
+// The bounds-check build's record (RTX_CHK): a violation since the last
+// read is an error, reported with its site, index and bound.  (Waits for
+// the device.)
+static rtx_status bounds_check_report() {
+#ifdef RTX_BOUNDS_CHECK
+  unsigned long long h[3] = {0, 0, 0};
+  HIP_TRY(hipDeviceSynchronize());
+  HIP_TRY(hipMemcpyFromSymbol(h, HIP_SYMBOL(rtx_chk_state), sizeof(h)));
+  if (h[0] != 0ull) {
+    const unsigned long long z[3] = {0, 0, 0};
+    HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(rtx_chk_state), z, sizeof(z)));
+    g_err = "rtx bounds check: " + std::to_string(h[0]) + " out-of-range index(es); the first at site " +
+            std::to_string(h[1] >> 48) + ", index " + std::to_string(static_cast<long long>(h[1] & 0xffffffffffffull)) +
+            ", bound " + std::to_string(h[2]);
+    fprintf(stderr, "%s\n", g_err.c_str());
+    return RTX_ERR_INVALID;
+  }
+#endif
+  return RTX_OK;
+}
+
 rtx_status rtx_frame_status(void* scene, int64_t* first_bad, int64_t* bad_frames) {
   if (!scene) return RTX_ERR_INVALID;
   SceneState* st = static_cast<SceneState*>(scene);
   HIP_TRY(hipSetDevice(st->device));
+  {
+    const rtx_status bc = bounds_check_report();
+    if (bc != RTX_OK) return bc;
+  }
   for (FrameCtx& X : st->cx) collect_check(st, X, true);
   const int64_t fb = st->bad_first, nb = st->bad_n;
   st->bad_first = -1;
@@ -3171,6 +3243,7 @@ static rtx_status render_once(SceneState* st, const RtxRenderParams* params, uin
     F.cam_split = 1;
     F.n_samples *= F.ncam;
   }
+  F.chk_samples = static_cast<int64_t>(npix) * F.spp;
   if (F.cam_split && hits) HIP_TRY(hipMemsetAsync(d_hits, 0xff, npix * F.spp * sizeof(RtxHitRecord), ws));
   if (!(adaptive && megakernel)) {
     const size_t need = size_t(npix) * F.spp * (F.cam_split ? F.ncam : 1) * 3 * sizeof(double);
@@ -3635,6 +3708,15 @@ static rtx_status render_once(SceneState* st, const RtxRenderParams* params, uin
     if ((rc = fit(&X->d_wf, &X->wf_bytes, size_t(G) * (bytes_qc + bytes_qn + 2 * al(gs * sizeof(int))))) != RTX_OK)
       return rc;
     F.fuse = fuse ? 1 : 0;
+    F.chk_units = fork_ok ? static_cast<int64_t>(nunit_out) : 0;
+    F.chk_wunits = static_cast<int>(n_units);
+    F.chk_live = static_cast<int>(gs);
+#ifdef RTX_BOUNDS_CHECK
+    // (the check's self-test: a live-list bound of 1, so the first group's
+    // second live slot must be reported — profiles/r06i_bounds_check.txt)
+    if (const char* e = getenv("RTX_TEST_CHK_SELFTEST"))
+      if (atoi(e) != 0) F.chk_live = 1;
+#endif
     F.wterm = nullptr;
     if (fuse && nl > 0) {
       if ((rc = fit(reinterpret_cast<void**>(&X->d_wterm), &X->wterm_bytes, n_units * ns * 3 * sizeof(double))) !=
@@ -4343,6 +4425,9 @@ rtx_status rtx_render(void* scene, const RtxRenderParams* params, uint8_t* rgb8,
       return RTX_ERR_FRAME;
     }
   }
+#ifdef RTX_BOUNDS_CHECK
+  if (rc == RTX_OK && (!device_ptrs || stats)) rc = bounds_check_report();
+#endif
   return rc;
 }
 
