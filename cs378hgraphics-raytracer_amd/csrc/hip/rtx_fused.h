@@ -670,11 +670,8 @@ __device__ __forceinline__ void advance_fused(LaneRef& LR, const DevScene& S, co
 // hit's colour, then run the machine to the next closest query (appended to
 // q0 with ballot + popc + mbcnt, the ray read from the slot's pending stack)
 // while walks go to q1 as they are found.
-#ifndef RTX_FUSED_ADV_WAVES
-#define RTX_FUSED_ADV_WAVES RTX_ADV_WAVES
-#endif
 template <bool STATS, bool FORK>
-__global__ void __launch_bounds__(WG, STATS ? 1 : RTX_FUSED_ADV_WAVES)
+__global__ void __launch_bounds__(WG, STATS ? 1 : RTX_ADV_WAVES)
     advance_fused_kernel(DevScene S, const DevScene* __restrict__ Sg, const FrameParams* __restrict__ Fp, LaneMem lm,
                          double* __restrict__ sbuf, RtxHitRecord* __restrict__ hits, double* __restrict__ pbuf,
                          int pend_cap, QList q0, QList q1, unsigned int* __restrict__ counters,

@@ -1850,12 +1850,6 @@ __global__ void __launch_bounds__(WG) tail_kernel(DevScene S, const DevScene* __
 // FUSED Q_CLOSEST: a lane whose query completes shades the hit (shade_hit:
 // colour, walk records, reflection / refraction pushes) before it claims
 // the next query.
-#ifndef RTX_SHADE_WAVES
-#define RTX_SHADE_WAVES RTX_TRACE_WAVES
-#endif
-#ifndef RTX_WALK_WAVES
-#define RTX_WALK_WAVES RTX_TRACE_WAVES
-#endif
 // CAM: the first iteration's instantiation (claims + first camera rays,
 // SA.cam_n > 0); the others carry none of that code, so the later
 // iterations' closest-hit launches keep their own register budget.
@@ -1866,7 +1860,7 @@ __global__ void __launch_bounds__(WG) tail_kernel(DevScene S, const DevScene* __
 // VGPRs the persistent walk state no longer holds; spills of the fused
 // kernels 48 / 64 B -> 0 / 16 B, headline 31.8-32.0 -> 30.6-31.2 ms).
 template <bool STATS, int MODE, bool FUSED = false, bool FORK = false, bool CAM = false, bool SHORT = false>
-__global__ void __launch_bounds__(WG, !FUSED ? RTX_TRACE_WAVES : (MODE == Q_CLOSEST ? RTX_SHADE_WAVES : RTX_WALK_WAVES))
+__global__ void __launch_bounds__(WG, RTX_TRACE_WAVES)
     trace_kernel(DevScene S, const DevScene* __restrict__ Sg, QList Q, unsigned int* __restrict__ counters,
                  LaneMem lm, int stack_cap, unsigned long long* __restrict__ stats, double* __restrict__ wterm,
                  ShadeArgs SA, int clr) {
@@ -3857,7 +3851,7 @@ static rtx_status render_once(SceneState* st, const RtxRenderParams* params, uin
     }
     if (tgrid > per) tgrid = per;
     // the fused kernels' own residency (their launch bounds differ:
-    // RTX_SHADE_WAVES / RTX_WALK_WAVES)
+    // as the plain ones, RTX_TRACE_WAVES, but different register counts)
     int64_t tgrid_c = tgrid, tgrid_n = tgrid;
     int64_t tfull_c = tgrid_full, tfull_n = tgrid_full;  // whole-GPU residency
     if (fuse) {
