@@ -12,7 +12,8 @@ set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 mkdir -p gpurun_out
 for cfg in "$@"; do
+  log="gpurun_out/robust_$(basename "${cfg//[= ]/_}").log"
   env $cfg timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread \
-    > "gpurun_out/robust_${cfg//[= ]/_}.log" 2>&1 || { echo "[$cfg] FAIL"; tail -20 "gpurun_out/robust_${cfg//[= ]/_}.log"; exit 1; }
-  echo "[$cfg] $(tail -1 "gpurun_out/robust_${cfg//[= ]/_}.log")"
+    > "$log" 2>&1 || { echo "[$cfg] FAIL"; tail -20 "$log"; exit 1; }
+  echo "[$cfg] $(tail -1 "$log")"
 done
