@@ -3896,8 +3896,10 @@ static rtx_status render_once(SceneState* st, const RtxRenderParams* params, uin
     const int dbg_level = dbg_env ? atoi(dbg_env) : 0;
     const int check_every = 4;
     // costly traversal units wait while this many lanes of a wave are at a
-    // 4-wide record (trace_kernel; RTX_LEAF_K, 1..65, 65: never wait)
-    int leaf_k = 16;
+    // 4-wide record (trace_kernel; RTX_LEAF_K, 1..65, 65: never wait).  8
+    // since round 6 (cold state in LDS): headline unchanged, R1 247 -> 243,
+    // C4 40.9 -> 40.4 ms against 16 (profiles/r06n_ab_leaf_k.txt)
+    int leaf_k = 8;
     {
       const char* e = getenv("RTX_LEAF_K");
       if (e && atoi(e) > 0) leaf_k = std::min(65, atoi(e));
