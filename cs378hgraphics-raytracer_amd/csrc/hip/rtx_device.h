@@ -243,6 +243,17 @@ struct RayInv {
   bool fast;
 };
 
+// ray_inv's fast flag: no component tiny but nonzero (1 / d past 1e290)
+RT_HD bool ray_inv_fast(const dvec3& d) {
+  bool f = true;
+#pragma unroll
+  for (int a = 0; a < 3; ++a) {
+    const double v = rtm::get(d, a);
+    if (v != 0.0 && fabs(v) < 1e-290) f = false;
+  }
+  return f;
+}
+
 RT_HD RayInv ray_inv(const dvec3& d) {
   RayInv r;
   r.fast = true;

@@ -70,7 +70,7 @@ struct ColdRegs {
     ri.fast = true;
   }
 };
-#define RTX_COLD_FIELDS 10  // doubles per lane in a ColdLDS block (P, D, 1/D, fast)
+#define RTX_COLD_FIELDS 9  // doubles per lane in a ColdLDS block (P, D, 1/D; fast is D's)
 // (The mesh-local ray lp, ld — read by every leaf step — stays in registers:
 // in LDS as well it measured no faster, 31.33 vs 31.32 ms with the short
 // stack, and its 3 KB per wave do not fit beside a whole stack.)
@@ -88,7 +88,7 @@ struct ColdLDS {
   RT_HD RayInv getRI() const {
     RayInv r;
     r.inv = mk3(c[6 * 64], c[7 * 64], c[8 * 64]);
-    r.fast = c[9 * 64] != 0.0;
+    r.fast = ray_inv_fast(getD());  // (ray_inv's flag, from D again)
     return r;
   }
   RT_HD void set(const dvec3& p, const dvec3& d, const RayInv& r) {
@@ -101,7 +101,6 @@ struct ColdLDS {
     c[6 * 64] = r.inv.x;
     c[7 * 64] = r.inv.y;
     c[8 * 64] = r.inv.z;
-    c[9 * 64] = r.fast ? 1.0 : 0.0;
   }
   RT_HD void reset() { lp = ld = mk3(0.0, 0.0, 0.0); }
 };
@@ -710,14 +709,29 @@ inline bool build_node4(const RtxNode* nodes, int n, std::vector<DevNode4>& out,
     out.emplace_back();
     DevNode4 r;
     std::memset(&r, 0, sizeof(r));
+    // the node's children, then — while the record has room — the internal
+    // entry of the largest surface area opened into its two children (a
+    // node whose child is a leaf still fills four entries)
     int ents[4], ne = 0;
-    for (const int c : {i + 1, nodes[i].right}) {
-      if (nodes[c].count == 0) {
-        ents[ne++] = c + 1;
-        ents[ne++] = nodes[c].right;
-      } else {
-        ents[ne++] = c;
+    ents[ne++] = i + 1;
+    ents[ne++] = nodes[i].right;
+    while (ne < 4) {
+      int best = -1;
+      double bsa = -1.0;
+      for (int k = 0; k < ne; ++k) {
+        const RtxNode& c = nodes[ents[k]];
+        if (c.count != 0) continue;
+        const double x = c.bmax[0] - c.bmin[0], y = c.bmax[1] - c.bmin[1], z = c.bmax[2] - c.bmin[2];
+        const double sa = x * y + y * z + z * x;
+        if (sa > bsa) {
+          bsa = sa;
+          best = k;
+        }
       }
+      if (best < 0) break;
+      const int e = ents[best];
+      ents[best] = e + 1;
+      ents[ne++] = nodes[e].right;
     }
     r.count = ne;
     for (int k = ne; k < 4; ++k) {  // unused entries: empty boxes, never visited (k >= count)
