@@ -544,14 +544,18 @@ __device__ dvec3 box_normal(const DevScene& S, const RtxMaterial& m, int bestInd
 // denominators; the barycentrics are computed for the winner only.
 // tcap: callers pass a bound past which the hit cannot matter (see
 // traverse); rejecting there only skips work, never changes a result.
-RT_HD bool tri_hit(const RtxFace& F, const dvec3& p, const dvec3& d, double tcap,
-                                        double& tOut) {
-  // the face whole before the plane test (its vertices used to be loaded
-  // after it: a second dependent round trip per face)
-  const dvec3 n = ld3(F.n);
-  const dvec3 v0 = ld3(F.v0), v1 = ld3(F.v1), v2 = ld3(F.v2);
-  pin(n.x), pin(n.y), pin(n.z), pin(v0.x), pin(v0.y), pin(v0.z);
-  pin(v1.x), pin(v1.y), pin(v1.z), pin(v2.x), pin(v2.y), pin(v2.z);
+// One face's plane and vertices in registers (the leaf loop loads the next
+// face's while it tests this one).
+struct FaceV {
+  dvec3 n, v0, v1, v2;
+};
+RT_HD FaceV face_ld(const RtxFace& F) { return FaceV{ld3(F.n), ld3(F.v0), ld3(F.v1), ld3(F.v2)}; }
+RT_HD void face_pin(const FaceV& q) {
+  pin(q.n.x), pin(q.n.y), pin(q.n.z), pin(q.v0.x), pin(q.v0.y), pin(q.v0.z);
+  pin(q.v1.x), pin(q.v1.y), pin(q.v1.z), pin(q.v2.x), pin(q.v2.y), pin(q.v2.z);
+}
+RT_HD bool tri_test(const FaceV& q, const dvec3& p, const dvec3& d, double tcap, double& tOut) {
+  const dvec3 n = q.n, v0 = q.v0, v1 = q.v1, v2 = q.v2;
   double t = rtm::dot(n, d);
   if (t < RTX_EPS32 && t > -RTX_EPS32) return false;
   t = rtm::dot(v0 - p, n) / t;
@@ -564,6 +568,14 @@ RT_HD bool tri_hit(const RtxFace& F, const dvec3& p, const dvec3& d, double tcap
   if (faceArea < RTX_EPS32 && faceArea > -RTX_EPS32) return false;
   tOut = t;
   return true;
+}
+RT_HD bool tri_hit(const RtxFace& F, const dvec3& p, const dvec3& d, double tcap,
+                                        double& tOut) {
+  // the face whole before the plane test (its vertices used to be loaded
+  // after it: a second dependent round trip per face)
+  const FaceV q = face_ld(F);
+  face_pin(q);
+  return tri_test(q, p, d, tcap, tOut);
 }
 
 RT_HD dvec3 tri_bary(const RtxFace& F, const dvec3& p, const dvec3& d, double t) {

@@ -580,16 +580,24 @@ RT_HD bool trav_step(TR& T, const DevScene& S, const STK& stk, Counters& C) {
     const int f0 = code >> 2, f1 = f0 + (code & 3);
     // a face whose plane hit lies beyond this bound cannot win (closest:
     // strictly farther than the mesh's best; next: farther than the
-    // current best key) — tri_hit stops before the edge tests
+    // current best key) — tri_test stops before the edge tests
     const double tcap = closest && T.mhave ? rtm::gmin(whi, T.mbest) : whi;
     const dvec3 lp = T.cold.getLP(), ld = T.cold.getLD();
+    // the next face's loads go out before this face's tests: one round trip
+    // per leaf entry instead of one per face
+    FaceV qn = face_ld(S.tfaces[T.mfoff + f0]);
+    TMeta mn = S.tmeta[T.mfoff + f0];
     for (int f = f0; f < f1; ++f) {
       if (STATS) C.tris++;
       double tf;
-      // the face's reference rank (ties, answer) and leaf, issued before the
-      // face's own loads so they arrive in the same burst
-      const TMeta meta = S.tmeta[T.mfoff + f];
-      const bool hit = tri_hit(S.tfaces[T.mfoff + f], lp, ld, tcap, tf);
+      const FaceV q = qn;
+      const TMeta meta = mn;
+      if (f + 1 < f1) {
+        qn = face_ld(S.tfaces[T.mfoff + f + 1]);
+        mn = S.tmeta[T.mfoff + f + 1];
+      }
+      face_pin(q);
+      const bool hit = tri_test(q, lp, ld, tcap, tf);
       pin(meta.rank);
       pin(meta.leaf);
       if (hit) {
